@@ -1,0 +1,178 @@
+/*
+ * lsmgpu.h — C ABI of the MI355X-native SST block codec (drop-in for the
+ * fjall-rs/lsm-tree 3.1.9 block build/read API; see INTEGRATION.md for the
+ * Rust `extern "C"` binding a maintainer would add).
+ *
+ * All entry points are batched: one call encodes or decodes many blocks in HBM.
+ * Pointers named d_* are DEVICE pointers (hipMalloc'd, or torch CUDA tensors);
+ * structs are passed by host pointer and hold device pointers.  `stream` is a
+ * hipStream_t (NULL = default stream).  Every call is asynchronous on `stream`
+ * and returns LSM_OK once the work is enqueued, or an argument error.
+ * Per-block outcomes are written to d_status[] (lsm_status codes) on device.
+ *
+ * Reference interfaces replaced (paths relative to the reference repo):
+ *   lsm_encode_blocks  <- DataBlock::encode_into   src/table/data_block/mod.rs:523-549
+ *                         IndexBlock::encode_into  src/table/index_block/mod.rs:110-127
+ *                         Block::write_into        src/table/block/mod.rs:45-84
+ *                         (per-block loop of Writer::spill_block, src/table/writer/mod.rs:303-337)
+ *   lsm_decode_blocks  <- Block::from_file         src/table/block/mod.rs:131-182
+ *                         Block::from_reader       src/table/block/mod.rs:87-128
+ *                         load_block type check    src/table/util.rs:79-86
+ *                         DataBlock::iter/Decoder  src/table/data_block/mod.rs:476, block/decoder.rs:442-483
+ *                         IndexBlock::iter         src/table/index_block/mod.rs:91-95
+ *   lsm_cut_blocks     <- Writer::write chunking   src/table/writer/mod.rs:243-296
+ *   lsm_xxh3_128_batch <- hash128                  src/hash.rs:7-9 (checksum of arbitrary byte ranges)
+ */
+#ifndef LSMGPU_H
+#define LSMGPU_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define LSM_ABI_VERSION 1
+#define LSM_HEADER_LEN 33  /* Header::serialized_len(), header.rs:64-76 */
+#define LSM_TRAILER_LEN 31 /* TRAILER_SIZE, trailer.rs:14-23 */
+/* d_blocks must be 16-byte aligned and readable for LSM_INPUT_PADDING bytes
+ * past the last block (vector loads stage whole 16-byte granules). */
+#define LSM_INPUT_PADDING 64
+
+/* Per-block status.  Values mirror crate::Error (src/error.rs:134-167). */
+typedef enum lsm_status {
+    LSM_OK = 0,
+    LSM_BAD_MAGIC = 1,     /* Error::InvalidHeader("Block")           header.rs:125-127 */
+    LSM_BAD_TYPE = 2,      /* Error::InvalidTag(("BlockType", v))     type.rs:33 */
+    LSM_HDR_CKSUM = 3,     /* Error::ChecksumMismatch (header)        header.rs:156-161 */
+    LSM_CKSUM = 4,         /* Error::ChecksumMismatch (payload)       block/mod.rs:141-149 */
+    LSM_PARSE = 5,         /* malformed payload: the reference panics (lib.rs:62-66) */
+    LSM_OVERFLOW = 6,      /* output capacity exceeded */
+    LSM_TYPE_MISMATCH = 7, /* Error::InvalidTag, block type != expected (util.rs:81-86) */
+    LSM_TRUNCATED = 8,     /* handle shorter than header / data_length mismatch (Error::Io) */
+    LSM_UNSUPPORTED = 9,   /* compression != None, filter block parse */
+    LSM_BAD_ARG = 10,
+    LSM_HIP_ERROR = 11
+} lsm_status;
+
+/* BlockType codes, src/table/block/type.rs:13-22 */
+enum { LSM_BLOCK_DATA = 0, LSM_BLOCK_INDEX = 1, LSM_BLOCK_FILTER = 2, LSM_BLOCK_META = 3 };
+/* ValueType codes, src/value_type.rs:36-58 */
+enum { LSM_VALUE = 0, LSM_TOMBSTONE = 1, LSM_WEAK_TOMBSTONE = 2, LSM_INDIRECTION = 4 };
+
+/* Encode input: the items of all blocks, in key order, as SoA arenas.
+ * Item i: key = keys[key_off[i] .. key_off[i+1]), value likewise.
+ * Data/meta blocks use keys, vals, seqno, vtype (InternalValue, value.rs:85-153).
+ * Index blocks use keys (= end_key), seqno, handle_off, handle_size
+ * (KeyedBlockHandle, index_block/block_handle.rs:67-80). */
+typedef struct lsm_items {
+    const uint8_t* keys;
+    const uint64_t* key_off;     /* [n_items + 1] */
+    const uint8_t* vals;
+    const uint64_t* val_off;     /* [n_items + 1] */
+    const uint64_t* seqno;       /* [n_items] */
+    const uint8_t* vtype;        /* [n_items] ValueType code */
+    const uint64_t* handle_off;  /* [n_items] index blocks only, else NULL */
+    const uint32_t* handle_size; /* [n_items] index blocks only, else NULL */
+    uint64_t n_items;
+} lsm_items;
+
+/* Decode output (mirrors DataBlockParsedItem / IndexBlockParsedItem,
+ * data_block/mod.rs:272-316, index_block/mod.rs:24-62): payload-relative
+ * SliceIndexes into each block's data (util.rs:26).  Item k of block b is
+ * k in [item_start[b], item_start[b+1]).  NULL fields are not written.
+ *   key     = payload[key_off .. key_off + key_len]  (suffix when truncated)
+ *   prefix  = payload[head.key_off .. + prefix_len], head = first item of the
+ *             restart interval (materialize: Slice::fused(prefix, key))
+ *   value   = payload[val_off .. val_off + val_len]  (val_len 0 for tombstones)
+ * Index blocks: vtype = 0, prefix_len = 0, val_len = BlockHandle size,
+ *   handle_off = BlockHandle offset, val_off = end of the end_key. */
+typedef struct lsm_parsed_items {
+    uint64_t* seqno;
+    uint32_t* key_off;
+    uint32_t* val_off;
+    uint32_t* val_len;
+    uint16_t* key_len;
+    uint16_t* prefix_len;
+    uint8_t* vtype;
+    uint64_t* handle_off;
+} lsm_parsed_items;
+
+typedef struct lsm_block_params {
+    uint8_t restart_interval; /* data_block_restart_interval (config default 16); forced 1 for index */
+    uint8_t block_type;       /* LSM_BLOCK_DATA / LSM_BLOCK_INDEX / LSM_BLOCK_META */
+    uint8_t compression;      /* 0 = CompressionType::None (the only supported value) */
+    uint8_t reserved;
+    float hash_ratio;         /* data_block_hash_ratio (default 0.0) */
+} lsm_block_params;
+
+/* Tuning knobs for the decode kernel (0 = library default). */
+typedef struct lsm_decode_tuning {
+    uint32_t blocks_per_wave;  /* consecutive blocks one wave owns */
+    uint32_t stage_bytes;      /* LDS bytes per wave for staged block bytes */
+    uint32_t tile_items;       /* LDS output tile capacity in items */
+    uint32_t flags;            /* LSM_DECODE_ITEM_START_VALID: d_item_start already holds the
+                                  prefix sum of this batch (skip the count + scan pass) */
+} lsm_decode_tuning;
+#define LSM_DECODE_ITEM_START_VALID 1u
+
+int lsm_abi_version(void);
+const char* lsm_status_name(int status);
+/* Last HIP error string of this thread (after LSM_HIP_ERROR). */
+const char* lsm_last_error(void);
+int lsm_device_count(void);
+int lsm_set_device(int device);
+
+/* ---- decode ---------------------------------------------------------------
+ * Verifies and parses n_blocks on-disk blocks (header || payload) located at
+ * d_blocks[d_block_off[b] .. d_block_off[b+1]) (d_block_off: n_blocks+1
+ * device u64, the BlockHandle offsets/sizes).  expect_type: block type every
+ * block must have (util.rs:81-86), or -1 for any.  Writes d_item_start
+ * (n_blocks+1 u32: prefix sum of the trailers' item counts, clamped at
+ * item_cap), the parsed items, and d_status[n_blocks].
+ * d_workspace: lsm_decode_workspace_size(n_blocks) bytes of device memory. */
+size_t lsm_decode_workspace_size(uint32_t n_blocks);
+int lsm_decode_blocks(const uint8_t* d_blocks, const uint64_t* d_block_off, uint32_t n_blocks,
+                      int32_t expect_type, const lsm_parsed_items* d_out, uint64_t item_cap,
+                      uint32_t* d_item_start, int32_t* d_status, void* d_workspace,
+                      size_t workspace_bytes, void* stream);
+int lsm_decode_blocks_tuned(const uint8_t* d_blocks, const uint64_t* d_block_off, uint32_t n_blocks,
+                            int32_t expect_type, const lsm_parsed_items* d_out, uint64_t item_cap,
+                            uint32_t* d_item_start, int32_t* d_status, void* d_workspace,
+                            size_t workspace_bytes, const lsm_decode_tuning* tuning, void* stream);
+
+/* ---- encode ---------------------------------------------------------------
+ * Encodes n_blocks blocks; block b holds items [d_block_item_start[b],
+ * d_block_item_start[b+1]) (n_blocks+1 device u32; every block non-empty,
+ * mod.rs:530).  Output blocks (header || payload) are packed back to back
+ * into d_out; d_block_off (n_blocks+1 device u64) receives their offsets.
+ * d_out needs lsm_encode_bound(...) bytes (status LSM_OVERFLOW otherwise).
+ * d_workspace: lsm_encode_workspace_size(n_items, n_blocks) bytes. */
+uint64_t lsm_encode_bound(uint64_t n_items, uint32_t n_blocks, uint64_t key_bytes, uint64_t val_bytes,
+                          const lsm_block_params* params);
+size_t lsm_encode_workspace_size(uint64_t n_items, uint32_t n_blocks);
+int lsm_encode_blocks(const lsm_items* d_items, const uint32_t* d_block_item_start, uint32_t n_blocks,
+                      const lsm_block_params* params, uint8_t* d_out, uint64_t out_cap,
+                      uint64_t* d_block_off, int32_t* d_status, void* d_workspace,
+                      size_t workspace_bytes, void* stream);
+
+/* ---- host-side helpers (no device work) ------------------------------------
+ * Writer chunking on HOST arrays: cut a block when the running
+ * sum(key_len + value_len) >= block_size (writer/mod.rs:284-290), the last
+ * partial chunk is flushed as its own block (writer/mod.rs:374).  key_off and
+ * val_off are host [n_items+1] arrays.  Writes block_item_start
+ * (cap_blocks+1 entries) and returns the number of blocks. */
+uint64_t lsm_cut_blocks(const uint64_t* key_off, const uint64_t* val_off, uint64_t n_items,
+                        uint32_t block_size, uint32_t* block_item_start, uint64_t cap_blocks);
+
+/* ---- checksums --------------------------------------------------------------
+ * xxh3_128 (hash128, src/hash.rs:7-9) of n byte ranges
+ * d_data[d_off[i] .. d_off[i+1]) into d_out (2 u64 per range: low, high). */
+int lsm_xxh3_128_batch(const uint8_t* d_data, const uint64_t* d_off, uint32_t n, uint64_t* d_out,
+                       void* stream);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* LSMGPU_H */

@@ -1,0 +1,34 @@
+// decode.hpp — host-side launch interface of the decode kernels.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "lsmgpu.h"
+
+namespace lsmgpu {
+
+struct DecodeParams {
+  const uint8_t* blocks;
+  const uint64_t* block_off;
+  uint32_t n_blocks;
+  int32_t expect_type;
+  lsm_parsed_items out;
+  uint64_t item_cap;
+  const uint32_t* item_start;  // read by the decode kernel
+  uint32_t* item_start_w;      // written by the count/scan pass (same buffer)
+  int32_t* status;
+  uint32_t blocks_per_wave;
+  uint32_t stage_bytes;
+  uint32_t tile_items;
+  uint32_t flags;
+};
+
+size_t decode_workspace_size(uint32_t n_blocks);
+uint32_t decode_lds_bytes(uint32_t stage_bytes, uint32_t tile_items);
+hipError_t launch_decode(const DecodeParams& P, void* workspace, hipStream_t st);
+
+hipError_t launch_xxh3_128_batch(const uint8_t* data, const uint64_t* off, uint32_t n, uint64_t* out,
+                                 hipStream_t st);
+
+}  // namespace lsmgpu

@@ -1,0 +1,518 @@
+// device_common.hpp — gfx950 device building blocks for the SST block codec.
+//
+// * XXH3-64 / XXH3-128 (seed 0, default secret): the per-lane short paths
+//   (<= 240 B, used for the 29-byte header checksum, hash-index keys and tiny
+//   payloads) and a WAVE-COOPERATIVE long path (> 240 B) for block payloads:
+//   one 64-lane wave covers one 1 KiB XXH3 block per step (lane l owns bytes
+//   [16l, 16l+16) = stripe l>>2, accumulator pair 2(l&3), 2(l&3)+1), the 16
+//   stripe contributions are summed with a 4-step xor butterfly and every
+//   lane applies the per-KiB scramble to its own accumulator pair.
+//   Reference call sites: src/hash.rs:2-9, src/table/block/mod.rs:70,94,141,
+//   src/table/block/header.rs:83-109, hash_index/mod.rs:35-41.
+// * LEB128 (varint-rs) decoding from a 16-byte register window.
+// * Unaligned 16-byte windows over LDS or global bytes (aligned dword reads +
+//   v_alignbyte_b32), wave scans.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace lsmgpu {
+
+constexpr int kWave = 64;
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+constexpr uint32_t kHdrLen = 33;
+constexpr uint32_t kTrailerLen = 31;
+constexpr uint8_t kTrailerMarker = 0xFF;
+constexpr uint8_t kHashFree = 254;
+constexpr uint8_t kHashConflict = 255;
+constexpr uint32_t kHashMaxPointers = 254;
+
+enum : int32_t {
+  ST_OK = 0, ST_BAD_MAGIC = 1, ST_BAD_TYPE = 2, ST_HDR_CKSUM = 3, ST_CKSUM = 4, ST_PARSE = 5,
+  ST_OVERFLOW = 6, ST_TYPE_MISMATCH = 7, ST_TRUNCATED = 8, ST_UNSUPPORTED = 9, ST_BAD_ARG = 10
+};
+
+// ---------------------------------------------------------------- XXH3 consts
+constexpr uint32_t P32_1 = 0x9E3779B1U, P32_2 = 0x85EBCA77U, P32_3 = 0xC2B2AE3DU;
+constexpr uint64_t P64_1 = 0x9E3779B185EBCA87ULL, P64_2 = 0xC2B2AE3D27D4EB4FULL,
+                   P64_3 = 0x165667B19E3779F9ULL, P64_4 = 0x85EBCA77C2B2AE63ULL,
+                   P64_5 = 0x27D4EB2F165667C5ULL, PMX1 = 0x165667919E3779F9ULL,
+                   PMX2 = 0x9FB21C651E98DF25ULL;
+
+// The default 192-byte XXH3 secret as little-endian u64 at every byte offset
+// the algorithm reads is obtained from this table with constant offsets only,
+// so the compiler folds them into immediates.
+struct Secret {
+  static constexpr uint8_t b[192] = {
+      0xb8, 0xfe, 0x6c, 0x39, 0x23, 0xa4, 0x4b, 0xbe, 0x7c, 0x01, 0x81, 0x2c, 0xf7, 0x21, 0xad, 0x1c,
+      0xde, 0xd4, 0x6d, 0xe9, 0x83, 0x90, 0x97, 0xdb, 0x72, 0x40, 0xa4, 0xa4, 0xb7, 0xb3, 0x67, 0x1f,
+      0xcb, 0x79, 0xe6, 0x4e, 0xcc, 0xc0, 0xe5, 0x78, 0x82, 0x5a, 0xd0, 0x7d, 0xcc, 0xff, 0x72, 0x21,
+      0xb8, 0x08, 0x46, 0x74, 0xf7, 0x43, 0x24, 0x8e, 0xe0, 0x35, 0x90, 0xe6, 0x81, 0x3a, 0x26, 0x4c,
+      0x3c, 0x28, 0x52, 0xbb, 0x91, 0xc3, 0x00, 0xcb, 0x88, 0xd0, 0x65, 0x8b, 0x1b, 0x53, 0x2e, 0xa3,
+      0x71, 0x64, 0x48, 0x97, 0xa2, 0x0d, 0xf9, 0x4e, 0x38, 0x19, 0xef, 0x46, 0xa9, 0xde, 0xac, 0xd8,
+      0xa8, 0xfa, 0x76, 0x3f, 0xe3, 0x9c, 0x34, 0x3f, 0xf9, 0xdc, 0xbb, 0xc7, 0xc7, 0x0b, 0x4f, 0x1d,
+      0x8a, 0x51, 0xe0, 0x4b, 0xcd, 0xb4, 0x59, 0x31, 0xc8, 0x9f, 0x7e, 0xc9, 0xd9, 0x78, 0x73, 0x64,
+      0xea, 0xc5, 0xac, 0x83, 0x34, 0xd3, 0xeb, 0xc3, 0xc5, 0x81, 0xa0, 0xff, 0xfa, 0x13, 0x63, 0xeb,
+      0x17, 0x0d, 0xdd, 0x51, 0xb7, 0xf0, 0xda, 0x49, 0xd3, 0x16, 0x55, 0x26, 0x29, 0xd4, 0x68, 0x9e,
+      0x2b, 0x16, 0xbe, 0x58, 0x7d, 0x47, 0xa1, 0xfc, 0x8f, 0xf8, 0xb8, 0xd1, 0x7a, 0xd0, 0x31, 0xce,
+      0x45, 0xcb, 0x3a, 0x8f, 0x95, 0x16, 0x04, 0x28, 0xaf, 0xd7, 0xfb, 0xca, 0xbb, 0x4b, 0x40, 0x7e,
+  };
+  static constexpr uint64_t u64(int o) {
+    return (uint64_t)b[o] | ((uint64_t)b[o + 1] << 8) | ((uint64_t)b[o + 2] << 16) |
+           ((uint64_t)b[o + 3] << 24) | ((uint64_t)b[o + 4] << 32) | ((uint64_t)b[o + 5] << 40) |
+           ((uint64_t)b[o + 6] << 48) | ((uint64_t)b[o + 7] << 56);
+  }
+  static constexpr uint32_t u32(int o) {
+    return (uint32_t)b[o] | ((uint32_t)b[o + 1] << 8) | ((uint32_t)b[o + 2] << 16) |
+           ((uint32_t)b[o + 3] << 24);
+  }
+};
+
+// Secret words for the wave long path (runtime-indexed -> constant memory).
+struct LongSecret {
+  uint64_t acc[24];   // u64 at byte 8j, j = 0..23 (stripe keys: stripe s, acc i -> acc[s+i])
+  uint64_t last[8];   // u64 at byte 121 + 8i (last stripe, XXH_SECRET_LASTACC_START = 7)
+  uint64_t mlo[8];    // u64 at byte 11 + 8i  (mergeAccs low)
+  uint64_t mhi[8];    // u64 at byte 117 + 8i (mergeAccs high)
+};
+constexpr LongSecret make_long_secret() {
+  LongSecret ls{};
+  for (int j = 0; j < 24; ++j) ls.acc[j] = Secret::u64(8 * j);
+  for (int i = 0; i < 8; ++i) {
+    ls.last[i] = Secret::u64(121 + 8 * i);
+    ls.mlo[i] = Secret::u64(11 + 8 * i);
+    ls.mhi[i] = Secret::u64(117 + 8 * i);
+  }
+  return ls;
+}
+// One copy per translation unit (no -fgpu-rdc).
+static __constant__ LongSecret kLongSecret = make_long_secret();
+
+__device__ __forceinline__ uint64_t mul_fold64(uint64_t a, uint64_t b) {
+  return (a * b) ^ __umul64hi(a, b);
+}
+__device__ __forceinline__ uint64_t xxh64_avalanche(uint64_t h) {
+  h ^= h >> 33; h *= P64_2; h ^= h >> 29; h *= P64_3; h ^= h >> 32;
+  return h;
+}
+__device__ __forceinline__ uint64_t xxh3_avalanche(uint64_t h) {
+  h ^= h >> 37; h *= PMX1; h ^= h >> 32;
+  return h;
+}
+__device__ __forceinline__ uint64_t rotl64(uint64_t x, int r) { return (x << r) | (x >> (64 - r)); }
+__device__ __forceinline__ uint32_t rotl32(uint32_t x, int r) { return (x << r) | (x >> (32 - r)); }
+__device__ __forceinline__ uint32_t bswap32(uint32_t x) { return __builtin_bswap32(x); }
+__device__ __forceinline__ uint64_t bswap64(uint64_t x) { return __builtin_bswap64(x); }
+
+// ------------------------------------------------- byte access (LDS / global)
+// `base` is 16-byte aligned (an LDS image base or a global span base); all
+// reads are aligned dwords, unaligned views are assembled with v_alignbyte.
+__device__ __forceinline__ uint32_t ld32(const uint8_t* base, uint32_t aligned_off) {
+  return *reinterpret_cast<const uint32_t*>(base + aligned_off);
+}
+__device__ __forceinline__ uint32_t alignbyte(uint32_t hi, uint32_t lo, uint32_t shift) {
+  return __builtin_amdgcn_alignbyte(hi, lo, shift);
+}
+__device__ __forceinline__ uint8_t ld8(const uint8_t* base, uint32_t off) { return base[off]; }
+
+struct Win16 {
+  uint64_t lo, hi;
+};
+// 16 bytes at base[pos..pos+16) (reads up to 4 bytes past pos+16).
+__device__ __forceinline__ Win16 read_win16(const uint8_t* base, uint32_t pos) {
+  const uint32_t a = pos & ~3u, s = pos & 3u;
+  uint32_t d0 = ld32(base, a), d1 = ld32(base, a + 4), d2 = ld32(base, a + 8),
+           d3 = ld32(base, a + 12), d4 = ld32(base, a + 16);
+  uint32_t e0 = alignbyte(d1, d0, s), e1 = alignbyte(d2, d1, s), e2 = alignbyte(d3, d2, s),
+           e3 = alignbyte(d4, d3, s);
+  return {(uint64_t)e0 | ((uint64_t)e1 << 32), (uint64_t)e2 | ((uint64_t)e3 << 32)};
+}
+__device__ __forceinline__ uint32_t read_u32_unaligned(const uint8_t* base, uint32_t pos) {
+  const uint32_t a = pos & ~3u, s = pos & 3u;
+  return alignbyte(ld32(base, a + 4), ld32(base, a), s);
+}
+__device__ __forceinline__ uint16_t read_u16_unaligned(const uint8_t* base, uint32_t pos) {
+  return (uint16_t)(read_u32_unaligned(base, pos) & 0xFFFF);
+}
+
+// Drop the low n bytes (0 <= n <= 16) of a 128-bit window.
+__device__ __forceinline__ void win_shift(Win16& w, uint32_t n) {
+  if (n >= 16) {
+    w.lo = w.hi = 0;
+    return;
+  }
+  if (n >= 8) {
+    w.lo = w.hi;
+    w.hi = 0;
+    n -= 8;
+  }
+  if (n) {
+    w.lo = (w.lo >> (8 * n)) | (w.hi << (64 - 8 * n));
+    w.hi >>= 8 * n;
+  }
+}
+
+// LEB128 (varint-rs VarintReader) from the low bytes of a window.
+// Returns the byte length (1..max_bytes) or 0 if the varint does not
+// terminate within min(max_bytes, avail) bytes.  Value is truncated to the
+// type width by the caller's mask (`as $type` in varint-rs).
+__device__ __forceinline__ uint32_t leb_decode(const Win16& w, uint32_t max_bytes, uint32_t avail,
+                                                uint64_t& v) {
+  const uint64_t msb = 0x8080808080808080ULL;
+  uint64_t stop = ~w.lo & msb;
+  uint32_t n;
+  if (stop) {
+    n = (uint32_t)(__builtin_ctzll(stop) >> 3) + 1;  // 1..8
+  } else {
+    uint64_t stop2 = ~w.hi & 0x8080ULL;              // bytes 9, 10
+    n = stop2 ? 9 + (uint32_t)(__builtin_ctzll(stop2) >> 3) : 99;
+  }
+  if (n > max_bytes || n > avail) return 0;
+  uint64_t x = w.lo;
+  if (n < 8) x &= (1ULL << (8 * n)) - 1;
+  // compact 7-bit groups: 8 x 7 -> 56 bits
+  x = ((x & 0x7F007F007F007F00ULL) >> 1) | (x & 0x007F007F007F007FULL);
+  x = ((x & 0x3FFF00003FFF0000ULL) >> 2) | (x & 0x00003FFF00003FFFULL);
+  x = ((x & 0x0FFFFFFF00000000ULL) >> 4) | (x & 0x000000000FFFFFFFULL);
+  if (n > 8) {
+    x |= (w.hi & 0x7FULL) << 56;
+    if (n > 9) x |= (w.hi & 0x7F00ULL) << 55;  // bits 63..69 (only bit 63 survives)
+  }
+  v = x;
+  return n;
+}
+
+// ------------------------------------------------- XXH3 per-lane short paths
+// Input bytes come from a caller-supplied reader R: R(off) -> u64 at byte off
+// (unaligned little-endian), R8(off) -> byte.
+template <class R8, class R64>
+__device__ __forceinline__ void xxh3_128_short(uint32_t len, R8 rb, R64 r64, uint64_t& out_lo,
+                                               uint64_t& out_hi) {
+  using S = Secret;
+  if (len == 0) {
+    out_lo = xxh64_avalanche(S::u64(64) ^ S::u64(72));
+    out_hi = xxh64_avalanche(S::u64(80) ^ S::u64(88));
+    return;
+  }
+  if (len <= 3) {
+    uint32_t c1 = rb(0), c2 = rb(len >> 1), c3 = rb(len - 1);
+    uint32_t cl = (c1 << 16) | (c2 << 24) | c3 | (len << 8);
+    uint32_t ch = rotl32(bswap32(cl), 13);
+    out_lo = xxh64_avalanche((uint64_t)cl ^ (uint64_t)(S::u32(0) ^ S::u32(4)));
+    out_hi = xxh64_avalanche((uint64_t)ch ^ (uint64_t)(S::u32(8) ^ S::u32(12)));
+    return;
+  }
+  if (len <= 8) {
+    uint32_t in_lo = (uint32_t)r64(0), in_hi = (uint32_t)r64(len - 4);
+    uint64_t keyed = (in_lo + ((uint64_t)in_hi << 32)) ^ (S::u64(16) ^ S::u64(24));
+    uint64_t m = P64_1 + ((uint64_t)len << 2);
+    uint64_t lo = keyed * m, hi = __umul64hi(keyed, m);
+    hi += lo << 1;
+    lo ^= hi >> 3;
+    lo ^= lo >> 35;
+    lo *= PMX2;
+    lo ^= lo >> 28;
+    out_lo = lo;
+    out_hi = xxh3_avalanche(hi);
+    return;
+  }
+  if (len <= 16) {
+    uint64_t in_lo = r64(0), in_hi = r64(len - 8);
+    uint64_t k = in_lo ^ in_hi ^ (S::u64(32) ^ S::u64(40));
+    uint64_t mlo = k * P64_1, mhi = __umul64hi(k, P64_1);
+    mlo += (uint64_t)(len - 1) << 54;
+    in_hi ^= S::u64(48) ^ S::u64(56);
+    mhi += in_hi + (uint64_t)(uint32_t)in_hi * (uint64_t)(P32_2 - 1);
+    mlo ^= bswap64(mhi);
+    uint64_t hlo = mlo * P64_2, hhi = __umul64hi(mlo, P64_2);
+    hhi += mhi * P64_2;
+    out_lo = xxh3_avalanche(hlo);
+    out_hi = xxh3_avalanche(hhi);
+    return;
+  }
+  auto mix16 = [&](uint32_t io, int so, uint64_t seed) {
+    return mul_fold64(r64(io) ^ (S::u64(so) + seed), r64(io + 8) ^ (S::u64(so + 8) - seed));
+  };
+  uint64_t alo = (uint64_t)len * P64_1, ahi = 0;
+  auto mix32 = [&](uint32_t i1, uint32_t i2, int so, uint64_t seed) {
+    alo += mix16(i1, so, seed);
+    alo ^= r64(i2) + r64(i2 + 8);
+    ahi += mix16(i2, so + 16, seed);
+    ahi ^= r64(i1) + r64(i1 + 8);
+  };
+  if (len <= 128) {
+    if (len > 32) {
+      if (len > 64) {
+        if (len > 96) mix32(48, len - 64, 96, 0);
+        mix32(32, len - 48, 64, 0);
+      }
+      mix32(16, len - 32, 32, 0);
+    }
+    mix32(0, len - 16, 0, 0);
+  } else {  // 129..240
+#pragma unroll
+    for (int i = 32; i < 160; i += 32) mix32(i - 32, i - 16, i - 32, 0);
+    alo = xxh3_avalanche(alo);
+    ahi = xxh3_avalanche(ahi);
+#pragma unroll
+    for (int i = 160; i <= 240; i += 32)
+      if ((uint32_t)i <= len) mix32(i - 32, i - 16, 3 + i - 160, 0);
+    mix32(len - 16, len - 32, 136 - 17 - 16, 0);
+  }
+  uint64_t hlo = alo + ahi;
+  uint64_t hhi = alo * P64_1 + ahi * P64_4 + (uint64_t)len * P64_2;
+  out_lo = xxh3_avalanche(hlo);
+  out_hi = 0 - xxh3_avalanche(hhi);
+}
+
+template <class R8, class R64>
+__device__ __forceinline__ uint64_t xxh3_64_short(uint32_t len, R8 rb, R64 r64) {
+  using S = Secret;
+  if (len == 0) return xxh64_avalanche(S::u64(56) ^ S::u64(64));
+  if (len <= 3) {
+    uint32_t c1 = rb(0), c2 = rb(len >> 1), c3 = rb(len - 1);
+    uint32_t combined = (c1 << 16) | (c2 << 24) | c3 | (len << 8);
+    return xxh64_avalanche((uint64_t)combined ^ (uint64_t)(S::u32(0) ^ S::u32(4)));
+  }
+  if (len <= 8) {
+    uint32_t in1 = (uint32_t)r64(0), in2 = (uint32_t)r64(len - 4);
+    uint64_t h = (in2 + ((uint64_t)in1 << 32)) ^ (S::u64(8) ^ S::u64(16));
+    h ^= rotl64(h, 49) ^ rotl64(h, 24);
+    h *= PMX2;
+    h ^= (h >> 35) + len;
+    h *= PMX2;
+    return h ^ (h >> 28);
+  }
+  if (len <= 16) {
+    uint64_t lo = r64(0) ^ (S::u64(24) ^ S::u64(32));
+    uint64_t hi = r64(len - 8) ^ (S::u64(40) ^ S::u64(48));
+    uint64_t acc = len + bswap64(lo) + hi + mul_fold64(lo, hi);
+    return xxh3_avalanche(acc);
+  }
+  auto mix16 = [&](uint32_t io, int so) {
+    return mul_fold64(r64(io) ^ S::u64(so), r64(io + 8) ^ S::u64(so + 8));
+  };
+  uint64_t acc = (uint64_t)len * P64_1;
+  if (len <= 128) {
+    if (len > 32) {
+      if (len > 64) {
+        if (len > 96) {
+          acc += mix16(48, 96);
+          acc += mix16(len - 64, 112);
+        }
+        acc += mix16(32, 64);
+        acc += mix16(len - 48, 80);
+      }
+      acc += mix16(16, 32);
+      acc += mix16(len - 32, 48);
+    }
+    acc += mix16(0, 0);
+    acc += mix16(len - 16, 16);
+    return xxh3_avalanche(acc);
+  }
+  // 129..240
+#pragma unroll
+  for (int i = 0; i < 8; ++i) acc += mix16(16 * i, 16 * i);
+  acc = xxh3_avalanche(acc);
+  const uint32_t rounds = len / 16;
+#pragma unroll
+  for (int i = 8; i < 15; ++i)
+    if ((uint32_t)i < rounds) acc += mix16(16 * i, 16 * (i - 8) + 3);
+  acc += mix16(len - 16, 136 - 17);
+  return xxh3_avalanche(acc);
+}
+
+// Generic byte reader over a (possibly unaligned) byte pointer, for per-lane
+// hashing of keys in global memory (hash index) — byte loads, any alignment.
+struct PtrReader {
+  const uint8_t* p;
+  __device__ __forceinline__ uint32_t operator()(uint32_t o) const { return p[o]; }
+};
+struct PtrReader64 {
+  const uint8_t* p;
+  __device__ __forceinline__ uint64_t operator()(uint32_t o) const {
+    uint64_t v = 0;
+#pragma unroll
+    for (int i = 7; i >= 0; --i) v = (v << 8) | p[o + i];
+    return v;
+  }
+};
+
+
+// ------------------------------------------------- XXH3-128 wave long path
+// 16 bytes of the input at byte offset o (relative to the aligned base),
+// with input start alignment folded in: see read_win16.
+struct WaveHashState {
+  uint64_t a0, a1;  // accumulators 2(l&3), 2(l&3)+1 (every lane of a quad group holds them)
+};
+
+__device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int mask) {
+  uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+  lo = __shfl_xor((int)lo, mask);
+  hi = __shfl_xor((int)hi, mask);
+  return (uint64_t)lo | ((uint64_t)hi << 32);
+}
+
+// Contribution of one 16-byte chunk (lane's part of a stripe) to its pair.
+__device__ __forceinline__ void stripe_part(const Win16& w, uint64_t k0, uint64_t k1, uint64_t& c0,
+                                            uint64_t& c1) {
+  uint64_t x0 = w.lo ^ k0, x1 = w.hi ^ k1;
+  c0 += (uint64_t)(uint32_t)x0 * (x0 >> 32) + w.hi;  // acc[w0] += mul(k0) ; acc[w0] (=w1^1) += v1
+  c1 += (uint64_t)(uint32_t)x1 * (x1 >> 32) + w.lo;  // acc[w1] += mul(k1) ; acc[w1] (=w0^1) += v0
+}
+
+// XXH3-128 of base[pos .. pos+len), len > 240, computed by the whole wave
+// (all 64 lanes must call it with identical arguments).  `base` 16-aligned.
+__device__ __forceinline__ void xxh3_128_wave_long(const uint8_t* base, uint32_t pos, uint32_t len,
+                                                   const LongSecret* __restrict__ ls, uint64_t& out_lo,
+                                                   uint64_t& out_hi) {
+  const int lane = threadIdx.x & 63;
+  const int q = lane & 3;          // accumulator pair index
+  const int s = lane >> 2;         // stripe in block
+  const uint64_t k0 = ls->acc[s + 2 * q], k1 = ls->acc[s + 2 * q + 1];
+  // XXH3 initial accumulators {P32_3, P64_1, P64_2, P64_3, P64_4, P32_2, P64_5, P32_1}
+  uint64_t a0 = q == 0 ? (uint64_t)P32_3 : q == 1 ? P64_2 : q == 2 ? P64_4 : P64_5;
+  uint64_t a1 = q == 0 ? P64_1 : q == 1 ? P64_3 : q == 2 ? (uint64_t)P32_2 : (uint64_t)P32_1;
+  const uint64_t scr0 = ls->acc[16 + 2 * q], scr1 = ls->acc[16 + 2 * q + 1];  // secret + 128
+  const uint32_t nb_blocks = (len - 1) / 1024;
+  for (uint32_t n = 0; n < nb_blocks; ++n) {
+    Win16 w = read_win16(base, pos + n * 1024 + 16 * lane);
+    uint64_t c0 = 0, c1 = 0;
+    stripe_part(w, k0, k1, c0, c1);
+#pragma unroll
+    for (int m = 4; m < 64; m <<= 1) {
+      c0 += shfl_xor64(c0, m);
+      c1 += shfl_xor64(c1, m);
+    }
+    a0 += c0;
+    a1 += c1;
+    a0 ^= a0 >> 47; a0 ^= scr0; a0 *= P32_1;
+    a1 ^= a1 >> 47; a1 ^= scr1; a1 *= P32_1;
+  }
+  {
+    const uint32_t tail0 = nb_blocks * 1024;
+    const uint32_t nb_stripes = ((len - 1) - tail0) / 64;
+    uint64_t c0 = 0, c1 = 0;
+    if ((uint32_t)s < nb_stripes) {
+      Win16 w = read_win16(base, pos + tail0 + 16 * lane);
+      stripe_part(w, k0, k1, c0, c1);
+    }
+    if (lane < 4) {  // last stripe: input[len-64 .. len), secret + 121
+      Win16 w = read_win16(base, pos + len - 64 + 16 * lane);
+      stripe_part(w, ls->last[2 * q], ls->last[2 * q + 1], c0, c1);
+    }
+#pragma unroll
+    for (int m = 4; m < 64; m <<= 1) {
+      c0 += shfl_xor64(c0, m);
+      c1 += shfl_xor64(c1, m);
+    }
+    a0 += c0;
+    a1 += c1;
+  }
+  // mergeAccs: lane pair q holds acc[2q], acc[2q+1]
+  uint64_t tlo = mul_fold64(a0 ^ ls->mlo[2 * q], a1 ^ ls->mlo[2 * q + 1]);
+  uint64_t thi = mul_fold64(a0 ^ ls->mhi[2 * q], a1 ^ ls->mhi[2 * q + 1]);
+  tlo += shfl_xor64(tlo, 1);
+  thi += shfl_xor64(thi, 1);
+  tlo += shfl_xor64(tlo, 2);
+  thi += shfl_xor64(thi, 2);
+  out_lo = xxh3_avalanche((uint64_t)len * P64_1 + tlo);
+  out_hi = xxh3_avalanche(~((uint64_t)len * P64_2) + thi);
+}
+
+// Window-backed readers for the per-lane short path over an aligned base.
+struct BaseReader8 {
+  const uint8_t* base;
+  uint32_t pos;
+  __device__ __forceinline__ uint32_t operator()(uint32_t o) const { return base[pos + o]; }
+};
+struct BaseReader64 {
+  const uint8_t* base;
+  uint32_t pos;
+  __device__ __forceinline__ uint64_t operator()(uint32_t o) const {
+    const uint32_t p = pos + o, a = p & ~3u, s = p & 3u;
+    uint32_t d0 = ld32(base, a), d1 = ld32(base, a + 4), d2 = ld32(base, a + 8);
+    return (uint64_t)alignbyte(d1, d0, s) | ((uint64_t)alignbyte(d2, d1, s) << 32);
+  }
+};
+
+// XXH3-128 of base[pos..pos+len) for any len: long inputs use the whole wave
+// (wave-uniform len required), short inputs are computed by every lane
+// redundantly (results identical in all lanes).
+__device__ __forceinline__ void xxh3_128_wave(const uint8_t* base, uint32_t pos, uint32_t len,
+                                              const LongSecret* ls, uint64_t& lo, uint64_t& hi) {
+  if (len > 240) {
+    xxh3_128_wave_long(base, pos, len, ls, lo, hi);
+  } else {
+    xxh3_128_short(len, BaseReader8{base, pos}, BaseReader64{base, pos}, lo, hi);
+  }
+}
+
+// Per-lane XXH3-64 for inputs > 240 B (hash-index keys longer than 240 B;
+// rare).  Scalar restatement of hashLong + mergeAccs on one lane.
+template <class R64>
+__device__ __noinline__ uint64_t xxh3_64_long_lane(uint32_t len, R64 r64, const LongSecret* ls) {
+  uint64_t acc[8] = {P32_3, P64_1, P64_2, P64_3, P64_4, P32_2, P64_5, P32_1};
+  auto stripe = [&](uint32_t off, const uint64_t* key) {
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      const uint64_t v = r64(off + 8 * i);
+      const uint64_t x = v ^ key[i];
+      acc[i ^ 1] += v;
+      acc[i] += (uint64_t)(uint32_t)x * (x >> 32);
+    }
+  };
+  const uint32_t nb = (len - 1) / 1024;
+  for (uint32_t n = 0; n < nb; ++n) {
+    for (uint32_t s = 0; s < 16; ++s) stripe(n * 1024 + 64 * s, ls->acc + s);
+#pragma unroll
+    for (int i = 0; i < 8; ++i) {
+      uint64_t a = acc[i];
+      a ^= a >> 47;
+      a ^= ls->acc[16 + i];
+      acc[i] = a * P32_1;
+    }
+  }
+  const uint32_t ns = ((len - 1) - nb * 1024) / 64;
+  for (uint32_t s = 0; s < ns; ++s) stripe(nb * 1024 + 64 * s, ls->acc + s);
+  stripe(len - 64, ls->last);
+  uint64_t r = (uint64_t)len * P64_1;
+#pragma unroll
+  for (int i = 0; i < 4; ++i) r += mul_fold64(acc[2 * i] ^ ls->mlo[2 * i], acc[2 * i + 1] ^ ls->mlo[2 * i + 1]);
+  return xxh3_avalanche(r);
+}
+
+template <class R8, class R64>
+__device__ __forceinline__ uint64_t xxh3_64_any(uint32_t len, R8 rb, R64 r64) {
+  if (len > 240) return xxh3_64_long_lane(len, r64, &kLongSecret);
+  return xxh3_64_short(len, rb, r64);
+}
+
+// ------------------------------------------------------------ wave helpers
+__device__ __forceinline__ uint32_t wave_incl_scan_u32(uint32_t v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    uint32_t t = __shfl_up((int)v, d);
+    if (lane >= d) v += t;
+  }
+  return v;
+}
+__device__ __forceinline__ uint64_t wave_incl_scan_u64(uint64_t v) {
+  const int lane = threadIdx.x & 63;
+#pragma unroll
+  for (int d = 1; d < 64; d <<= 1) {
+    uint32_t lo = __shfl_up((int)(uint32_t)v, d), hi = __shfl_up((int)(uint32_t)(v >> 32), d);
+    uint64_t t = (uint64_t)lo | ((uint64_t)hi << 32);
+    if (lane >= d) v += t;
+  }
+  return v;
+}
+__device__ __forceinline__ uint32_t wave_bcast_u32(uint32_t v, int src) { return __shfl((int)v, src); }
+__device__ __forceinline__ uint64_t wave_bcast_u64(uint64_t v, int src) {
+  uint32_t lo = __shfl((int)(uint32_t)v, src), hi = __shfl((int)(uint32_t)(v >> 32), src);
+  return (uint64_t)lo | ((uint64_t)hi << 32);
+}
+
+}  // namespace lsmgpu

@@ -1,0 +1,98 @@
+// scan.hpp — device-wide exclusive prefix sum over u64 counts (block item
+// counts -> item_start, encoded block sizes -> block offsets).
+// Three small launches: per-tile reduce, scan of tile sums, per-tile scan.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+#include "device_common.hpp"
+
+namespace lsmgpu {
+
+constexpr int kScanThreads = 256;
+constexpr int kScanPerThread = 8;
+constexpr int kScanTile = kScanThreads * kScanPerThread;  // 2048
+
+__device__ __forceinline__ uint64_t block_excl_scan_u64(uint64_t v, uint64_t* sh /*[kScanThreads/64]*/,
+                                                        uint64_t& total) {
+  const int lane = threadIdx.x & 63, wid = threadIdx.x >> 6;
+  uint64_t incl = wave_incl_scan_u64(v);
+  if (lane == 63) sh[wid] = incl;
+  __syncthreads();
+  uint64_t wbase = 0, tot = 0;
+  for (int i = 0; i < kScanThreads / 64; ++i) {
+    uint64_t s = sh[i];
+    if (i < wid) wbase += s;
+    tot += s;
+  }
+  __syncthreads();
+  total = tot;
+  return wbase + incl - v;
+}
+
+static __global__ __launch_bounds__(kScanThreads) void scan_tile_reduce(const uint64_t* __restrict__ in, uint64_t n,
+                                                                 uint64_t* __restrict__ tile_sums) {
+  __shared__ uint64_t sh[kScanThreads / 64];
+  const uint64_t base = (uint64_t)blockIdx.x * kScanTile + (uint64_t)threadIdx.x * kScanPerThread;
+  uint64_t s = 0;
+#pragma unroll
+  for (int i = 0; i < kScanPerThread; ++i)
+    if (base + i < n) s += in[base + i];
+  uint64_t total;
+  block_excl_scan_u64(s, sh, total);
+  if (threadIdx.x == 0) tile_sums[blockIdx.x] = total;
+}
+
+// Single workgroup: exclusive scan of the tile sums in place.
+static __global__ __launch_bounds__(kScanThreads) void scan_tile_sums(uint64_t* __restrict__ sums, uint64_t n_tiles) {
+  __shared__ uint64_t sh[kScanThreads / 64];
+  uint64_t carry = 0;
+  for (uint64_t base = 0; base < n_tiles; base += kScanThreads) {
+    const uint64_t i = base + threadIdx.x;
+    uint64_t v = i < n_tiles ? sums[i] : 0;
+    uint64_t total;
+    uint64_t ex = block_excl_scan_u64(v, sh, total);
+    if (i < n_tiles) sums[i] = carry + ex;
+    carry += total;
+  }
+}
+
+// Out(i, prefix) is called for i in [0, n] with the exclusive prefix.
+template <class Out>
+__global__ __launch_bounds__(kScanThreads) void scan_tile_apply(const uint64_t* __restrict__ in, uint64_t n,
+                                                                const uint64_t* __restrict__ tile_offsets,
+                                                                Out out) {
+  __shared__ uint64_t sh[kScanThreads / 64];
+  const uint64_t base = (uint64_t)blockIdx.x * kScanTile + (uint64_t)threadIdx.x * kScanPerThread;
+  uint64_t v[kScanPerThread];
+  uint64_t s = 0;
+#pragma unroll
+  for (int i = 0; i < kScanPerThread; ++i) {
+    v[i] = base + i < n ? in[base + i] : 0;
+    s += v[i];
+  }
+  uint64_t total;
+  uint64_t ex = block_excl_scan_u64(s, sh, total) + tile_offsets[blockIdx.x];
+#pragma unroll
+  for (int i = 0; i < kScanPerThread; ++i) {
+    if (base + i < n) out(base + i, ex);
+    if (base + i == n - 1) out(n, ex + v[i]);
+    ex += v[i];
+  }
+}
+
+inline uint64_t scan_tiles(uint64_t n) { return (n + kScanTile - 1) / kScanTile; }
+
+// Enqueue the scan; `tmp` holds scan_tiles(n) u64.  n >= 1.
+template <class Out>
+inline hipError_t launch_excl_scan(const uint64_t* in, uint64_t n, uint64_t* tmp, Out out, hipStream_t st) {
+  const uint64_t tiles = scan_tiles(n);
+  hipLaunchKernelGGL(scan_tile_reduce, dim3((uint32_t)tiles), dim3(kScanThreads), 0, st, in, n, tmp);
+  hipLaunchKernelGGL(scan_tile_sums, dim3(1), dim3(kScanThreads), 0, st, tmp, tiles);
+  hipLaunchKernelGGL(scan_tile_apply<Out>, dim3((uint32_t)tiles), dim3(kScanThreads), 0, st, in, n,
+                     (const uint64_t*)tmp, out);
+  return hipGetLastError();
+}
+
+}  // namespace lsmgpu

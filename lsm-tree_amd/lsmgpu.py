@@ -1,0 +1,271 @@
+"""ctypes binding of lsm-tree_amd/liblsmgpu.so (include/lsmgpu.h) for tests and bench.
+
+Device memory comes from torch CUDA tensors (plumbing only).  Every call goes
+through the C ABI; there is no CPU fallback: importing this module on a box
+without the built library raises, and calls without a GPU fail loudly.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+HERE = Path(__file__).resolve().parent
+LIB_PATH = HERE / "liblsmgpu.so"
+
+LSM_HEADER_LEN = 33
+LSM_TRAILER_LEN = 31
+LSM_INPUT_PADDING = 64
+
+STATUS = {0: "OK", 1: "BAD_MAGIC", 2: "BAD_TYPE", 3: "HDR_CKSUM", 4: "CKSUM", 5: "PARSE", 6: "OVERFLOW",
+          7: "TYPE_MISMATCH", 8: "TRUNCATED", 9: "UNSUPPORTED", 10: "BAD_ARG", 11: "HIP_ERROR"}
+BLOCK_DATA, BLOCK_INDEX, BLOCK_FILTER, BLOCK_META = 0, 1, 2, 3
+
+
+class LsmItems(C.Structure):
+    _fields_ = [("keys", C.c_void_p), ("key_off", C.c_void_p), ("vals", C.c_void_p), ("val_off", C.c_void_p),
+                ("seqno", C.c_void_p), ("vtype", C.c_void_p), ("handle_off", C.c_void_p),
+                ("handle_size", C.c_void_p), ("n_items", C.c_uint64)]
+
+
+class LsmParsed(C.Structure):
+    _fields_ = [("seqno", C.c_void_p), ("key_off", C.c_void_p), ("val_off", C.c_void_p), ("val_len", C.c_void_p),
+                ("key_len", C.c_void_p), ("prefix_len", C.c_void_p), ("vtype", C.c_void_p),
+                ("handle_off", C.c_void_p)]
+
+
+class LsmBlockParams(C.Structure):
+    _fields_ = [("restart_interval", C.c_uint8), ("block_type", C.c_uint8), ("compression", C.c_uint8),
+                ("reserved", C.c_uint8), ("hash_ratio", C.c_float)]
+
+
+class LsmDecodeTuning(C.Structure):
+    _fields_ = [("blocks_per_wave", C.c_uint32), ("stage_bytes", C.c_uint32), ("tile_items", C.c_uint32),
+                ("flags", C.c_uint32)]
+
+
+DECODE_ITEM_START_VALID = 1
+
+
+class LsmError(RuntimeError):
+    pass
+
+
+def build():
+    import subprocess
+    subprocess.run(["make", "-s", "-C", str(HERE), "-j8"], check=True)
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            raise LsmError(f"{LIB_PATH} not built: run `make -C {HERE}` (or __graft_entry__.build())")
+        L = C.CDLL(str(LIB_PATH))
+        L.lsm_abi_version.restype = C.c_int
+        L.lsm_status_name.restype = C.c_char_p
+        L.lsm_status_name.argtypes = [C.c_int]
+        L.lsm_last_error.restype = C.c_char_p
+        L.lsm_device_count.restype = C.c_int
+        L.lsm_set_device.restype = C.c_int
+        L.lsm_set_device.argtypes = [C.c_int]
+        L.lsm_decode_workspace_size.restype = C.c_size_t
+        L.lsm_decode_workspace_size.argtypes = [C.c_uint32]
+        L.lsm_decode_blocks.restype = C.c_int
+        L.lsm_decode_blocks.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_int32, C.POINTER(LsmParsed),
+                                        C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]
+        L.lsm_decode_blocks_tuned.restype = C.c_int
+        L.lsm_decode_blocks_tuned.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_int32, C.POINTER(LsmParsed),
+                                              C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t,
+                                              C.POINTER(LsmDecodeTuning), C.c_void_p]
+        L.lsm_encode_bound.restype = C.c_uint64
+        L.lsm_encode_bound.argtypes = [C.c_uint64, C.c_uint32, C.c_uint64, C.c_uint64, C.POINTER(LsmBlockParams)]
+        L.lsm_encode_workspace_size.restype = C.c_size_t
+        L.lsm_encode_workspace_size.argtypes = [C.c_uint64, C.c_uint32]
+        L.lsm_encode_blocks.restype = C.c_int
+        L.lsm_encode_blocks.argtypes = [C.POINTER(LsmItems), C.c_void_p, C.c_uint32, C.POINTER(LsmBlockParams),
+                                        C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t,
+                                        C.c_void_p]
+        L.lsm_cut_blocks.restype = C.c_uint64
+        L.lsm_cut_blocks.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p, C.c_uint64]
+        L.lsm_xxh3_128_batch.restype = C.c_int
+        L.lsm_xxh3_128_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p]
+        _lib = L
+    return _lib
+
+
+EXPORTED_SYMBOLS = ["lsm_abi_version", "lsm_status_name", "lsm_last_error", "lsm_device_count", "lsm_set_device",
+                    "lsm_decode_workspace_size", "lsm_decode_blocks", "lsm_decode_blocks_tuned", "lsm_encode_bound",
+                    "lsm_encode_workspace_size", "lsm_encode_blocks", "lsm_cut_blocks", "lsm_xxh3_128_batch"]
+
+
+def _check(rc, what):
+    if rc != 0:
+        raise LsmError(f"{what} failed: {STATUS.get(rc, rc)} {lib().lsm_last_error().decode()}")
+
+
+def _torch():
+    import torch
+    if not torch.cuda.is_available():
+        raise LsmError("no GPU visible: the lsmgpu product path has no CPU fallback")
+    return torch
+
+
+def _stream(stream):
+    torch = _torch()
+    s = stream if stream is not None else torch.cuda.current_stream()
+    return C.c_void_p(s.cuda_stream)
+
+
+def _ptr(t):
+    return C.c_void_p(t.data_ptr()) if t is not None else None
+
+
+def padded_bytes(n, device="cuda"):
+    """uint8 device buffer of n bytes + LSM_INPUT_PADDING slack (16-aligned by the allocator)."""
+    torch = _torch()
+    buf = torch.zeros(n + LSM_INPUT_PADDING, dtype=torch.uint8, device=device)
+    return buf
+
+
+def to_device_bytes(data, device="cuda"):
+    """Host bytes / numpy uint8 -> padded device buffer (first len bytes valid)."""
+    import numpy as np
+    torch = _torch()
+    a = np.frombuffer(bytes(data), np.uint8) if isinstance(data, (bytes, bytearray, memoryview)) else np.asarray(data, np.uint8)
+    buf = padded_bytes(len(a), device)
+    if len(a):
+        buf[:len(a)].copy_(torch.from_numpy(a.copy()))
+    return buf
+
+
+PARSED_FIELDS = (("seqno", "int64"), ("key_off", "int32"), ("val_off", "int32"), ("val_len", "int32"),
+                 ("key_len", "int16"), ("prefix_len", "int16"), ("vtype", "uint8"), ("handle_off", "int64"))
+
+
+class Decoder:
+    """Reusable decode context: holds the workspace for up to n_blocks."""
+
+    def __init__(self, device="cuda"):
+        self.device = device
+        self.ws = None
+
+    def workspace(self, n_blocks):
+        torch = _torch()
+        need = lib().lsm_decode_workspace_size(n_blocks)
+        if self.ws is None or self.ws.numel() < need:
+            self.ws = torch.empty(max(need, 256), dtype=torch.uint8, device=self.device)
+        return self.ws
+
+    def alloc_outputs(self, item_cap, n_blocks, fields=None):
+        torch = _torch()
+        fields = fields or [f for f, _ in PARSED_FIELDS]
+        out = {}
+        for f, dt in PARSED_FIELDS:
+            if f in fields:
+                out[f] = torch.empty(max(item_cap, 1), dtype=getattr(torch, dt), device=self.device)
+        out["item_start"] = torch.empty(n_blocks + 1, dtype=torch.int32, device=self.device)
+        out["status"] = torch.empty(max(n_blocks, 1), dtype=torch.int32, device=self.device)
+        return out
+
+    def decode(self, blocks, block_off, n_blocks, out, item_cap, expect_type=-1, tuning=None, stream=None):
+        """Enqueue lsm_decode_blocks. blocks: uint8 cuda (padded); block_off: int64 cuda [n+1]."""
+        ws = self.workspace(n_blocks)
+        ps = LsmParsed()
+        for f, _ in PARSED_FIELDS:
+            setattr(ps, f, out[f].data_ptr() if f in out else None)
+        if tuning is not None:
+            t = LsmDecodeTuning(*tuning)  # (blocks_per_wave, stage_bytes, tile_items[, flags])
+            rc = lib().lsm_decode_blocks_tuned(_ptr(blocks), _ptr(block_off), n_blocks, expect_type, C.byref(ps),
+                                               item_cap, _ptr(out["item_start"]), _ptr(out["status"]), _ptr(ws),
+                                               ws.numel(), C.byref(t), _stream(stream))
+        else:
+            rc = lib().lsm_decode_blocks(_ptr(blocks), _ptr(block_off), n_blocks, expect_type, C.byref(ps), item_cap,
+                                         _ptr(out["item_start"]), _ptr(out["status"]), _ptr(ws), ws.numel(),
+                                         _stream(stream))
+        _check(rc, "lsm_decode_blocks")
+        return out
+
+
+def decode_blocks(blocks, block_off, n_blocks=None, expect_type=-1, item_cap=None, fields=None, tuning=None):
+    """Convenience: decode device blocks, returns dict of device tensors."""
+    n_blocks = (block_off.numel() - 1) if n_blocks is None else n_blocks
+    if item_cap is None:
+        item_cap = blocks.numel() // 3 + 1
+    d = Decoder(blocks.device)
+    out = d.alloc_outputs(item_cap, n_blocks, fields)
+    return d.decode(blocks, block_off, n_blocks, out, item_cap, expect_type, tuning)
+
+
+class Encoder:
+    def __init__(self, device="cuda"):
+        self.device = device
+        self.ws = None
+
+    def encode(self, items, starts, n_blocks, restart_interval=16, hash_ratio=0.0, block_type=BLOCK_DATA,
+               out=None, stream=None):
+        """items: dict of cuda tensors keys(u8, padded) key_off(i64 n+1) vals(u8, padded) val_off(i64 n+1)
+        seqno(i64) vtype(u8) [handle_off(i64) handle_size(i32)]; starts: int32 cuda [n_blocks+1]."""
+        torch = _torch()
+        n_items = items["seqno"].numel()
+        it = LsmItems()
+        it.keys = items["keys"].data_ptr()
+        it.key_off = items["key_off"].data_ptr()
+        it.vals = items["vals"].data_ptr() if "vals" in items else items["keys"].data_ptr()
+        it.val_off = items["val_off"].data_ptr() if "val_off" in items else items["key_off"].data_ptr()
+        it.seqno = items["seqno"].data_ptr()
+        it.vtype = items["vtype"].data_ptr() if "vtype" in items else None
+        it.handle_off = items["handle_off"].data_ptr() if "handle_off" in items else None
+        it.handle_size = items["handle_size"].data_ptr() if "handle_size" in items else None
+        it.n_items = n_items
+        params = LsmBlockParams(restart_interval, block_type, 0, 0, hash_ratio)
+        key_bytes = int(items["keys"].numel())
+        val_bytes = int(items["vals"].numel()) if "vals" in items else 0
+        bound = lib().lsm_encode_bound(n_items, n_blocks, key_bytes, val_bytes, C.byref(params))
+        need = lib().lsm_encode_workspace_size(n_items, n_blocks)
+        if self.ws is None or self.ws.numel() < need:
+            self.ws = torch.empty(max(need, 256), dtype=torch.uint8, device=self.device)
+        if out is None or out["buf"].numel() < bound:
+            out = {"buf": torch.empty(bound + LSM_INPUT_PADDING, dtype=torch.uint8, device=self.device),
+                   "block_off": torch.empty(n_blocks + 1, dtype=torch.int64, device=self.device),
+                   "status": torch.empty(max(n_blocks, 1), dtype=torch.int32, device=self.device)}
+        rc = lib().lsm_encode_blocks(C.byref(it), _ptr(starts), n_blocks, C.byref(params), _ptr(out["buf"]),
+                                     bound, _ptr(out["block_off"]), _ptr(out["status"]), _ptr(self.ws),
+                                     self.ws.numel(), _stream(stream))
+        _check(rc, "lsm_encode_blocks")
+        return out
+
+
+def xxh3_128_batch(data, off, n):
+    torch = _torch()
+    out = torch.empty(2 * max(n, 1), dtype=torch.int64, device=data.device)
+    _check(lib().lsm_xxh3_128_batch(_ptr(data), _ptr(off), n, _ptr(out), _stream(None)), "lsm_xxh3_128_batch")
+    return out
+
+
+def cut_blocks(key_off, val_off, block_size):
+    """Host-side Writer chunking (numpy uint64 [n+1] arrays) -> numpy uint32 starts."""
+    import numpy as np
+    key_off = np.ascontiguousarray(key_off, np.uint64)
+    val_off = np.ascontiguousarray(val_off, np.uint64)
+    n = len(key_off) - 1
+    starts = np.zeros(n + 2, np.uint32)
+    nb = lib().lsm_cut_blocks(key_off.ctypes.data, val_off.ctypes.data, n, block_size, starts.ctypes.data, n + 1)
+    return starts[:nb + 1].copy()
+
+
+def items_to_device(items_np, device="cuda"):
+    """pyoracle.Items-like numpy SoA -> dict of padded cuda tensors for Encoder.encode."""
+    import numpy as np
+    torch = _torch()
+    d = {"keys": to_device_bytes(items_np.keys, device), "vals": to_device_bytes(items_np.vals, device)}
+    d["key_off"] = torch.from_numpy(items_np.key_off.astype(np.int64)).to(device)
+    d["val_off"] = torch.from_numpy(items_np.val_off.astype(np.int64)).to(device)
+    d["seqno"] = torch.from_numpy(items_np.seqno.view(np.int64)).to(device)
+    d["vtype"] = torch.from_numpy(items_np.vtype).to(device)
+    d["handle_off"] = torch.from_numpy(items_np.handle_off.view(np.int64)).to(device)
+    d["handle_size"] = torch.from_numpy(items_np.handle_size.view(np.int32)).to(device)
+    return d

@@ -1,0 +1,300 @@
+"""ctypes binding of oracle/liblsmoracle.so — TEST INFRASTRUCTURE ONLY.
+
+Used by tests/ (as the checker), __graft_entry__.smoke() and bench.py's
+cpu_baseline leg.  The product path (lsm-tree_amd/) never imports this.
+See oracle/lsm_oracle.h for the reference citations.
+"""
+from __future__ import annotations
+
+import ctypes as C
+import os
+from pathlib import Path
+
+import numpy as np
+
+HERE = Path(__file__).resolve().parent
+LIB_PATH = HERE / "liblsmoracle.so"
+
+u8p = C.POINTER(C.c_uint8)
+u16p = C.POINTER(C.c_uint16)
+u32p = C.POINTER(C.c_uint32)
+u64p = C.POINTER(C.c_uint64)
+i32p = C.POINTER(C.c_int32)
+
+
+class OrcItems(C.Structure):
+    _fields_ = [
+        ("keys", u8p), ("key_off", u64p), ("vals", u8p), ("val_off", u64p),
+        ("seqno", u64p), ("vtype", u8p), ("handle_off", u64p), ("handle_size", u32p),
+        ("n_items", C.c_uint64),
+    ]
+
+
+class OrcParsed(C.Structure):
+    _fields_ = [
+        ("seqno", u64p), ("key_off", u32p), ("val_off", u32p), ("val_len", u32p),
+        ("key_len", u16p), ("prefix_len", u16p), ("vtype", u8p), ("handle_off", u64p),
+    ]
+
+
+class OrcHeader(C.Structure):
+    _fields_ = [("block_type", C.c_uint8), ("cksum_lo", C.c_uint64), ("cksum_hi", C.c_uint64),
+                ("data_length", C.c_uint32), ("uncompressed_length", C.c_uint32)]
+
+
+def build():
+    import subprocess
+    subprocess.run(["make", "-s", "-C", str(HERE)], check=True)
+
+
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not LIB_PATH.exists():
+            build()
+        L = C.CDLL(str(LIB_PATH))
+        L.orc_xxh3_64.restype = C.c_uint64
+        L.orc_xxh3_64.argtypes = [C.c_void_p, C.c_size_t]
+        L.orc_xxh3_128.restype = None
+        L.orc_xxh3_128.argtypes = [C.c_void_p, C.c_size_t, u64p, u64p]
+        L.orc_data_block_encode.restype = C.c_int64
+        L.orc_data_block_encode.argtypes = [C.POINTER(OrcItems), C.c_uint64, C.c_uint64, C.c_uint8,
+                                            C.c_float, C.c_void_p, C.c_size_t]
+        L.orc_index_block_encode.restype = C.c_int64
+        L.orc_index_block_encode.argtypes = [C.POINTER(OrcItems), C.c_uint64, C.c_uint64, C.c_void_p, C.c_size_t]
+        L.orc_block_write.restype = C.c_int64
+        L.orc_block_write.argtypes = [C.c_void_p, C.c_size_t, C.c_uint8, C.c_void_p, C.c_size_t]
+        L.orc_header_decode.restype = C.c_int
+        L.orc_header_decode.argtypes = [C.c_void_p, C.c_size_t, C.POINTER(OrcHeader)]
+        L.orc_block_verify.restype = C.c_int
+        L.orc_block_verify.argtypes = [C.c_void_p, C.c_size_t, C.POINTER(OrcHeader)]
+        L.orc_data_block_decode.restype = C.c_int64
+        L.orc_data_block_decode.argtypes = [C.c_void_p, C.c_size_t, C.POINTER(OrcParsed), C.c_uint64, C.c_uint64]
+        L.orc_index_block_decode.restype = C.c_int64
+        L.orc_index_block_decode.argtypes = [C.c_void_p, C.c_size_t, C.POINTER(OrcParsed), C.c_uint64, C.c_uint64]
+        L.orc_data_block_point_read.restype = C.c_int64
+        L.orc_data_block_point_read.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t, C.c_uint64]
+        L.orc_cut_blocks.restype = C.c_uint64
+        L.orc_cut_blocks.argtypes = [C.POINTER(OrcItems), C.c_uint32, C.c_void_p, C.c_uint64]
+        L.orc_encode_blocks.restype = C.c_int
+        L.orc_encode_blocks.argtypes = [C.POINTER(OrcItems), C.c_void_p, C.c_uint32, C.c_uint8, C.c_float,
+                                        C.c_uint8, C.c_void_p, C.c_uint64, C.c_void_p, C.c_int]
+        L.orc_decode_blocks.restype = C.c_int
+        L.orc_decode_blocks.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_int, C.POINTER(OrcParsed),
+                                        C.c_uint64, C.c_void_p, C.c_void_p, C.c_int]
+        L.orc_decode_materialize_blocks.restype = C.c_uint64
+        L.orc_decode_materialize_blocks.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_int, u64p]
+        _lib = L
+    return _lib
+
+
+def _ptr(a, t=C.c_void_p):
+    if a is None:
+        return None
+    return C.cast(a.ctypes.data, t)
+
+
+def xxh3_64(b: bytes) -> int:
+    a = np.frombuffer(b, dtype=np.uint8) if len(b) else np.zeros(1, np.uint8)
+    return lib().orc_xxh3_64(_ptr(a), len(b))
+
+
+def xxh3_128(b: bytes) -> int:
+    a = np.frombuffer(b, dtype=np.uint8) if len(b) else np.zeros(1, np.uint8)
+    lo, hi = C.c_uint64(), C.c_uint64()
+    lib().orc_xxh3_128(_ptr(a), len(b), C.byref(lo), C.byref(hi))
+    return (hi.value << 64) | lo.value
+
+
+class Items:
+    """Host SoA item batch (same layout as include/lsmgpu.h lsm_items)."""
+
+    def __init__(self, keys, key_off, vals, val_off, seqno, vtype, handle_off=None, handle_size=None):
+        self.keys = np.ascontiguousarray(keys, dtype=np.uint8)
+        self.key_off = np.ascontiguousarray(key_off, dtype=np.uint64)
+        self.vals = np.ascontiguousarray(vals, dtype=np.uint8)
+        self.val_off = np.ascontiguousarray(val_off, dtype=np.uint64)
+        self.seqno = np.ascontiguousarray(seqno, dtype=np.uint64)
+        self.vtype = np.ascontiguousarray(vtype, dtype=np.uint8)
+        n = len(self.seqno)
+        self.handle_off = np.ascontiguousarray(handle_off if handle_off is not None else np.zeros(n), dtype=np.uint64)
+        self.handle_size = np.ascontiguousarray(handle_size if handle_size is not None else np.zeros(n), dtype=np.uint32)
+        self.n = n
+        if len(self.keys) == 0:
+            self.keys = np.zeros(1, np.uint8)
+        if len(self.vals) == 0:
+            self.vals = np.zeros(1, np.uint8)
+
+    @classmethod
+    def from_list(cls, items):
+        """items: list of (key bytes, value bytes, seqno, vtype) or index tuples
+        (key, seqno, handle_offset, handle_size) when len==4 and value is int."""
+        keys = b"".join(k for k, *_ in items)
+        kl = np.array([len(k) for k, *_ in items], dtype=np.uint64)
+        key_off = np.concatenate([[0], np.cumsum(kl)]).astype(np.uint64)
+        vals = b"".join(v for _, v, _, _ in items)
+        vl = np.array([len(v) for _, v, _, _ in items], dtype=np.uint64)
+        val_off = np.concatenate([[0], np.cumsum(vl)]).astype(np.uint64)
+        seq = np.array([s for _, _, s, _ in items], dtype=np.uint64)
+        vt = np.array([t for _, _, _, t in items], dtype=np.uint8)
+        return cls(np.frombuffer(keys, np.uint8), key_off, np.frombuffer(vals, np.uint8), val_off, seq, vt)
+
+    def struct(self) -> OrcItems:
+        s = OrcItems()
+        s.keys = _ptr(self.keys, u8p); s.key_off = _ptr(self.key_off, u64p)
+        s.vals = _ptr(self.vals, u8p); s.val_off = _ptr(self.val_off, u64p)
+        s.seqno = _ptr(self.seqno, u64p); s.vtype = _ptr(self.vtype, u8p)
+        s.handle_off = _ptr(self.handle_off, u64p); s.handle_size = _ptr(self.handle_size, u32p)
+        s.n_items = self.n
+        return s
+
+
+def data_block_encode(items: Items, first=0, count=None, restart_interval=16, hash_ratio=0.0) -> bytes:
+    count = items.n - first if count is None else count
+    cap = 64 + 3 * (len(items.keys) + len(items.vals)) + 64 * count + 2 * 1024 * 1024
+    out = np.zeros(cap, np.uint8)
+    s = items.struct()
+    n = lib().orc_data_block_encode(C.byref(s), first, count, restart_interval, hash_ratio, _ptr(out), cap)
+    if n < 0:
+        raise ValueError(f"encode failed status {-n}")
+    return out[:n].tobytes()
+
+
+def index_block_encode(items: Items, first=0, count=None) -> bytes:
+    count = items.n - first if count is None else count
+    cap = 64 + 3 * len(items.keys) + 64 * count + 4096
+    out = np.zeros(cap, np.uint8)
+    s = items.struct()
+    n = lib().orc_index_block_encode(C.byref(s), first, count, _ptr(out), cap)
+    if n < 0:
+        raise ValueError(f"encode failed status {-n}")
+    return out[:n].tobytes()
+
+
+def block_write(payload: bytes, block_type=0) -> bytes:
+    cap = len(payload) + 33
+    out = np.zeros(cap, np.uint8)
+    src = np.frombuffer(payload, np.uint8) if payload else np.zeros(1, np.uint8)
+    n = lib().orc_block_write(_ptr(src), len(payload), block_type, _ptr(out), cap)
+    if n < 0:
+        raise ValueError(f"write failed {-n}")
+    return out[:n].tobytes()
+
+
+def header_decode(buf: bytes):
+    h = OrcHeader()
+    a = np.frombuffer(buf, np.uint8) if buf else np.zeros(1, np.uint8)
+    st = lib().orc_header_decode(_ptr(a), len(buf), C.byref(h))
+    return st, h
+
+
+def block_verify(buf: bytes):
+    h = OrcHeader()
+    a = np.frombuffer(buf, np.uint8) if buf else np.zeros(1, np.uint8)
+    st = lib().orc_block_verify(_ptr(a), len(buf), C.byref(h))
+    return st, h
+
+
+class Parsed:
+    FIELDS = (("seqno", np.uint64), ("key_off", np.uint32), ("val_off", np.uint32), ("val_len", np.uint32),
+              ("key_len", np.uint16), ("prefix_len", np.uint16), ("vtype", np.uint8), ("handle_off", np.uint64))
+
+    def __init__(self, n):
+        for name, dt in self.FIELDS:
+            setattr(self, name, np.zeros(max(n, 1), dt))
+        self.n = n
+
+    def struct(self) -> OrcParsed:
+        s = OrcParsed()
+        s.seqno = _ptr(self.seqno, u64p); s.key_off = _ptr(self.key_off, u32p)
+        s.val_off = _ptr(self.val_off, u32p); s.val_len = _ptr(self.val_len, u32p)
+        s.key_len = _ptr(self.key_len, u16p); s.prefix_len = _ptr(self.prefix_len, u16p)
+        s.vtype = _ptr(self.vtype, u8p); s.handle_off = _ptr(self.handle_off, u64p)
+        return s
+
+    def trimmed(self, n):
+        return {name: getattr(self, name)[:n].copy() for name, _ in self.FIELDS}
+
+
+def data_block_decode(payload: bytes, cap=None, index=False):
+    a = np.frombuffer(payload, np.uint8)
+    cap = cap if cap is not None else max(1, len(payload))
+    p = Parsed(cap)
+    s = p.struct()
+    fn = lib().orc_index_block_decode if index else lib().orc_data_block_decode
+    n = fn(_ptr(a), len(payload), C.byref(s), 0, cap)
+    if n < 0:
+        return int(n), None
+    return int(n), p.trimmed(n)
+
+
+def materialize(payload: bytes, parsed: dict, restart_interval: int):
+    """DataBlockParsedItem::materialize (data_block/mod.rs:296-315) in Python."""
+    out = []
+    n = len(parsed["seqno"])
+    for i in range(n):
+        h = (i // restart_interval) * restart_interval
+        ko, kl, pl = int(parsed["key_off"][i]), int(parsed["key_len"][i]), int(parsed["prefix_len"][i])
+        hk = int(parsed["key_off"][h])
+        key = payload[hk:hk + pl] + payload[ko:ko + kl]
+        vt = int(parsed["vtype"][i])
+        vo, vl = int(parsed["val_off"][i]), int(parsed["val_len"][i])
+        val = b"" if vt in (1, 2) else payload[vo:vo + vl]
+        out.append((key, val, int(parsed["seqno"][i]), vt))
+    return out
+
+
+def point_read(payload: bytes, needle: bytes, snapshot: int) -> int:
+    a = np.frombuffer(payload, np.uint8)
+    nd = np.frombuffer(needle, np.uint8) if needle else np.zeros(1, np.uint8)
+    return int(lib().orc_data_block_point_read(_ptr(a), len(payload), _ptr(nd), len(needle), snapshot))
+
+
+def cut_blocks(items: Items, block_size: int) -> np.ndarray:
+    starts = np.zeros(items.n + 2, np.uint32)
+    s = items.struct()
+    nb = lib().orc_cut_blocks(C.byref(s), block_size, _ptr(starts), items.n + 1)
+    return starts[:nb + 1].copy()
+
+
+def encode_blocks(items: Items, starts: np.ndarray, restart_interval=16, hash_ratio=0.0, block_type=0,
+                  nthreads=None):
+    nthreads = nthreads or os.cpu_count() or 1
+    nb = len(starts) - 1
+    starts = np.ascontiguousarray(starts, dtype=np.uint32)
+    cap = 64 * nb + 3 * (len(items.keys) + len(items.vals)) + 64 * items.n + 4096
+    out = np.zeros(cap, np.uint8)
+    off = np.zeros(nb + 1, np.uint64)
+    s = items.struct()
+    rc = lib().orc_encode_blocks(C.byref(s), _ptr(starts), nb, restart_interval, hash_ratio, block_type,
+                                 _ptr(out), cap, _ptr(off), nthreads)
+    if rc != 0:
+        raise ValueError(f"orc_encode_blocks failed status {-rc}")
+    return out[:int(off[-1])], off
+
+
+def decode_blocks(blocks: np.ndarray, block_off: np.ndarray, expect_type=-1, nthreads=None, item_cap=None):
+    nthreads = nthreads or os.cpu_count() or 1
+    nb = len(block_off) - 1
+    blocks = np.ascontiguousarray(blocks, dtype=np.uint8)
+    block_off = np.ascontiguousarray(block_off, dtype=np.uint64)
+    if item_cap is None:
+        item_cap = len(blocks) // 3 + 1
+    p = Parsed(item_cap)
+    item_start = np.zeros(nb + 1, np.uint32)
+    status = np.zeros(max(nb, 1), np.int32)
+    s = p.struct()
+    lib().orc_decode_blocks(_ptr(blocks), _ptr(block_off), nb, expect_type, C.byref(s), item_cap,
+                            _ptr(item_start), _ptr(status), nthreads)
+    n = int(item_start[-1])
+    return p.trimmed(n), item_start, status[:nb]
+
+
+def decode_materialize_blocks(blocks: np.ndarray, block_off: np.ndarray, nthreads=1):
+    fold = C.c_uint64()
+    n = lib().orc_decode_materialize_blocks(_ptr(np.ascontiguousarray(blocks)), _ptr(np.ascontiguousarray(block_off, dtype=np.uint64)),
+                                            len(block_off) - 1, nthreads, C.byref(fold))
+    return int(n), fold.value

@@ -1,0 +1,289 @@
+"""GPU parity tests: the HIP product path (through the C ABI) against the oracle
+and the committed golden vectors.  Bar: bit-exact bytes / fields / statuses.
+"""
+import random
+
+import numpy as np
+import pytest
+
+import pyoracle
+from conftest import case_expected_items, case_items
+from helpers import (FIELD_VIEW, compare_decode, counter_items, gpu_decode, index_items, pack, prefix_items,
+                     random_sorted_items)
+
+pytestmark = pytest.mark.gpu
+
+
+def _torch():
+    import torch
+    return torch
+
+
+# ------------------------------------------------------------------ XXH3
+
+def test_xxh3_batch_kats(gpu, xxh3_kat):
+    torch = _torch()
+    chunks, off = [], [0]
+    rng = random.Random(1)
+    pad_first = []
+    for v in xxh3_kat:
+        n = v["len"]
+        lead = rng.randint(0, 17)  # every alignment of the range start
+        b = bytes(rng.getrandbits(8) for _ in range(lead)) + bytes(((31 * i + 7) & 0xFF) for i in range(n))
+        chunks.append(b)
+        pad_first.append(lead)
+    data = b"".join(chunks)
+    starts, ends = [], []
+    pos = 0
+    for lead, c in zip(pad_first, chunks):
+        starts.append(pos + lead)
+        ends.append(pos + len(c))
+        pos += len(c)
+    # ranges are disjoint but not contiguous: encode each as its own [start,end) via two-entry offsets
+    d = gpu.to_device_bytes(data)
+    res = []
+    for s, e in zip(starts, ends):
+        off_t = torch.tensor([s, e], dtype=torch.int64, device="cuda")
+        res.append(gpu.xxh3_128_batch(d, off_t, 1))
+    torch.cuda.synchronize()
+    for v, r in zip(xxh3_kat, res):
+        lo, hi = [int(x) & 0xFFFFFFFFFFFFFFFF for x in r.cpu().tolist()[:2]]
+        assert (hi << 64) | lo == int(v["xxh3_128"]), v["len"]
+
+
+def test_xxh3_batch_random(gpu):
+    torch = _torch()
+    rng = np.random.default_rng(2)
+    data = rng.integers(0, 256, 300000, dtype=np.uint8)
+    cuts = np.sort(rng.choice(np.arange(1, len(data)), 200, replace=False))
+    off = np.concatenate([[0], cuts, [len(data)]]).astype(np.int64)
+    d = gpu.to_device_bytes(data)
+    out = gpu.xxh3_128_batch(d, torch.from_numpy(off).cuda(), len(off) - 1).cpu().numpy().view(np.uint64)
+    for i in range(len(off) - 1):
+        exp = pyoracle.xxh3_128(data[off[i]:off[i + 1]].tobytes())
+        assert (int(out[2 * i + 1]) << 64) | int(out[2 * i]) == exp, i
+
+
+# ------------------------------------------------------------------ golden
+
+def test_decode_golden_blocks(gpu, golden_blocks):
+    blocks = [bytes.fromhex(c["block"]) for c in golden_blocks]
+    buf, off = pack(blocks)
+    g = gpu_decode(gpu, buf, off)
+    parsed, item_start, status = pyoracle.decode_blocks(buf, off)
+    assert (status == 0).all()
+    compare_decode(g, parsed, item_start, status)
+    # and materialised items equal the golden inputs
+    for b, case in enumerate(golden_blocks):
+        s0, s1 = int(item_start[b]), int(item_start[b + 1])
+        payload = blocks[b][33:]
+        one = {f: g[f].view(dt)[s0:s1] for f, dt in FIELD_VIEW.items()}
+        if case["kind"] == "index":
+            for j, (k, s, o, sz) in enumerate(case_expected_items(case)):
+                ko, kl = int(one["key_off"][j]), int(one["key_len"][j])
+                assert payload[ko:ko + kl] == k and int(one["seqno"][j]) == s
+                assert int(one["handle_off"][j]) == o and int(one["val_len"][j]) == sz
+        else:
+            assert pyoracle.materialize(payload, one, case["restart_interval"]) == case_expected_items(case), case["name"]
+
+
+@pytest.mark.parametrize("tuning", [None, (1, 256, 64), (4, 4096, 64), (64, 65536, 2048)])
+def test_decode_golden_blocks_tunings(gpu, golden_blocks, tuning):
+    """Staged path, direct-from-HBM path (tiny stage) and large groups agree."""
+    blocks = [bytes.fromhex(c["block"]) for c in golden_blocks]
+    buf, off = pack(blocks)
+    g = gpu_decode(gpu, buf, off, tuning=tuning)
+    parsed, item_start, status = pyoracle.decode_blocks(buf, off)
+    compare_decode(g, parsed, item_start, status)
+
+
+def _gpu_encode(gpu, items, starts, ri, ratio, block_type):
+    torch = _torch()
+    d_items = gpu.items_to_device(items)
+    d_starts = torch.from_numpy(np.asarray(starts, np.int64).astype(np.int32)).cuda()
+    out = gpu.Encoder().encode(d_items, d_starts, len(starts) - 1, restart_interval=ri, hash_ratio=ratio,
+                               block_type=block_type)
+    torch.cuda.synchronize()
+    off = out["block_off"].cpu().numpy().view(np.uint64)
+    buf = out["buf"].cpu().numpy()[:int(off[-1])]
+    return buf, off, out["status"].cpu().numpy()[:len(starts) - 1]
+
+
+def test_encode_golden_blocks(gpu, golden_blocks):
+    for case in golden_blocks:
+        items = case_items(case)
+        buf, off, st = _gpu_encode(gpu, items, [0, items.n], case["restart_interval"], case["hash_ratio"],
+                                   case["block_type"])
+        assert (st == 0).all(), case["name"]
+        assert buf.tobytes().hex() == case["block"], case["name"]
+
+
+# ------------------------------------------------------------------ fuzz-like
+
+@pytest.mark.parametrize("ri", [1, 2, 5, 16, 64])
+@pytest.mark.parametrize("ratio", [0.0, 1.33])
+def test_encode_decode_random_batches(gpu, ri, ratio):
+    items = random_sorted_items(3000, seed=ri * 7 + int(ratio), vmax=120)
+    rng = random.Random(ri)
+    # random cut points (blocks of 1..120 items)
+    starts = [0]
+    while starts[-1] < items.n:
+        starts.append(min(items.n, starts[-1] + rng.randint(1, 120)))
+    starts = np.array(starts, np.uint32)
+    ref_buf, ref_off = pyoracle.encode_blocks(items, starts, restart_interval=ri, hash_ratio=ratio)
+    buf, off, st = _gpu_encode(gpu, items, starts, ri, ratio, 0)
+    assert (st == 0).all()
+    assert (off == ref_off).all()
+    assert buf.tobytes() == ref_buf.tobytes()
+    g = gpu_decode(gpu, buf, off)
+    parsed, item_start, status = pyoracle.decode_blocks(buf, off)
+    assert (status == 0).all()
+    compare_decode(g, parsed, item_start, status)
+
+
+def test_index_blocks(gpu):
+    items = index_items(2000)
+    starts = np.array(list(range(0, 2000, 97)) + [2000], np.uint32)
+    ref_buf, ref_off = pyoracle.encode_blocks(items, starts, block_type=1)
+    buf, off, st = _gpu_encode(gpu, items, starts, 1, 0.0, 1)
+    assert (st == 0).all() and buf.tobytes() == ref_buf.tobytes()
+    for et in (-1, 1):
+        g = gpu_decode(gpu, buf, off, expect_type=et)
+        parsed, item_start, status = pyoracle.decode_blocks(buf, off, expect_type=et)
+        assert (status == 0).all()
+        compare_decode(g, parsed, item_start, status)
+    g = gpu_decode(gpu, buf, off, expect_type=0)
+    assert (g["status"] == 7).all()  # TYPE_MISMATCH (util.rs:81-86)
+
+
+# ------------------------------------------------------------------ configs (reduced counts)
+
+def test_config2_shape_counter_keys(gpu):
+    items = counter_items(52 * 2048, seed=21)
+    starts = pyoracle.cut_blocks(items, 4096)
+    assert len(starts) - 1 == 2048
+    ref_buf, ref_off = pyoracle.encode_blocks(items, starts)
+    buf, off, st = _gpu_encode(gpu, items, starts, 16, 0.0, 0)
+    assert (st == 0).all() and buf.tobytes() == ref_buf.tobytes()
+    g = gpu_decode(gpu, buf, off)
+    parsed, item_start, status = pyoracle.decode_blocks(buf, off)
+    compare_decode(g, parsed, item_start, status)
+
+
+def test_config4_prefix_heavy_16k(gpu):
+    items = prefix_items(56 * 300)
+    starts = pyoracle.cut_blocks(items, 16384)
+    ref_buf, ref_off = pyoracle.encode_blocks(items, starts)
+    assert int(ref_off[1]) == 14953
+    buf, off, st = _gpu_encode(gpu, items, starts, 16, 0.0, 0)
+    assert (st == 0).all() and buf.tobytes() == ref_buf.tobytes()
+    for tuning in (None, (8, 32768, 512)):
+        g = gpu_decode(gpu, buf, off, tuning=tuning)
+        parsed, item_start, status = pyoracle.decode_blocks(buf, off)
+        compare_decode(g, parsed, item_start, status)
+
+
+def test_64k_blocks_u32_binary_index(gpu):
+    """64 KiB random-key blocks: binary-index step 4 (builder.rs:22-32), larger
+    than the default LDS stage -> the direct-from-HBM paths."""
+    rng = np.random.default_rng(8)
+    n = 820 * 12
+    keys = np.sort(rng.integers(0, 2 ** 63, n, dtype=np.uint64))
+    import pyoracle as po
+    kb = keys.byteswap().view(np.uint8).reshape(n, 8)
+    keys16 = np.concatenate([kb, rng.integers(0, 256, (n, 8), dtype=np.uint8)], axis=1).reshape(-1)
+    vals = rng.integers(0, 256, n * 64, dtype=np.uint8)
+    items = po.Items(keys16, np.arange(n + 1, dtype=np.uint64) * np.uint64(16), vals,
+                     np.arange(n + 1, dtype=np.uint64) * np.uint64(64), np.full(n, 63, np.uint64), np.zeros(n, np.uint8))
+    starts = po.cut_blocks(items, 65536)
+    ref_buf, ref_off = po.encode_blocks(items, starts)
+    p0 = ref_buf[33:int(ref_off[1])].tobytes()
+    assert p0[-31 + 1] == 4  # u32 binary index
+    buf, off, st = _gpu_encode(gpu, items, starts, 16, 0.0, 0)
+    assert (st == 0).all() and buf.tobytes() == ref_buf.tobytes()
+    g = gpu_decode(gpu, buf, off)
+    parsed, item_start, status = po.decode_blocks(buf, off)
+    compare_decode(g, parsed, item_start, status)
+
+
+# ------------------------------------------------------------------ corruption / edge cases
+
+def test_corruption_statuses_match_oracle(gpu):
+    items = random_sorted_items(2500, seed=5)
+    starts = np.array(list(range(0, 2500, 50)) + [2500], np.uint32)
+    buf, off = pyoracle.encode_blocks(items, starts, restart_interval=4, hash_ratio=1.0)
+    buf = buf.copy()
+    rng = random.Random(99)
+    nb = len(off) - 1
+    for b in range(0, nb, 2):
+        o, e = int(off[b]), int(off[b + 1])
+        where = rng.choice(["magic", "type", "hdr", "payload", "trailer", "len"])
+        if where == "magic":
+            buf[o] ^= 0x40
+        elif where == "type":
+            buf[o + 4] = rng.choice([2, 3, 7])
+        elif where == "hdr":
+            buf[o + rng.randint(5, 32)] ^= 1 << rng.randint(0, 7)
+        elif where == "payload":
+            buf[rng.randint(o + 33, e - 1)] ^= 1 << rng.randint(0, 7)
+        elif where == "trailer":
+            buf[e - rng.randint(1, 31)] ^= 0xFF
+        else:
+            buf[o + 21] ^= 1
+    g = gpu_decode(gpu, buf, off)
+    parsed, item_start, status = pyoracle.decode_blocks(buf, off)
+    assert (status[1::2] == 0).all() and (status[0::2] != 0).all()
+    compare_decode(g, parsed, item_start, status)
+
+
+def test_structurally_broken_payloads_with_valid_checksums(gpu):
+    """Payload corruption re-sealed with a correct header: exercises the parse
+    validation (the reference would panic, lib.rs:62-66; both report PARSE)."""
+    items = random_sorted_items(1200, seed=6)
+    rng = random.Random(5)
+    blocks = []
+    for b in range(60):
+        payload = bytearray(pyoracle.data_block_encode(items, b * 20, 20, restart_interval=rng.choice([1, 3, 16])))
+        kind = b % 6
+        if kind == 1:
+            payload[rng.randrange(0, len(payload) - 31)] = rng.getrandbits(8)
+        elif kind == 2:
+            payload[-31] = 0  # restart interval 0
+        elif kind == 3:
+            payload[-4] ^= 1  # item count
+        elif kind == 4:
+            payload[-31 + 6] ^= 1  # binary index offset
+        elif kind == 5:
+            payload = payload[:rng.randint(0, 40)]
+        blocks.append(pyoracle.block_write(bytes(payload)))
+    buf, off = pack(blocks)
+    for tuning in (None, (1, 256, 64)):
+        g = gpu_decode(gpu, buf, off, tuning=tuning)
+        parsed, item_start, status = pyoracle.decode_blocks(buf, off)
+        compare_decode(g, parsed, item_start, status)
+
+
+def test_edge_handles(gpu):
+    good = pyoracle.block_write(pyoracle.data_block_encode(pyoracle.Items.from_list([(b"k", b"v", 1, 0)])))
+    blocks = [good, good[:10], b"", good[:33], pyoracle.block_write(b"x" * 40, 2), good]
+    buf, off = pack(blocks)
+    g = gpu_decode(gpu, buf, off)
+    parsed, item_start, status = pyoracle.decode_blocks(buf, off)
+    compare_decode(g, parsed, item_start, status)
+    assert list(status) == [0, 8, 8, 4, 9, 0]
+    # item capacity smaller than needed -> OVERFLOW on the clamped blocks
+    g = gpu_decode(gpu, buf, off, item_cap=1)
+    parsed, item_start, status = pyoracle.decode_blocks(buf, off, item_cap=1)
+    compare_decode(g, parsed, item_start, status)
+
+
+def test_round_trip_tombstones_and_big_seqnos(gpu):
+    items = random_sorted_items(4000, seed=12, big_seq=True, vtypes=(0, 1, 2, 4))
+    starts = pyoracle.cut_blocks(items, 1024)
+    for ri, ratio in ((16, 0.0), (3, 2.5)):
+        ref_buf, ref_off = pyoracle.encode_blocks(items, starts, restart_interval=ri, hash_ratio=ratio)
+        buf, off, st = _gpu_encode(gpu, items, starts, ri, ratio, 0)
+        assert (st == 0).all() and buf.tobytes() == ref_buf.tobytes()
+        g = gpu_decode(gpu, buf, off)
+        parsed, item_start, status = pyoracle.decode_blocks(buf, off)
+        compare_decode(g, parsed, item_start, status)
