@@ -105,6 +105,154 @@ __device__ __forceinline__ bool parse_data_record(Cursor& c, bool restart, uint3
   return true;
 }
 
+// ---------------------------------------------------------------- fast path
+// One aligned 36-byte LDS/HBM read burst gives a 32-byte register window at
+// the record start; the record header (vtype, seqno <= 7 LEB bytes, shared,
+// rest/key_len) and, for short keys, the value-length varint are decoded from
+// registers with bit tricks (no per-byte loop).  Anything outside that shape
+// (seqno >= 2^49, long key before the value length) falls back to Cursor.
+struct Win32 {
+  uint64_t w0, w1, w2, w3;
+};
+__device__ __forceinline__ Win32 read_win32(const uint8_t* base, uint32_t pos) {
+  const uint32_t a = pos & ~3u, s = pos & 3u;
+  uint32_t d[9];
+#pragma unroll
+  for (int k = 0; k < 9; ++k) d[k] = ld32(base, a + 4 * k);
+  uint32_t e[8];
+#pragma unroll
+  for (int k = 0; k < 8; ++k) e[k] = alignbyte(d[k + 1], d[k], s);
+  return {(uint64_t)e[0] | ((uint64_t)e[1] << 32), (uint64_t)e[2] | ((uint64_t)e[3] << 32),
+          (uint64_t)e[4] | ((uint64_t)e[5] << 32), (uint64_t)e[6] | ((uint64_t)e[7] << 32)};
+}
+// bytes o..o+7 of the window (o <= 24)
+__device__ __forceinline__ uint64_t win_at(const Win32& w, uint32_t o) {
+  const uint32_t q = o >> 3, k = (o & 7) << 3;
+  const uint64_t a = q == 0 ? w.w0 : q == 1 ? w.w1 : q == 2 ? w.w2 : w.w3;
+  const uint64_t b = q == 0 ? w.w1 : q == 1 ? w.w2 : q == 2 ? w.w3 : 0;
+  return k ? (a >> k) | (b << (64 - k)) : a;
+}
+// LEB128 length within 8 bytes (9 = not terminated)
+__device__ __forceinline__ uint32_t leb_len8(uint64_t x) {
+  const uint64_t t = ~x & 0x8080808080808080ULL;
+  return t ? (uint32_t)(__builtin_ctzll(t) >> 3) + 1 : 9;
+}
+__device__ __forceinline__ uint64_t leb_val8(uint64_t x, uint32_t n) {  // n in 1..8
+  if (n < 8) x &= (1ULL << (8 * n)) - 1;
+  x = ((x & 0x7F007F007F007F00ULL) >> 1) | (x & 0x007F007F007F007FULL);
+  x = ((x & 0x3FFF00003FFF0000ULL) >> 2) | (x & 0x00003FFF00003FFFULL);
+  x = ((x & 0x0FFFFFFF00000000ULL) >> 4) | (x & 0x000000000FFFFFFFULL);
+  return x;
+}
+
+// Returns 1 = parsed (next = position after the record), 0 = take the Cursor
+// path, -1 = malformed (same outcomes as oracle parse_data_item).
+__device__ __forceinline__ int parse_data_fast(const uint8_t* base, uint32_t p0, uint32_t pos, uint32_t end,
+                                               bool restart, uint32_t base_key_off, ItemFields& f,
+                                               uint32_t& next) {
+  if (pos >= end) return -1;
+  const Win32 w = read_win32(base, p0 + pos);
+  const uint32_t vt = (uint32_t)(w.w0 & 0xFF);
+  if (!valid_vtype(vt)) return -1;  // includes the 0xFF marker inside an interval
+  const uint64_t x = win_at(w, 1);
+  const uint32_t n1 = leb_len8(x);
+  if (n1 > 7) return 0;
+  const uint64_t seq = leb_val8(x, n1);
+  uint32_t o = 1 + n1;
+  uint64_t y = win_at(w, o);
+  uint64_t shared = 0;
+  if (!restart) {
+    const uint32_t n2 = leb_len8(y);
+    if (n2 > 3) return -1;
+    shared = leb_val8(y, n2) & 0xFFFF;
+    y >>= 8 * n2;
+    o += n2;
+  }
+  const uint32_t n3 = leb_len8(y);
+  if (n3 > 3) return -1;
+  const uint32_t klen = (uint32_t)(leb_val8(y, n3) & 0xFFFF);
+  o += n3;
+  if (pos + o > end) return -1;  // a header byte at/after the record area end
+  if (!restart && (uint64_t)base_key_off + shared > end) return -1;
+  const uint32_t q = o + klen;
+  if ((uint64_t)pos + q > end) return -1;
+  uint64_t vl = 0;
+  uint32_t n4 = 0;
+  if (!is_tombstone(vt)) {
+    uint64_t z;
+    if (q <= 24) {
+      z = win_at(w, q);
+    } else {
+      z = read_win16(base, p0 + pos + q).lo;
+    }
+    n4 = leb_len8(z);
+    if (n4 > 5) return -1;
+    vl = leb_val8(z, n4) & 0xFFFFFFFFULL;
+    if (pos + q + n4 > end) return -1;
+  }
+  const uint32_t val_off = pos + q + n4;
+  if ((uint64_t)val_off + vl > end) return -1;
+  f.seqno = seq;
+  f.handle_off = 0;
+  f.key_off = pos + o;
+  f.key_len = (uint16_t)klen;
+  f.prefix_len = (uint16_t)shared;
+  f.val_off = val_off;
+  f.val_len = (uint32_t)vl;
+  f.vtype = (uint8_t)vt;
+  next = val_off + (uint32_t)vl;
+  return 1;
+}
+
+// Record boundary only (decode phase A): the serial walk of a restart
+// interval needs nothing but each record's length.  Varint boundaries come
+// from the terminator bit mask (~bytes & 0x80) by repeatedly clearing the
+// lowest set bit; values are only materialised for the key length (1 byte)
+// and the value length (1-2 bytes).  Other shapes return 0 (Cursor path).
+// -1 = malformed in a way the oracle also rejects.  key_off is valid on 1.
+__device__ __forceinline__ int data_record_next_fast(const uint8_t* base, uint32_t p0, uint32_t p, uint32_t end,
+                                                     bool restart, uint32_t& next, uint32_t& key_off) {
+  if (p >= end) return -1;
+  const Win32 w = read_win32(base, p0 + p);
+  const uint64_t lo = w.w0;
+  const uint32_t vt = (uint32_t)(lo & 0xFF);
+  if (!valid_vtype(vt)) return -1;
+  uint64_t t = ~lo & 0x8080808080808000ULL;  // varint terminators in bytes 1..7
+  if (!t) return 0;
+  const uint32_t e1 = (uint32_t)__builtin_ctzll(t);  // seqno
+  t &= t - 1;
+  uint32_t e2 = e1;
+  if (!restart) {                                    // shared prefix length
+    if (!t) return 0;
+    e2 = (uint32_t)__builtin_ctzll(t);
+    t &= t - 1;
+  }
+  if (!t) return 0;
+  const uint32_t e3 = (uint32_t)__builtin_ctzll(t);  // key (suffix) length
+  if (e3 - e2 != 8) return 0;                        // multi-byte key length
+  const uint32_t klen = (uint32_t)(lo >> (e3 - 7)) & 0x7F;
+  const uint32_t h = (e3 >> 3) + 1;
+  key_off = p + h;
+  const uint32_t q = h + klen;
+  if (is_tombstone(vt)) {
+    next = p + q;
+    return 1;
+  }
+  if (p + q >= end) return -1;  // the value length byte must precede the record area end
+  const uint64_t z = q <= 24 ? win_at(w, q) : read_win16(base, p0 + p + q).lo;
+  uint32_t vl;
+  if (!(z & 0x80)) {
+    vl = (uint32_t)(z & 0x7F);
+    next = p + q + 1 + vl;
+  } else if (!(z & 0x8000)) {
+    vl = (uint32_t)(z & 0x7F) | ((uint32_t)(z >> 1) & 0x3F80);
+    next = p + q + 2 + vl;
+  } else {
+    return 0;
+  }
+  return 1;
+}
+
 // KeyedBlockHandle::parse_full, src/table/index_block/block_handle.rs:175-206.
 __device__ __forceinline__ bool parse_index_record(Cursor& c, ItemFields& f) {
   uint32_t m;

@@ -5,18 +5,21 @@
 // (src/table/util.rs:79-86) and the full forward DataBlock::iter() /
 // IndexBlock::iter() (src/table/block/decoder.rs:442-483) over a whole batch.
 //
-// Launch shape (DESIGN.md "Decode kernel"):
-//   * one 64-lane wave per workgroup; wave w owns blocks [w*BPW, (w+1)*BPW);
-//   * it repeatedly takes the longest run of its next blocks that fits the
-//     LDS stage (stage_bytes) and the output tile (tile_items), copies the
-//     run's bytes HBM->LDS in one coalesced 16 B/lane sweep (consecutive
-//     blocks are contiguous on disk, so a run is one contiguous span);
-//   * header checks run lane-parallel (lane j = block j of the run);
-//   * each payload's xxh3_128 is computed by the whole wave from LDS;
-//   * restart intervals are the unit of parallelism: lane = (block, restart),
-//     each lane walks its interval's records with a 16-byte register window;
-//   * parsed items land in an LDS SoA tile and leave in coalesced stores.
-// Blocks larger than the stage run the same code directly on HBM.
+// Launch shape (DESIGN.md "Decode kernel"): one 64-lane wave per workgroup,
+// wave w owns blocks [w*BPW, (w+1)*BPW) and walks them in GROUPS — the longest
+// run of consecutive blocks that fits the LDS stage (consecutive blocks are
+// contiguous on disk, so a group is one contiguous span):
+//   1. lane j holds block j's handle and item range in registers;
+//   2. the span is copied HBM -> LDS with global_load_lds_dwordx4 (1 KiB per
+//      wave instruction), one wait per group;
+//   3. lane j checks block j's header (magic, type, 29-byte xxh3 checksum);
+//   4. the four 16-lane DPP rows hash four payloads at a time (xxh3_128);
+//   5. lane j reads block j's trailer, a wave scan numbers the restart
+//      intervals of the group;
+//   6. phase A: lane = restart interval, walks record boundaries only;
+//   7. phase B: lane = record, parses and validates every field and stores
+//      the parsed-item SoA with coalesced global stores.
+// Blocks larger than the stage take decode_block_direct (same parsers on HBM).
 #include <hip/hip_runtime.h>
 
 #include "block_format.hpp"
@@ -24,6 +27,14 @@
 #include "scan.hpp"
 
 namespace lsmgpu {
+
+// Diagnostic-only flags (lsm_decode_tuning.flags high bits): drop one phase to
+// price it in a profile.  Outputs are NOT valid with any of them set.
+constexpr uint32_t kDiagSkipHash = 0x100, kDiagSkipParse = 0x200, kDiagSkipStore = 0x400;
+
+constexpr uint32_t kMaxGroup = 32;  // blocks per staged group
+constexpr uint32_t kNoItem = 0xFFFFFFFFu;
+constexpr uint32_t kInfoRestart = 1u << 21;
 
 struct alignas(16) BlockMeta {
   uint64_t ck_lo, ck_hi;
@@ -35,41 +46,17 @@ struct alignas(16) BlockMeta {
   uint32_t item0;     // first output index relative to the group base
   uint32_t chain0;    // exclusive prefix of restart intervals in the group
 };
-constexpr uint32_t kMetaBytes = 64 * sizeof(BlockMeta);
+constexpr uint32_t kMetaBytes = kMaxGroup * sizeof(BlockMeta);
 
-struct TileView {
-  uint64_t* seqno;
-  uint32_t *key_off, *val_off, *val_len;
-  uint16_t *key_len, *prefix_len;
-  uint8_t* vtype;
-};
-
-__host__ __device__ constexpr uint32_t tile_bytes(uint32_t items) {
-  // each array 16-byte aligned
-  return ((items * 8 + 15) & ~15u) + 3 * ((items * 4 + 15) & ~15u) + 2 * ((items * 2 + 15) & ~15u) +
-         ((items + 15) & ~15u);
-}
-__device__ __forceinline__ TileView make_tile(uint8_t* t, uint32_t items) {
-  TileView v;
-  v.seqno = (uint64_t*)t; t += (items * 8 + 15) & ~15u;
-  v.key_off = (uint32_t*)t; t += (items * 4 + 15) & ~15u;
-  v.val_off = (uint32_t*)t; t += (items * 4 + 15) & ~15u;
-  v.val_len = (uint32_t*)t; t += (items * 4 + 15) & ~15u;
-  v.key_len = (uint16_t*)t; t += (items * 2 + 15) & ~15u;
-  v.prefix_len = (uint16_t*)t; t += (items * 2 + 15) & ~15u;
-  v.vtype = (uint8_t*)t;
-  return v;
+__device__ __forceinline__ void wave_sync() {
+  // Single-wave workgroups: LDS operations of a wave complete in order, so a
+  // compiler barrier is all cross-lane LDS hand-offs need (no s_barrier, and
+  // no vmcnt(0) drain of the output stores as __syncthreads would imply).
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-__device__ __forceinline__ void emit_tile(const TileView& t, uint32_t i, const ItemFields& f) {
-  t.seqno[i] = f.seqno;
-  t.key_off[i] = f.key_off;
-  t.val_off[i] = f.val_off;
-  t.val_len[i] = f.val_len;
-  t.key_len[i] = f.key_len;
-  t.prefix_len[i] = f.prefix_len;
-  t.vtype[i] = f.vtype;
-}
 __device__ __forceinline__ void emit_global(const lsm_parsed_items& o, uint64_t i, const ItemFields& f) {
   if (o.seqno) o.seqno[i] = f.seqno;
   if (o.key_off) o.key_off[i] = f.key_off;
@@ -81,21 +68,20 @@ __device__ __forceinline__ void emit_global(const lsm_parsed_items& o, uint64_t 
   if (o.handle_off) o.handle_off[i] = f.handle_off;
 }
 
-// Lane-level: header + (after the wave hash) trailer checks, oracle order.
+// Lane-level: header checks in oracle order (header.rs:116-169).
 __device__ __forceinline__ void meta_header(const uint8_t* base, uint32_t hb, uint64_t len, BlockMeta& m) {
   HeaderInfo h;
   m.hb = hb;
   m.len = (uint32_t)len;
   m.st = (len > 0xFFFFFF00ULL) ? ST_TRUNCATED : check_header(base, hb, len, h);
-  if (m.st == ST_OK) {
-    m.ck_lo = h.ck_lo;
-    m.ck_hi = h.ck_hi;
-    m.type = h.type;
-    m.item_count = h.data_length;  // stash data_length until meta_trailer
-  }
+  m.ck_lo = h.ck_lo;
+  m.ck_hi = h.ck_hi;
+  m.type = h.type;
+  m.item_count = h.data_length;  // stash data_length until meta_trailer
   m.chain0 = 0;
 }
 
+// After the payload checksum: data_length, expected type, trailer structure.
 __device__ __forceinline__ void meta_trailer(const uint8_t* base, int32_t expect_type, uint32_t cap, BlockMeta& m) {
   if (m.st != ST_OK) return;
   const uint32_t plen = m.len - kHdrLen;
@@ -112,38 +98,129 @@ __device__ __forceinline__ void meta_trailer(const uint8_t* base, int32_t expect
   m.item_count = t.item_count; m.rec_end = t.rec_end;
 }
 
-// Walk restart interval r of a block whose payload starts at base[p0].
-// Emits through `emit(j, fields)` with j = item index within the block.
-template <class Emit>
-__device__ __forceinline__ bool walk_interval(const uint8_t* base, uint32_t p0, const BlockMeta& m, uint32_t r,
-                                              Emit emit) {
+__device__ __forceinline__ TrailerInfo trailer_of(const BlockMeta& m) {
   TrailerInfo t;
   t.ri = m.ri; t.step = m.step; t.bin_len = m.bin_len; t.bin_off = m.bin_off;
   t.item_count = m.item_count; t.rec_end = m.rec_end;
+  t.hash_len = 0; t.hash_off = 0;
+  return t;
+}
+
+// Rare record shapes (long varints) through the general LEB cursor; kept out
+// of line so the hot loops stay small in the instruction cache.
+__device__ __noinline__ bool parse_data_slow(const uint8_t* base, uint32_t p0, uint32_t pos, uint32_t end,
+                                             bool restart, uint32_t base_key, ItemFields* f, uint32_t* next) {
+  Cursor c;
+  c.init(base, p0, pos, end);
+  if (!parse_data_record(c, restart, base_key, *f)) return false;
+  *next = c.pos;
+  return true;
+}
+__device__ __noinline__ bool parse_index_slow(const uint8_t* base, uint32_t p0, uint32_t pos, uint32_t end,
+                                              ItemFields* f, uint32_t* next) {
+  Cursor c;
+  c.init(base, p0, pos, end);
+  if (!parse_index_record(c, *f)) return false;
+  *next = c.pos;
+  return true;
+}
+
+// Full parse of one record at pos; returns next position or false.
+__device__ __forceinline__ bool parse_record(const uint8_t* base, uint32_t p0, uint32_t pos, const TrailerInfo& t,
+                                             uint32_t type, bool restart, uint32_t base_key, ItemFields& f,
+                                             uint32_t& next) {
+  ItemFields tmp;  // only the out-of-line paths take an address (keeps f in registers)
+  uint32_t tnext;
+  bool ok;
+  if (type == 1) {
+    ok = parse_index_slow(base, p0, pos, t.rec_end, &tmp, &tnext);
+  } else {
+    const int rc = parse_data_fast(base, p0, pos, t.rec_end, restart, base_key, f, next);
+    if (rc > 0) return true;
+    if (rc < 0) return false;
+    ok = parse_data_slow(base, p0, pos, t.rec_end, restart, base_key, &tmp, &tnext);
+  }
+  f = tmp;
+  next = tnext;
+  return ok;
+}
+
+// Phase A for restart interval r of group block j: record start positions
+// (payload-relative, u16) into info[], the interval head's key offset into
+// bkey[].  The last record's end is checked in phase B.
+__device__ __forceinline__ bool walk_boundaries(const uint8_t* img, const BlockMeta& m, uint32_t j, uint32_t r,
+                                                uint32_t* info, uint16_t* bkey) {
+  const TrailerInfo t = trailer_of(m);
+  const uint32_t p0 = m.hb + kHdrLen;
+  const uint32_t start = bin_get(img, p0, t, r);
+  const uint32_t count = (r + 1 == t.bin_len) ? t.item_count - r * t.ri : t.ri;
+  const uint32_t ib0 = m.item0 + r * t.ri;
+  if (start >= t.rec_end) return false;  // a record must start before the trailer marker
+  info[ib0] = start | (j << 16) | kInfoRestart;
+  if (m.type == 1) return true;          // index blocks: one record per restart interval
+  uint32_t p = start;
+  for (uint32_t jj = 0; jj + 1 < count; ++jj) {
+    uint32_t next, key_off;
+    const int rc = data_record_next_fast(img, p0, p, t.rec_end, jj == 0, next, key_off);
+    if (rc < 0) return false;
+    if (rc == 0) {
+      ItemFields tmp;
+      uint32_t tnext;
+      if (!parse_data_slow(img, p0, p, t.rec_end, jj == 0, jj == 0 ? 0 : bkey[ib0], &tmp, &tnext)) return false;
+      key_off = tmp.key_off;
+      next = tnext;
+    }
+    if (jj == 0) bkey[ib0] = (uint16_t)key_off;
+    p = next;
+    if (p >= t.rec_end) return false;
+    info[ib0 + jj + 1] = p | (j << 16);
+  }
+  return true;
+}
+
+// Phase B for group item i: full parse at its recorded start, checking that
+// the record ends exactly where the next one (or the interval) begins.
+__device__ __forceinline__ bool parse_item(const uint8_t* img, const BlockMeta& m, uint32_t i, uint32_t inf,
+                                           const uint32_t* info, const uint16_t* bkey, ItemFields& f) {
+  if (m.st != ST_OK) return false;
+  const TrailerInfo t = trailer_of(m);
+  const uint32_t p0 = m.hb + kHdrLen;
+  const uint32_t p = inf & 0xFFFF;
+  const uint32_t ib = i - m.item0;
+  const uint32_t r = ib / t.ri, jj = ib - r * t.ri;
+  const bool last = jj + 1 == t.ri || ib + 1 == t.item_count;
+  const uint32_t base_key = jj ? bkey[m.item0 + r * t.ri] : 0;
+  uint32_t next;
+  if (!parse_record(img, p0, p, t, m.type, jj == 0, base_key, f, next)) return false;
+  const uint32_t expect = last ? (r + 1 < t.bin_len ? bin_get(img, p0, t, r + 1) : t.rec_end)
+                               : (info[i + 1] & 0xFFFF);
+  return next == expect;
+}
+
+// Interval walk straight from a span (direct path); emit(j, fields).
+template <class Emit>
+__device__ __forceinline__ bool walk_interval(const uint8_t* base, uint32_t p0, const BlockMeta& m, uint32_t r,
+                                              Emit emit) {
+  const TrailerInfo t = trailer_of(m);
   const bool last = r + 1 == t.bin_len;
   const uint32_t start = bin_get(base, p0, t, r);
   const uint32_t stop = last ? t.rec_end : bin_get(base, p0, t, r + 1);
   const uint32_t count = last ? t.item_count - r * t.ri : t.ri;
   if (start > t.rec_end || stop > t.rec_end) return false;
-  Cursor c;
-  c.init(base, p0, start, t.rec_end);
+  uint32_t base_key = 0, pos = start;
   ItemFields f;
-  if (m.type == 1) {
-    if (!parse_index_record(c, f)) return false;
-    emit(r, f);
-  } else {
-    uint32_t base_key = 0;
-    for (uint32_t j = 0; j < count; ++j) {
-      if (!parse_data_record(c, j == 0, base_key, f)) return false;
-      if (j == 0) base_key = f.key_off;
-      emit(r * t.ri + j, f);
-    }
+  for (uint32_t j = 0; j < count; ++j) {
+    uint32_t next;
+    if (!parse_record(base, p0, pos, t, m.type, j == 0, base_key, f, next)) return false;
+    if (j == 0) base_key = f.key_off;
+    emit(r * t.ri + j, f);
+    pos = next;
   }
-  return c.pos == stop;
+  return pos == stop;
 }
 
 // One block straight from HBM (blocks larger than the LDS stage).
-__device__ void decode_block_direct(const DecodeParams& P, uint32_t b, BlockMeta* meta) {
+__device__ __noinline__ void decode_block_direct(const DecodeParams& P, uint32_t b, BlockMeta* meta) {
   const int lane = threadIdx.x;
   const uint64_t off = P.block_off[b], end = P.block_off[b + 1];
   const uint8_t* base = P.blocks + (off & ~15ULL);
@@ -152,15 +229,15 @@ __device__ void decode_block_direct(const DecodeParams& P, uint32_t b, BlockMeta
   const uint64_t item_base = P.item_start[b];
   const uint32_t cap = P.item_start[b + 1] - P.item_start[b];
   if (lane == 0) meta_header(base, hb, len, meta[0]);
-  __syncthreads();
+  wave_sync();
   if (meta[0].st == ST_OK) {
     uint64_t lo, hi;
     xxh3_128_wave(base, hb + kHdrLen, meta[0].len - kHdrLen, &kLongSecret, lo, hi);
     if (lane == 0 && (lo != meta[0].ck_lo || hi != meta[0].ck_hi)) meta[0].st = ST_CKSUM;
   }
-  __syncthreads();
+  wave_sync();
   if (lane == 0) meta_trailer(base, P.expect_type, cap, meta[0]);
-  __syncthreads();
+  wave_sync();
   const BlockMeta m = meta[0];
   if (m.st == ST_OK) {
     bool ok = true;
@@ -170,137 +247,124 @@ __device__ void decode_block_direct(const DecodeParams& P, uint32_t b, BlockMeta
     }
     if (!ok) atomicCAS(&meta[0].st, ST_OK, ST_PARSE);
   }
-  __syncthreads();
+  wave_sync();
   if (lane == 0) P.status[b] = meta[0].st;
-  __syncthreads();
+  wave_sync();
 }
 
+typedef __attribute__((address_space(3))) void lds_void_t;
+typedef const __attribute__((address_space(1))) void gbl_void_t;
+
 __global__ __launch_bounds__(64) void decode_blocks_kernel(DecodeParams P) {
+  // LDS: [meta: kMaxGroup x 64 B][info: u32 per item][bkey: u16 per item][staged bytes]
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   BlockMeta* meta = reinterpret_cast<BlockMeta*>(smem);
-  uint8_t* img = smem + kMetaBytes;
-  const TileView tile = make_tile(img + P.stage_bytes + 64, P.tile_items);
+  uint32_t* info = reinterpret_cast<uint32_t*>(smem + kMetaBytes);
+  uint16_t* bkey = reinterpret_cast<uint16_t*>(smem + kMetaBytes + 4 * P.tile_items);
+  uint8_t* img = smem + kMetaBytes + ((6 * P.tile_items + 15) & ~15u);
   const int lane = threadIdx.x;
   const uint32_t b_begin = blockIdx.x * P.blocks_per_wave;
   const uint32_t b_end = min(b_begin + P.blocks_per_wave, P.n_blocks);
 
   for (uint32_t b = b_begin; b < b_end;) {
-    // ---- group formation: longest run b..b+k-1 fitting stage + tile
-    const uint64_t off_b = P.block_off[b];
-    const uint64_t span0 = off_b & ~15ULL;
-    const uint32_t g_item0 = P.item_start[b];
+    // ---- 1. group formation; lane j keeps block b+j's handle and item range
     const uint32_t bj = b + lane;
-    bool fits = false;
-    if (bj < b_end) {
-      const uint64_t hi = P.block_off[bj + 1];
-      const uint64_t need = ((hi + 15) & ~15ULL) - span0;
-      const uint32_t items = P.item_start[bj + 1] - g_item0;
-      fits = hi >= off_b && need <= P.stage_bytes && items <= P.tile_items;
+    const bool in_run = bj < b_end && (uint32_t)lane < kMaxGroup;
+    uint64_t off_j = 0, end_j = 0;
+    uint32_t it0_j = 0, it1_j = 0;
+    if (in_run) {
+      off_j = P.block_off[bj];
+      end_j = P.block_off[bj + 1];
+      it0_j = P.item_start[bj];
+      it1_j = P.item_start[bj + 1];
     }
+    const uint64_t off_b = wave_bcast_u64(off_j, 0);
+    const uint32_t g_item0 = wave_bcast_u32(it0_j, 0);
+    const uint64_t span0 = off_b & ~15ULL;
+    const bool fits = in_run && end_j >= off_j && off_j >= off_b &&
+                      ((end_j + 15) & ~15ULL) - span0 <= P.stage_bytes && it1_j - g_item0 <= P.tile_items;
     const uint64_t fit_mask = __ballot(fits);
-    const uint32_t k = (fit_mask == ~0ULL) ? 64u : (uint32_t)__builtin_ctzll(~fit_mask);
+    const uint32_t k = (uint32_t)__builtin_ctzll(~fit_mask);  // lanes >= kMaxGroup never fit
     if (k == 0) {
       decode_block_direct(P, b, meta);
       b += 1;
       continue;
     }
-    // ---- stage the run's bytes HBM -> LDS (16 B per lane per step)
+    const uint64_t span1 = (wave_bcast_u64(end_j, k - 1) + 15) & ~15ULL;
+    const uint32_t n_items = wave_bcast_u32(it1_j, k - 1) - g_item0;
+    // ---- 2. stage the group's bytes HBM -> LDS by LDS-DMA, one wait
     {
-      const uint64_t span1 = (P.block_off[b + k] + 15) & ~15ULL;
       const uint32_t chunks = (uint32_t)((span1 - span0) >> 4);
-      const u32x4* __restrict__ src = reinterpret_cast<const u32x4*>(P.blocks + span0);
-      u32x4* dst = reinterpret_cast<u32x4*>(img);
-      uint32_t c = lane;
-      for (; c + 3 * kWave < chunks; c += 4 * kWave) {
-        u32x4 v0 = __builtin_nontemporal_load(src + c);
-        u32x4 v1 = __builtin_nontemporal_load(src + c + kWave);
-        u32x4 v2 = __builtin_nontemporal_load(src + c + 2 * kWave);
-        u32x4 v3 = __builtin_nontemporal_load(src + c + 3 * kWave);
-        dst[c] = v0;
-        dst[c + kWave] = v1;
-        dst[c + 2 * kWave] = v2;
-        dst[c + 3 * kWave] = v3;
+      const uint8_t* src = P.blocks + span0 + 16 * lane;
+      for (uint32_t i = 0; i * kWave < chunks; ++i) {
+        if (i * kWave + lane < chunks)
+          __builtin_amdgcn_global_load_lds((gbl_void_t*)(src + 1024 * i), (lds_void_t*)(img + 1024 * i), 16, 0, 0);
       }
-      for (; c < chunks; c += kWave) dst[c] = __builtin_nontemporal_load(src + c);
+      for (uint32_t i = lane; i < n_items; i += kWave) info[i] = kNoItem;
+      __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0): the DMA has landed
+      wave_sync();
     }
-    __syncthreads();
-    // ---- lane j: header of block b+j
+    // ---- 3. lane j: header of block b+j
     if ((uint32_t)lane < k) {
-      const uint64_t off = P.block_off[b + lane], end = P.block_off[b + lane + 1];
       BlockMeta m;
-      meta_header(img, (uint32_t)(off - span0), end - off, m);
-      m.item0 = P.item_start[b + lane] - g_item0;
+      meta_header(img, (uint32_t)(off_j - span0), end_j - off_j, m);
+      m.item0 = it0_j - g_item0;
       meta[lane] = m;
     }
-    __syncthreads();
-    // ---- payload checksums, one block at a time, whole wave
-    for (uint32_t j = 0; j < k; ++j) {
-      if (meta[j].st != ST_OK) continue;
-      const uint32_t hb = meta[j].hb, len = meta[j].len;
-      uint64_t lo, hi;
-      xxh3_128_wave(img, hb + kHdrLen, len - kHdrLen, &kLongSecret, lo, hi);
-      if (lane == 0 && (lo != meta[j].ck_lo || hi != meta[j].ck_hi)) meta[j].st = ST_CKSUM;
+    wave_sync();
+    // ---- 4. payload checksums: DPP row g hashes blocks g, g+4, ...
+    if (!(P.flags & kDiagSkipHash)) {
+      const uint32_t g = lane >> 4;
+      for (uint32_t j = g; j < k; j += 4) {
+        if (meta[j].st != ST_OK) continue;
+        const uint32_t hb = meta[j].hb, len = meta[j].len;
+        uint64_t lo, hi;
+        xxh3_128_row(img, hb + kHdrLen, len - kHdrLen, lo, hi);
+        if ((lane & 15) == 0 && (lo != meta[j].ck_lo || hi != meta[j].ck_hi)) meta[j].st = ST_CKSUM;
+      }
+      wave_sync();
     }
-    __syncthreads();
-    // ---- trailers + interval prefix
+    // ---- 5. trailers + restart-interval numbering
     uint32_t chains = 0;
     if ((uint32_t)lane < k) {
       BlockMeta m = meta[lane];
-      const uint32_t cap = P.item_start[b + lane + 1] - P.item_start[b + lane];
-      meta_trailer(img, P.expect_type, cap, m);
+      meta_trailer(img, P.expect_type, it1_j - it0_j, m);
       chains = m.st == ST_OK ? m.bin_len : 0;
+      m.chain0 = 0;
       meta[lane] = m;
     }
     const uint32_t incl = wave_incl_scan_u32(chains);
-    const uint32_t total = wave_bcast_u32(incl, 63);
+    const uint32_t total = (P.flags & kDiagSkipParse) ? 0 : wave_bcast_u32(incl, 63);
     if ((uint32_t)lane < k) meta[lane].chain0 = incl - chains;
-    __syncthreads();
-    // ---- walk restart intervals: lane = (block, interval)
+    wave_sync();
+    // ---- 6. phase A: lane = restart interval, record boundaries only
     for (uint32_t c = lane; c < total; c += kWave) {
       uint32_t lo = 0, hi = k - 1;
       while (lo < hi) {
         const uint32_t mid = (lo + hi + 1) >> 1;
         if (meta[mid].chain0 <= c) lo = mid; else hi = mid - 1;
       }
-      const BlockMeta& mm = meta[lo];
-      const uint32_t r = c - mm.chain0;
-      const uint32_t item0 = mm.item0;
-      bool ok;
-      if (mm.type == 1 && P.out.handle_off) {
-        const uint64_t gbase = (uint64_t)g_item0 + item0;
-        ok = walk_interval(img, mm.hb + kHdrLen, mm, r, [&](uint32_t j, const ItemFields& f) {
-          emit_tile(tile, item0 + j, f);
-          P.out.handle_off[gbase + j] = f.handle_off;
-        });
-      } else {
-        ok = walk_interval(img, mm.hb + kHdrLen, mm, r,
-                           [&](uint32_t j, const ItemFields& f) { emit_tile(tile, item0 + j, f); });
+      const uint32_t j = lo;
+      if (!walk_boundaries(img, meta[j], j, c - meta[j].chain0, info, bkey)) atomicCAS(&meta[j].st, ST_OK, ST_PARSE);
+    }
+    wave_sync();
+    // ---- 7. phase B: lane = record; full parse + validation; coalesced stores
+    const uint32_t parse_items = (P.flags & kDiagSkipParse) ? 0 : n_items;
+    const bool store = !(P.flags & kDiagSkipStore);
+    for (uint32_t i = lane; i < parse_items; i += kWave) {
+      const uint32_t inf = info[i];
+      if (inf == kNoItem) continue;
+      const uint32_t j = (inf >> 16) & 31;
+      ItemFields f;
+      if (!parse_item(img, meta[j], i, inf, info, bkey, f)) {
+        atomicCAS(&meta[j].st, ST_OK, ST_PARSE);
+        continue;
       }
-      if (!ok) atomicCAS(&meta[lo].st, ST_OK, ST_PARSE);
+      if (store) emit_global(P.out, (uint64_t)g_item0 + i, f);
     }
-    __syncthreads();
-    // ---- data-block handle_off (documented as 0 for data items)
-    if (P.out.handle_off) {
-      for (uint32_t j = 0; j < k; ++j) {
-        if (meta[j].type == 1) continue;
-        const uint32_t n0 = meta[j].item0, n1 = j + 1 < k ? meta[j + 1].item0 : P.item_start[b + k] - g_item0;
-        for (uint32_t i = n0 + lane; i < n1; i += kWave) P.out.handle_off[(uint64_t)g_item0 + i] = 0;
-      }
-    }
-    // ---- tile -> HBM, coalesced per field
-    {
-      const uint32_t n = P.item_start[b + k] - g_item0;
-      const uint64_t g0 = g_item0;
-      if (P.out.seqno) for (uint32_t i = lane; i < n; i += kWave) P.out.seqno[g0 + i] = tile.seqno[i];
-      if (P.out.key_off) for (uint32_t i = lane; i < n; i += kWave) P.out.key_off[g0 + i] = tile.key_off[i];
-      if (P.out.val_off) for (uint32_t i = lane; i < n; i += kWave) P.out.val_off[g0 + i] = tile.val_off[i];
-      if (P.out.val_len) for (uint32_t i = lane; i < n; i += kWave) P.out.val_len[g0 + i] = tile.val_len[i];
-      if (P.out.key_len) for (uint32_t i = lane; i < n; i += kWave) P.out.key_len[g0 + i] = tile.key_len[i];
-      if (P.out.prefix_len) for (uint32_t i = lane; i < n; i += kWave) P.out.prefix_len[g0 + i] = tile.prefix_len[i];
-      if (P.out.vtype) for (uint32_t i = lane; i < n; i += kWave) P.out.vtype[g0 + i] = tile.vtype[i];
-    }
+    wave_sync();
     if ((uint32_t)lane < k) P.status[b + lane] = meta[lane].st;
-    __syncthreads();
+    wave_sync();
     b += k;
   }
 }
@@ -338,7 +402,8 @@ size_t decode_workspace_size(uint32_t n_blocks) {
 }
 
 uint32_t decode_lds_bytes(uint32_t stage_bytes, uint32_t tile_items) {
-  return kMetaBytes + stage_bytes + 64 + tile_bytes(tile_items);
+  // the last DMA instruction of a group may land up to 1008 B past the span
+  return kMetaBytes + ((6 * tile_items + 15) & ~15u) + ((stage_bytes + 1023) & ~1023u) + 64;
 }
 
 hipError_t launch_decode(const DecodeParams& P0, void* ws, hipStream_t st) {

@@ -362,6 +362,35 @@ __device__ __forceinline__ void stripe_part(const Win16& w, uint64_t k0, uint64_
   c1 += (uint64_t)(uint32_t)x1 * (x1 >> 32) + w.lo;  // acc[w1] += mul(k1) ; acc[w1] (=w0^1) += v0
 }
 
+// Sum of v over the 16 lanes that share (lane & 3): two DPP row rotates
+// (within each 16-lane row) + gfx950 v_permlane16_swap / v_permlane32_swap
+// (across rows) — all VALU, no LDS round trips.
+__device__ __forceinline__ uint32_t dpp_ror4(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x124, 0xF, 0xF, false);
+}
+__device__ __forceinline__ uint32_t dpp_ror8(uint32_t x) {
+  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x128, 0xF, 0xF, false);
+}
+__device__ __forceinline__ uint64_t quad_group_sum64(uint64_t v) {
+  uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+  v += (uint64_t)dpp_ror4(lo) | ((uint64_t)dpp_ror4(hi) << 32);
+  lo = (uint32_t)v; hi = (uint32_t)(v >> 32);
+  v += (uint64_t)dpp_ror8(lo) | ((uint64_t)dpp_ror8(hi) << 32);
+  lo = (uint32_t)v; hi = (uint32_t)(v >> 32);
+  {
+    const auto a = __builtin_amdgcn_permlane16_swap(lo, lo, false, false);
+    const auto b = __builtin_amdgcn_permlane16_swap(hi, hi, false, false);
+    v = ((uint64_t)a[0] | ((uint64_t)b[0] << 32)) + ((uint64_t)a[1] | ((uint64_t)b[1] << 32));
+  }
+  lo = (uint32_t)v; hi = (uint32_t)(v >> 32);
+  {
+    const auto a = __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+    const auto b = __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    v = ((uint64_t)a[0] | ((uint64_t)b[0] << 32)) + ((uint64_t)a[1] | ((uint64_t)b[1] << 32));
+  }
+  return v;
+}
+
 // XXH3-128 of base[pos .. pos+len), len > 240, computed by the whole wave
 // (all 64 lanes must call it with identical arguments).  `base` 16-aligned.
 __device__ __forceinline__ void xxh3_128_wave_long(const uint8_t* base, uint32_t pos, uint32_t len,
@@ -376,19 +405,32 @@ __device__ __forceinline__ void xxh3_128_wave_long(const uint8_t* base, uint32_t
   uint64_t a1 = q == 0 ? P64_1 : q == 1 ? P64_3 : q == 2 ? (uint64_t)P32_2 : (uint64_t)P32_1;
   const uint64_t scr0 = ls->acc[16 + 2 * q], scr1 = ls->acc[16 + 2 * q + 1];  // secret + 128
   const uint32_t nb_blocks = (len - 1) / 1024;
-  for (uint32_t n = 0; n < nb_blocks; ++n) {
-    Win16 w = read_win16(base, pos + n * 1024 + 16 * lane);
+  // The per-KiB contributions do not depend on the accumulators, so two
+  // KiB blocks are loaded and reduced together; only the scramble is serial.
+  uint32_t n = 0;
+  for (; n + 2 <= nb_blocks; n += 2) {
+    const Win16 wa = read_win16(base, pos + n * 1024 + 16 * lane);
+    const Win16 wb = read_win16(base, pos + (n + 1) * 1024 + 16 * lane);
+    uint64_t c0 = 0, c1 = 0, d0 = 0, d1 = 0;
+    stripe_part(wa, k0, k1, c0, c1);
+    stripe_part(wb, k0, k1, d0, d1);
+    c0 = quad_group_sum64(c0);
+    c1 = quad_group_sum64(c1);
+    d0 = quad_group_sum64(d0);
+    d1 = quad_group_sum64(d1);
+    a0 += c0; a0 ^= a0 >> 47; a0 ^= scr0; a0 *= P32_1;
+    a1 += c1; a1 ^= a1 >> 47; a1 ^= scr1; a1 *= P32_1;
+    a0 += d0; a0 ^= a0 >> 47; a0 ^= scr0; a0 *= P32_1;
+    a1 += d1; a1 ^= a1 >> 47; a1 ^= scr1; a1 *= P32_1;
+  }
+  if (n < nb_blocks) {
+    const Win16 w = read_win16(base, pos + n * 1024 + 16 * lane);
     uint64_t c0 = 0, c1 = 0;
     stripe_part(w, k0, k1, c0, c1);
-#pragma unroll
-    for (int m = 4; m < 64; m <<= 1) {
-      c0 += shfl_xor64(c0, m);
-      c1 += shfl_xor64(c1, m);
-    }
-    a0 += c0;
-    a1 += c1;
-    a0 ^= a0 >> 47; a0 ^= scr0; a0 *= P32_1;
-    a1 ^= a1 >> 47; a1 ^= scr1; a1 *= P32_1;
+    c0 = quad_group_sum64(c0);
+    c1 = quad_group_sum64(c1);
+    a0 += c0; a0 ^= a0 >> 47; a0 ^= scr0; a0 *= P32_1;
+    a1 += c1; a1 ^= a1 >> 47; a1 ^= scr1; a1 *= P32_1;
   }
   {
     const uint32_t tail0 = nb_blocks * 1024;
@@ -402,13 +444,8 @@ __device__ __forceinline__ void xxh3_128_wave_long(const uint8_t* base, uint32_t
       Win16 w = read_win16(base, pos + len - 64 + 16 * lane);
       stripe_part(w, ls->last[2 * q], ls->last[2 * q + 1], c0, c1);
     }
-#pragma unroll
-    for (int m = 4; m < 64; m <<= 1) {
-      c0 += shfl_xor64(c0, m);
-      c1 += shfl_xor64(c1, m);
-    }
-    a0 += c0;
-    a1 += c1;
+    a0 += quad_group_sum64(c0);
+    a1 += quad_group_sum64(c1);
   }
   // mergeAccs: lane pair q holds acc[2q], acc[2q+1]
   uint64_t tlo = mul_fold64(a0 ^ ls->mlo[2 * q], a1 ^ ls->mlo[2 * q + 1]);
@@ -436,6 +473,90 @@ struct BaseReader64 {
     return (uint64_t)alignbyte(d1, d0, s) | ((uint64_t)alignbyte(d2, d1, s) << 32);
   }
 };
+
+// Row-cooperative XXH3-128 (> 240 B): the 16 lanes of one DPP row hash one
+// input, so a wave hashes four blocks at once.  Lane r = lane & 15 owns bytes
+// [256t + 16r, +16) of each KiB block (t = 0..3): stripe 4t + (r >> 2),
+// accumulator pair q = r & 3.  The per-KiB reduction is two DPP row rotates.
+__device__ __forceinline__ uint64_t row_quad_sum64(uint64_t v) {
+  uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+  v += (uint64_t)dpp_ror4(lo) | ((uint64_t)dpp_ror4(hi) << 32);
+  lo = (uint32_t)v; hi = (uint32_t)(v >> 32);
+  v += (uint64_t)dpp_ror8(lo) | ((uint64_t)dpp_ror8(hi) << 32);
+  return v;
+}
+// sum over the 4 lanes of each quad (DPP quad_perm [1,0,3,2] then [2,3,0,1])
+__device__ __forceinline__ uint64_t quad_sum64(uint64_t v) {
+  uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
+  v += (uint64_t)(uint32_t)__builtin_amdgcn_update_dpp(0, (int)lo, 0xB1, 0xF, 0xF, false) |
+       ((uint64_t)(uint32_t)__builtin_amdgcn_update_dpp(0, (int)hi, 0xB1, 0xF, 0xF, false) << 32);
+  lo = (uint32_t)v; hi = (uint32_t)(v >> 32);
+  v += (uint64_t)(uint32_t)__builtin_amdgcn_update_dpp(0, (int)lo, 0x4E, 0xF, 0xF, false) |
+       ((uint64_t)(uint32_t)__builtin_amdgcn_update_dpp(0, (int)hi, 0x4E, 0xF, 0xF, false) << 32);
+  return v;
+}
+
+__device__ __forceinline__ void xxh3_128_row_long(const uint8_t* base, uint32_t pos, uint32_t len,
+                                                  const LongSecret* __restrict__ ls, uint64_t& out_lo,
+                                                  uint64_t& out_hi) {
+  const int r = threadIdx.x & 15;
+  const int q = r & 3, s = r >> 2;
+  uint64_t k0[4], k1[4];
+#pragma unroll
+  for (int t = 0; t < 4; ++t) {
+    k0[t] = ls->acc[4 * t + s + 2 * q];
+    k1[t] = ls->acc[4 * t + s + 2 * q + 1];
+  }
+  uint64_t a0 = q == 0 ? (uint64_t)P32_3 : q == 1 ? P64_2 : q == 2 ? P64_4 : P64_5;
+  uint64_t a1 = q == 0 ? P64_1 : q == 1 ? P64_3 : q == 2 ? (uint64_t)P32_2 : (uint64_t)P32_1;
+  const uint64_t scr0 = ls->acc[16 + 2 * q], scr1 = ls->acc[16 + 2 * q + 1];
+  const uint32_t nb_blocks = (len - 1) / 1024;
+  for (uint32_t n = 0; n < nb_blocks; ++n) {
+    Win16 w[4];
+#pragma unroll
+    for (int t = 0; t < 4; ++t) w[t] = read_win16(base, pos + n * 1024 + 256 * t + 16 * r);
+    uint64_t c0 = 0, c1 = 0;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) stripe_part(w[t], k0[t], k1[t], c0, c1);
+    c0 = row_quad_sum64(c0);
+    c1 = row_quad_sum64(c1);
+    a0 += c0; a0 ^= a0 >> 47; a0 ^= scr0; a0 *= P32_1;
+    a1 += c1; a1 ^= a1 >> 47; a1 ^= scr1; a1 *= P32_1;
+  }
+  {
+    const uint32_t tail0 = nb_blocks * 1024;
+    const uint32_t nb_stripes = ((len - 1) - tail0) / 64;
+    uint64_t c0 = 0, c1 = 0;
+#pragma unroll
+    for (int t = 0; t < 4; ++t) {
+      if ((uint32_t)(4 * t + s) < nb_stripes) {
+        const Win16 w = read_win16(base, pos + tail0 + 256 * t + 16 * r);
+        stripe_part(w, k0[t], k1[t], c0, c1);
+      }
+    }
+    if (r < 4) {  // last stripe: input[len-64 .. len), secret + 121
+      const Win16 w = read_win16(base, pos + len - 64 + 16 * r);
+      stripe_part(w, ls->last[2 * q], ls->last[2 * q + 1], c0, c1);
+    }
+    a0 += row_quad_sum64(c0);
+    a1 += row_quad_sum64(c1);
+  }
+  uint64_t tlo = mul_fold64(a0 ^ ls->mlo[2 * q], a1 ^ ls->mlo[2 * q + 1]);
+  uint64_t thi = mul_fold64(a0 ^ ls->mhi[2 * q], a1 ^ ls->mhi[2 * q + 1]);
+  tlo = quad_sum64(tlo);
+  thi = quad_sum64(thi);
+  out_lo = xxh3_avalanche((uint64_t)len * P64_1 + tlo);
+  out_hi = xxh3_avalanche(~((uint64_t)len * P64_2) + thi);
+}
+
+__device__ __forceinline__ void xxh3_128_row(const uint8_t* base, uint32_t pos, uint32_t len,
+                                             uint64_t& lo, uint64_t& hi) {
+  if (len > 240) {
+    xxh3_128_row_long(base, pos, len, &kLongSecret, lo, hi);
+  } else {
+    xxh3_128_short(len, BaseReader8{base, pos}, BaseReader64{base, pos}, lo, hi);
+  }
+}
 
 // XXH3-128 of base[pos..pos+len) for any len: long inputs use the whole wave
 // (wave-uniform len required), short inputs are computed by every lane
