@@ -145,112 +145,93 @@ __device__ __forceinline__ uint64_t leb_val8(uint64_t x, uint32_t n) {  // n in 
   return x;
 }
 
-// Returns 1 = parsed (next = position after the record), 0 = take the Cursor
-// path, -1 = malformed (same outcomes as oracle parse_data_item).
+__device__ __forceinline__ uint32_t ctz64(uint64_t t) {  // 64 for t == 0
+  return t ? (uint32_t)__builtin_ctzll(t) : 64u;
+}
+
+// Record shape decoded from the 32-byte window at its start.  Branch-free:
+// every field is computed unconditionally and classified once
+// (cls: 0 = fast shape, 1 = needs the Cursor path, 2 = malformed).
+struct RecShape {
+  uint32_t vt, hdr, klen, q, n4, vl, cls;
+  uint64_t seq, shared;
+};
+__device__ __forceinline__ RecShape rec_shape(const Win32& w, bool restart, bool want_values) {
+  RecShape r;
+  const uint64_t lo = w.w0;
+  r.vt = (uint32_t)(lo & 0xFF);
+  const bool vt_ok = r.vt <= 4 && r.vt != 3;
+  const bool tomb = r.vt == 1 || r.vt == 2;
+  // varint terminators (MSB clear) among bytes 1..7: seqno, [shared], key length
+  const uint64_t t1 = ~lo & 0x8080808080808000ULL;
+  const uint32_t e1 = ctz64(t1);
+  const uint64_t t2 = t1 & (t1 - 1);
+  const uint32_t e2 = restart ? e1 : ctz64(t2);
+  const uint64_t t3 = restart ? t2 : t2 & (t2 - 1);
+  const uint32_t e3 = ctz64(t3);
+  const bool hdr_ok = t3 != 0 && e3 - e2 == 8;  // header within 8 bytes, 1-byte key length
+  const uint32_t sh3 = hdr_ok ? e3 - 7 : 0;
+  r.klen = (uint32_t)(lo >> sh3) & 0x7F;
+  r.hdr = (e3 >> 3) + 1;
+  r.q = r.hdr + r.klen;
+  r.seq = 0;
+  r.shared = 0;
+  if (want_values && hdr_ok) {
+    const uint32_t n1 = e1 >> 3;  // seqno bytes (1..7)
+    r.seq = leb_val8(lo >> 8, n1);
+    if (!restart) r.shared = leb_val8(lo >> (e1 + 1), (e2 - e1) >> 3);
+  }
+  // value length (1-2 byte varint) from the window when it lies inside it
+  const bool in_win = r.q <= 24;
+  const uint64_t z = win_at(w, in_win ? r.q : 24);
+  const bool two = (z & 0x80) != 0;
+  const bool vl_ok = tomb || (in_win && (z & 0x8080) != 0x8080);
+  r.n4 = tomb ? 0 : (two ? 2 : 1);
+  r.vl = tomb ? 0 : (two ? ((uint32_t)(z & 0x7F) | ((uint32_t)(z >> 1) & 0x3F80)) : (uint32_t)(z & 0x7F));
+  const bool shared_ok = restart || ((e2 - e1) >> 3) <= 3;
+  r.cls = !vt_ok ? 2u : ((hdr_ok && vl_ok && shared_ok) ? 0u : 1u);
+  return r;
+}
+
+// Full record parse (decode phase B).  Returns 1 = parsed, 0 = Cursor path,
+// -1 = malformed (same outcomes as oracle parse_data_item).
 __device__ __forceinline__ int parse_data_fast(const uint8_t* base, uint32_t p0, uint32_t pos, uint32_t end,
                                                bool restart, uint32_t base_key_off, ItemFields& f,
                                                uint32_t& next) {
   if (pos >= end) return -1;
   const Win32 w = read_win32(base, p0 + pos);
-  const uint32_t vt = (uint32_t)(w.w0 & 0xFF);
-  if (!valid_vtype(vt)) return -1;  // includes the 0xFF marker inside an interval
-  const uint64_t x = win_at(w, 1);
-  const uint32_t n1 = leb_len8(x);
-  if (n1 > 7) return 0;
-  const uint64_t seq = leb_val8(x, n1);
-  uint32_t o = 1 + n1;
-  uint64_t y = win_at(w, o);
-  uint64_t shared = 0;
-  if (!restart) {
-    const uint32_t n2 = leb_len8(y);
-    if (n2 > 3) return -1;
-    shared = leb_val8(y, n2) & 0xFFFF;
-    y >>= 8 * n2;
-    o += n2;
-  }
-  const uint32_t n3 = leb_len8(y);
-  if (n3 > 3) return -1;
-  const uint32_t klen = (uint32_t)(leb_val8(y, n3) & 0xFFFF);
-  o += n3;
-  if (pos + o > end) return -1;  // a header byte at/after the record area end
-  if (!restart && (uint64_t)base_key_off + shared > end) return -1;
-  const uint32_t q = o + klen;
-  if ((uint64_t)pos + q > end) return -1;
-  uint64_t vl = 0;
-  uint32_t n4 = 0;
-  if (!is_tombstone(vt)) {
-    uint64_t z;
-    if (q <= 24) {
-      z = win_at(w, q);
-    } else {
-      z = read_win16(base, p0 + pos + q).lo;
-    }
-    n4 = leb_len8(z);
-    if (n4 > 5) return -1;
-    vl = leb_val8(z, n4) & 0xFFFFFFFFULL;
-    if (pos + q + n4 > end) return -1;
-  }
-  const uint32_t val_off = pos + q + n4;
-  if ((uint64_t)val_off + vl > end) return -1;
-  f.seqno = seq;
+  const RecShape r = rec_shape(w, restart, true);
+  if (r.cls == 2) return -1;
+  if (r.cls == 1) return 0;
+  const uint32_t val_off = pos + r.q + r.n4;
+  const bool bad = (pos + r.hdr > end) || (!restart && (uint64_t)base_key_off + r.shared > end) ||
+                   ((uint64_t)pos + r.q > end) || (r.n4 && pos + r.q + r.n4 > end) ||
+                   ((uint64_t)val_off + r.vl > end);
+  f.seqno = r.seq;
   f.handle_off = 0;
-  f.key_off = pos + o;
-  f.key_len = (uint16_t)klen;
-  f.prefix_len = (uint16_t)shared;
+  f.key_off = pos + r.hdr;
+  f.key_len = (uint16_t)r.klen;
+  f.prefix_len = (uint16_t)r.shared;
   f.val_off = val_off;
-  f.val_len = (uint32_t)vl;
-  f.vtype = (uint8_t)vt;
-  next = val_off + (uint32_t)vl;
-  return 1;
+  f.val_len = r.vl;
+  f.vtype = (uint8_t)r.vt;
+  next = val_off + r.vl;
+  return bad ? -1 : 1;
 }
 
 // Record boundary only (decode phase A): the serial walk of a restart
-// interval needs nothing but each record's length.  Varint boundaries come
-// from the terminator bit mask (~bytes & 0x80) by repeatedly clearing the
-// lowest set bit; values are only materialised for the key length (1 byte)
-// and the value length (1-2 bytes).  Other shapes return 0 (Cursor path).
-// -1 = malformed in a way the oracle also rejects.  key_off is valid on 1.
+// interval needs nothing but each record's length.  1 = next/key_off valid,
+// 0 = Cursor path, -1 = malformed in a way the oracle also rejects.
 __device__ __forceinline__ int data_record_next_fast(const uint8_t* base, uint32_t p0, uint32_t p, uint32_t end,
                                                      bool restart, uint32_t& next, uint32_t& key_off) {
   if (p >= end) return -1;
   const Win32 w = read_win32(base, p0 + p);
-  const uint64_t lo = w.w0;
-  const uint32_t vt = (uint32_t)(lo & 0xFF);
-  if (!valid_vtype(vt)) return -1;
-  uint64_t t = ~lo & 0x8080808080808000ULL;  // varint terminators in bytes 1..7
-  if (!t) return 0;
-  const uint32_t e1 = (uint32_t)__builtin_ctzll(t);  // seqno
-  t &= t - 1;
-  uint32_t e2 = e1;
-  if (!restart) {                                    // shared prefix length
-    if (!t) return 0;
-    e2 = (uint32_t)__builtin_ctzll(t);
-    t &= t - 1;
-  }
-  if (!t) return 0;
-  const uint32_t e3 = (uint32_t)__builtin_ctzll(t);  // key (suffix) length
-  if (e3 - e2 != 8) return 0;                        // multi-byte key length
-  const uint32_t klen = (uint32_t)(lo >> (e3 - 7)) & 0x7F;
-  const uint32_t h = (e3 >> 3) + 1;
-  key_off = p + h;
-  const uint32_t q = h + klen;
-  if (is_tombstone(vt)) {
-    next = p + q;
-    return 1;
-  }
-  if (p + q >= end) return -1;  // the value length byte must precede the record area end
-  const uint64_t z = q <= 24 ? win_at(w, q) : read_win16(base, p0 + p + q).lo;
-  uint32_t vl;
-  if (!(z & 0x80)) {
-    vl = (uint32_t)(z & 0x7F);
-    next = p + q + 1 + vl;
-  } else if (!(z & 0x8000)) {
-    vl = (uint32_t)(z & 0x7F) | ((uint32_t)(z >> 1) & 0x3F80);
-    next = p + q + 2 + vl;
-  } else {
-    return 0;
-  }
-  return 1;
+  const RecShape r = rec_shape(w, restart, false);
+  key_off = p + r.hdr;
+  next = p + r.q + r.n4 + r.vl;
+  if (r.cls == 2) return -1;
+  if (r.cls == 1) return 0;
+  return (r.n4 && p + r.q >= end) ? -1 : 1;
 }
 
 // KeyedBlockHandle::parse_full, src/table/index_block/block_handle.rs:175-206.

@@ -30,7 +30,8 @@ namespace lsmgpu {
 
 // Diagnostic-only flags (lsm_decode_tuning.flags high bits): drop one phase to
 // price it in a profile.  Outputs are NOT valid with any of them set.
-constexpr uint32_t kDiagSkipHash = 0x100, kDiagSkipParse = 0x200, kDiagSkipStore = 0x400;
+constexpr uint32_t kDiagSkipHash = 0x100, kDiagSkipParse = 0x200, kDiagSkipStore = 0x400,
+                   kDiagSkipPhaseB = 0x800;
 
 constexpr uint32_t kMaxGroup = 32;  // blocks per staged group
 constexpr uint32_t kNoItem = 0xFFFFFFFFu;
@@ -349,7 +350,9 @@ __global__ __launch_bounds__(64) void decode_blocks_kernel(DecodeParams P) {
     }
     wave_sync();
     // ---- 7. phase B: lane = record; full parse + validation; coalesced stores
-    const uint32_t parse_items = (P.flags & kDiagSkipParse) ? 0 : n_items;
+    const uint32_t parse_items = (P.flags & (kDiagSkipParse | kDiagSkipPhaseB)) ? 0 : n_items;
+    const bool all_fields = P.out.seqno && P.out.key_off && P.out.val_off && P.out.val_len && P.out.key_len &&
+                            P.out.prefix_len && P.out.vtype;
     const bool store = !(P.flags & kDiagSkipStore);
     for (uint32_t i = lane; i < parse_items; i += kWave) {
       const uint32_t inf = info[i];
@@ -360,7 +363,20 @@ __global__ __launch_bounds__(64) void decode_blocks_kernel(DecodeParams P) {
         atomicCAS(&meta[j].st, ST_OK, ST_PARSE);
         continue;
       }
-      if (store) emit_global(P.out, (uint64_t)g_item0 + i, f);
+      if (!store) continue;
+      const uint64_t gi = (uint64_t)g_item0 + i;
+      if (all_fields) {  // common case: no per-field null checks
+        P.out.seqno[gi] = f.seqno;
+        P.out.key_off[gi] = f.key_off;
+        P.out.val_off[gi] = f.val_off;
+        P.out.val_len[gi] = f.val_len;
+        P.out.key_len[gi] = f.key_len;
+        P.out.prefix_len[gi] = f.prefix_len;
+        P.out.vtype[gi] = f.vtype;
+        if (P.out.handle_off) P.out.handle_off[gi] = f.handle_off;
+      } else {
+        emit_global(P.out, gi, f);
+      }
     }
     wave_sync();
     if ((uint32_t)lane < k) P.status[b + lane] = meta[lane].st;

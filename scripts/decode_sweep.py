@@ -28,7 +28,7 @@ def main():
     ap.add_argument("--blocks", type=int, default=1 << 20)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--tunings", default="32,16384,384;32,8192,192;32,12288,256;32,24576,640;32,32768,768;16,16384,384;64,16384,384")
+    ap.add_argument("--tunings", default="32,16384,384;32,8192,192;32,12288,256;32,24576,640;16,16384,384")
     ap.add_argument("--ablate", default="32,16384,384")
     ap.add_argument("--workload", default="counter", choices=["counter", "prefix16k"])
     args = ap.parse_args()
@@ -55,6 +55,7 @@ def main():
     variants["ablate no-hash"] = a + (1 | SKIP_HASH,)
     variants["ablate no-parse"] = a + (1 | SKIP_PARSE,)
     variants["ablate no-store"] = a + (1 | SKIP_STORE,)
+    variants["ablate phase-A only"] = a + (1 | 0x800,)
     variants["ablate stage-only"] = a + (1 | SKIP_HASH | SKIP_PARSE | SKIP_STORE,)
     times = {k: [] for k in variants}
     for _ in range(args.rounds):
