@@ -86,8 +86,9 @@ int lsm_decode_blocks_tuned(const uint8_t* d_blocks, const uint64_t* d_block_off
   P.tile_items = (tuning && tuning->tile_items) ? tuning->tile_items : kDefaultTileItems;
   P.flags = tuning ? tuning->flags : 0;
   P.stage_bytes = (P.stage_bytes + 15) & ~15u;
-  if (P.tile_items > 8192 || P.stage_bytes < 256 || P.stage_bytes > 65536) return LSM_BAD_ARG;
-  const uint32_t lds = lsmgpu::decode_lds_bytes(P.stage_bytes, P.tile_items);
+  if (P.tile_items > 8192 || P.stage_bytes < 256 || P.stage_bytes > 65536 || P.blocks_per_wave > 63)
+    return LSM_BAD_ARG;
+  const uint32_t lds = lsmgpu::decode_lds_bytes(P.stage_bytes, P.tile_items, P.blocks_per_wave);
   if (lds > 160 * 1024) return LSM_BAD_ARG;
   hipError_t e = lsmgpu::launch_decode(P, d_workspace, (hipStream_t)stream);
   return e == hipSuccess ? LSM_OK : set_hip_error(e, "lsm_decode_blocks");

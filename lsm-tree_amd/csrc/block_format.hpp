@@ -106,36 +106,23 @@ __device__ __forceinline__ bool parse_data_record(Cursor& c, bool restart, uint3
 }
 
 // ---------------------------------------------------------------- fast path
-// One aligned 36-byte LDS/HBM read burst gives a 32-byte register window at
-// the record start; the record header (vtype, seqno <= 7 LEB bytes, shared,
-// rest/key_len) and, for short keys, the value-length varint are decoded from
-// registers with bit tricks (no per-byte loop).  Anything outside that shape
-// (seqno >= 2^49, long key before the value length) falls back to Cursor.
-struct Win32 {
-  uint64_t w0, w1, w2, w3;
-};
-__device__ __forceinline__ Win32 read_win32(const uint8_t* base, uint32_t pos) {
-  const uint32_t a = pos & ~3u, s = pos & 3u;
-  uint32_t d[9];
-#pragma unroll
-  for (int k = 0; k < 9; ++k) d[k] = ld32(base, a + 4 * k);
-  uint32_t e[8];
-#pragma unroll
-  for (int k = 0; k < 8; ++k) e[k] = alignbyte(d[k + 1], d[k], s);
-  return {(uint64_t)e[0] | ((uint64_t)e[1] << 32), (uint64_t)e[2] | ((uint64_t)e[3] << 32),
-          (uint64_t)e[4] | ((uint64_t)e[5] << 32), (uint64_t)e[6] | ((uint64_t)e[7] << 32)};
+// The common record header (vtype, seqno <= 7 LEB bytes, shared <= 3 LEB
+// bytes, 1-byte key length) lies in the 8 bytes at the record start: one
+// unaligned 64-bit load (gfx950 serves unaligned ds_read_b64 and
+// global_load_dwordx2) decoded with bit tricks, then one dependent 16-bit load
+// at start + header + key length for a 1-2 byte value length.  Any other shape
+// (seqno >= 2^49, key length >= 128, value length >= 2^14) takes the Cursor.
+// Loads may run up to 138 bytes past the record start; callers guarantee that
+// many readable bytes (LDS stage padding) or clamp (see parse_data_fast).
+__device__ __forceinline__ uint64_t ld_u64u(const uint8_t* p) {
+  uint64_t v;
+  __builtin_memcpy(&v, p, 8);
+  return v;
 }
-// bytes o..o+7 of the window (o <= 24)
-__device__ __forceinline__ uint64_t win_at(const Win32& w, uint32_t o) {
-  const uint32_t q = o >> 3, k = (o & 7) << 3;
-  const uint64_t a = q == 0 ? w.w0 : q == 1 ? w.w1 : q == 2 ? w.w2 : w.w3;
-  const uint64_t b = q == 0 ? w.w1 : q == 1 ? w.w2 : q == 2 ? w.w3 : 0;
-  return k ? (a >> k) | (b << (64 - k)) : a;
-}
-// LEB128 length within 8 bytes (9 = not terminated)
-__device__ __forceinline__ uint32_t leb_len8(uint64_t x) {
-  const uint64_t t = ~x & 0x8080808080808080ULL;
-  return t ? (uint32_t)(__builtin_ctzll(t) >> 3) + 1 : 9;
+__device__ __forceinline__ uint32_t ld_u16u(const uint8_t* p) {
+  uint16_t v;
+  __builtin_memcpy(&v, p, 2);
+  return v;
 }
 __device__ __forceinline__ uint64_t leb_val8(uint64_t x, uint32_t n) {  // n in 1..8
   if (n < 8) x &= (1ULL << (8 * n)) - 1;
@@ -144,94 +131,102 @@ __device__ __forceinline__ uint64_t leb_val8(uint64_t x, uint32_t n) {  // n in 
   x = ((x & 0x0FFFFFFF00000000ULL) >> 4) | (x & 0x000000000FFFFFFFULL);
   return x;
 }
-
 __device__ __forceinline__ uint32_t ctz64(uint64_t t) {  // 64 for t == 0
   return t ? (uint32_t)__builtin_ctzll(t) : 64u;
 }
 
-// Record shape decoded from the 32-byte window at its start.  Branch-free:
-// every field is computed unconditionally and classified once
-// (cls: 0 = fast shape, 1 = needs the Cursor path, 2 = malformed).
-struct RecShape {
-  uint32_t vt, hdr, klen, q, n4, vl, cls;
-  uint64_t seq, shared;
+struct RecHead {
+  uint32_t vt, hdr, klen, q, e1, e2;
+  bool ok;  // header in the fast shape (vtype not checked)
 };
-__device__ __forceinline__ RecShape rec_shape(const Win32& w, bool restart, bool want_values) {
-  RecShape r;
-  const uint64_t lo = w.w0;
-  r.vt = (uint32_t)(lo & 0xFF);
-  const bool vt_ok = r.vt <= 4 && r.vt != 3;
-  const bool tomb = r.vt == 1 || r.vt == 2;
-  // varint terminators (MSB clear) among bytes 1..7: seqno, [shared], key length
-  const uint64_t t1 = ~lo & 0x8080808080808000ULL;
-  const uint32_t e1 = ctz64(t1);
+__device__ __forceinline__ RecHead rec_head(uint64_t h, bool restart) {
+  RecHead r;
+  r.vt = (uint32_t)(h & 0xFF);
+  // LEB terminators (MSB clear) among bytes 1..7: seqno, [shared], key length
+  const uint64_t t1 = ~h & 0x8080808080808000ULL;
+  r.e1 = ctz64(t1);
   const uint64_t t2 = t1 & (t1 - 1);
-  const uint32_t e2 = restart ? e1 : ctz64(t2);
+  r.e2 = restart ? r.e1 : ctz64(t2);
   const uint64_t t3 = restart ? t2 : t2 & (t2 - 1);
   const uint32_t e3 = ctz64(t3);
-  const bool hdr_ok = t3 != 0 && e3 - e2 == 8;  // header within 8 bytes, 1-byte key length
-  const uint32_t sh3 = hdr_ok ? e3 - 7 : 0;
-  r.klen = (uint32_t)(lo >> sh3) & 0x7F;
+  r.ok = t3 != 0 && e3 - r.e2 == 8 && (restart || r.e2 - r.e1 <= 24);
+  r.klen = (uint32_t)(h >> (r.ok ? e3 - 7 : 0)) & 0x7F;
   r.hdr = (e3 >> 3) + 1;
-  r.q = r.hdr + r.klen;
-  r.seq = 0;
-  r.shared = 0;
-  if (want_values && hdr_ok) {
-    const uint32_t n1 = e1 >> 3;  // seqno bytes (1..7)
-    r.seq = leb_val8(lo >> 8, n1);
-    if (!restart) r.shared = leb_val8(lo >> (e1 + 1), (e2 - e1) >> 3);
-  }
-  // value length (1-2 byte varint) from the window when it lies inside it
-  const bool in_win = r.q <= 24;
-  const uint64_t z = win_at(w, in_win ? r.q : 24);
-  const bool two = (z & 0x80) != 0;
-  const bool vl_ok = tomb || (in_win && (z & 0x8080) != 0x8080);
-  r.n4 = tomb ? 0 : (two ? 2 : 1);
-  r.vl = tomb ? 0 : (two ? ((uint32_t)(z & 0x7F) | ((uint32_t)(z >> 1) & 0x3F80)) : (uint32_t)(z & 0x7F));
-  const bool shared_ok = restart || ((e2 - e1) >> 3) <= 3;
-  r.cls = !vt_ok ? 2u : ((hdr_ok && vl_ok && shared_ok) ? 0u : 1u);
+  r.q = r.hdr + r.klen;  // <= 136
   return r;
 }
+// 16 bytes at p as two u64 (one unaligned ds_read_b128 / global_load_dwordx4)
+struct Win16u {
+  uint64_t lo, hi;
+};
+__device__ __forceinline__ Win16u ld_win16u(const uint8_t* p) {
+  Win16u w;
+  __builtin_memcpy(&w, p, 16);
+  return w;
+}
+// two bytes at offset q (q <= 14) of the window, branch-free
+__device__ __forceinline__ uint32_t win16u_u16(const Win16u& w, uint32_t q) {
+  const uint32_t d0 = (uint32_t)w.lo, d1 = (uint32_t)(w.lo >> 32), d2 = (uint32_t)w.hi, d3 = (uint32_t)(w.hi >> 32);
+  const uint32_t qi = q >> 2;
+  const uint32_t lo = qi == 0 ? d0 : qi == 1 ? d1 : qi == 2 ? d2 : d3;
+  const uint32_t hi = qi == 0 ? d1 : qi == 1 ? d2 : qi == 2 ? d3 : 0u;
+  return alignbyte(hi, lo, q & 3) & 0xFFFF;
+}
+// value length from the two bytes at start + q; false = longer varint
+__device__ __forceinline__ bool rec_vlen(uint32_t z, bool tomb, uint32_t& n4, uint32_t& vl) {
+  const bool two = (z & 0x80) != 0;
+  n4 = tomb ? 0 : (two ? 2 : 1);
+  vl = tomb ? 0 : (two ? ((z & 0x7F) | ((z >> 1) & 0x3F80)) : (z & 0x7F));
+  return tomb || (z & 0x8080) != 0x8080;
+}
 
-// Full record parse (decode phase B).  Returns 1 = parsed, 0 = Cursor path,
-// -1 = malformed (same outcomes as oracle parse_data_item).
+// Full record parse.  Returns 1 = parsed, 0 = Cursor path, -1 = malformed
+// (same outcomes as oracle parse_data_item).  Payload-relative positions.
+// Branch-free: both loads are unconditional (clamped to the marker, so they
+// stay inside the block) and every field is computed before classifying.
 __device__ __forceinline__ int parse_data_fast(const uint8_t* base, uint32_t p0, uint32_t pos, uint32_t end,
                                                bool restart, uint32_t base_key_off, ItemFields& f,
                                                uint32_t& next) {
-  if (pos >= end) return -1;
-  const Win32 w = read_win32(base, p0 + pos);
-  const RecShape r = rec_shape(w, restart, true);
-  if (r.cls == 2) return -1;
-  if (r.cls == 1) return 0;
-  const uint32_t val_off = pos + r.q + r.n4;
-  const bool bad = (pos + r.hdr > end) || (!restart && (uint64_t)base_key_off + r.shared > end) ||
-                   ((uint64_t)pos + r.q > end) || (r.n4 && pos + r.q + r.n4 > end) ||
-                   ((uint64_t)val_off + r.vl > end);
-  f.seqno = r.seq;
+  const uint64_t h = ld_u64u(base + p0 + min(pos, end));  // >= 33 block bytes follow the marker
+  const RecHead r = rec_head(h, restart);
+  const bool tomb = is_tombstone(r.vt);
+  const uint32_t z = ld_u16u(base + p0 + min(pos + r.q, end));
+  uint32_t n4, vl;
+  const bool vl_ok = rec_vlen(z, tomb, n4, vl);
+  const uint64_t seq = leb_val8(h >> 8, r.e1 >> 3);
+  const uint32_t shared =
+      restart ? 0u : (uint32_t)leb_val8(h >> min(r.e1 + 1, 63u), (r.e2 - r.e1) >> 3) & 0xFFFF;
+  const uint32_t val_off = pos + r.q + n4;
+  const bool bad = (pos + r.hdr > end) || (!restart && (uint64_t)base_key_off + shared > end) ||
+                   (pos + r.q + n4 > end) || ((uint64_t)val_off + vl > end);
+  f.seqno = seq;
   f.handle_off = 0;
   f.key_off = pos + r.hdr;
   f.key_len = (uint16_t)r.klen;
-  f.prefix_len = (uint16_t)r.shared;
+  f.prefix_len = (uint16_t)shared;
   f.val_off = val_off;
-  f.val_len = r.vl;
+  f.val_len = vl;
   f.vtype = (uint8_t)r.vt;
-  next = val_off + r.vl;
-  return bad ? -1 : 1;
+  next = val_off + vl;
+  const bool fast = r.ok && vl_ok;
+  return (pos >= end || !valid_vtype(r.vt)) ? -1 : (!fast ? 0 : (bad ? -1 : 1));
 }
 
-// Record boundary only (decode phase A): the serial walk of a restart
-// interval needs nothing but each record's length.  1 = next/key_off valid,
-// 0 = Cursor path, -1 = malformed in a way the oracle also rejects.
-__device__ __forceinline__ int data_record_next_fast(const uint8_t* base, uint32_t p0, uint32_t p, uint32_t end,
-                                                     bool restart, uint32_t& next, uint32_t& key_off) {
-  if (p >= end) return -1;
-  const Win32 w = read_win32(base, p0 + p);
-  const RecShape r = rec_shape(w, restart, false);
-  key_off = p + r.hdr;
-  next = p + r.q + r.n4 + r.vl;
-  if (r.cls == 2) return -1;
-  if (r.cls == 1) return 0;
-  return (r.n4 && p + r.q >= end) ? -1 : 1;
+// Record length only (decode phase A), at p with >= 138 readable bytes.
+// false = not the fast shape (caller takes the Cursor path).  A wrong length
+// for a malformed record is harmless: phase B re-parses every record and
+// checks it ends where the next begins.
+__device__ __forceinline__ bool data_record_len_fast(const uint8_t* p, bool restart, uint32_t& len,
+                                                     uint32_t& hdr) {
+  const Win16u w = ld_win16u(p);
+  const RecHead r = rec_head(w.lo, restart);
+  uint32_t z = win16u_u16(w, min(r.q, 14u));
+  if (r.q > 14) z = ld_u16u(p + r.q);  // long key suffix: one more LDS read
+  uint32_t n4, vl;
+  const bool vl_ok = rec_vlen(z, is_tombstone(r.vt), n4, vl);
+  len = r.q + n4 + vl;
+  hdr = r.hdr;
+  return r.ok && vl_ok && valid_vtype(r.vt);
 }
 
 // KeyedBlockHandle::parse_full, src/table/index_block/block_handle.rs:175-206.

@@ -635,5 +635,14 @@ __device__ __forceinline__ uint64_t wave_bcast_u64(uint64_t v, int src) {
   uint32_t lo = __shfl((int)(uint32_t)v, src), hi = __shfl((int)(uint32_t)(v >> 32), src);
   return (uint64_t)lo | ((uint64_t)hi << 32);
 }
+// per-lane source lane (ds_bpermute)
+__device__ __forceinline__ uint64_t wave_shfl_u64(uint64_t v, int src) { return wave_bcast_u64(v, src); }
+// wave-uniform source lane (v_readlane -> SGPR)
+__device__ __forceinline__ uint32_t wave_readlane_u32(uint32_t v, uint32_t src) {
+  return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)src);
+}
+__device__ __forceinline__ uint64_t wave_readlane_u64(uint64_t v, uint32_t src) {
+  return (uint64_t)wave_readlane_u32((uint32_t)v, src) | ((uint64_t)wave_readlane_u32((uint32_t)(v >> 32), src) << 32);
+}
 
 }  // namespace lsmgpu

@@ -48,15 +48,17 @@ def main():
     assert int((out["status"][:nb] != 0).sum()) == 0
 
     variants = {}
-    for t in args.tunings.split(";"):
-        bpw, st, ti = (int(x) for x in t.split(","))
-        variants[f"tune {t}"] = (bpw, st, ti, 1)
-    a = tuple(int(x) for x in args.ablate.split(","))
-    variants["ablate no-hash"] = a + (1 | SKIP_HASH,)
-    variants["ablate no-parse"] = a + (1 | SKIP_PARSE,)
-    variants["ablate no-store"] = a + (1 | SKIP_STORE,)
-    variants["ablate phase-A only"] = a + (1 | 0x800,)
-    variants["ablate stage-only"] = a + (1 | SKIP_HASH | SKIP_PARSE | SKIP_STORE,)
+    for t in args.tunings.replace("/", ";").split(";"):
+        v = [int(x, 0) for x in t.split(",")]
+        variants[f"tune {t}"] = (v[0], v[1], v[2], 1 | (v[3] if len(v) > 3 else 0))
+    a = tuple(int(x, 0) for x in args.ablate.split(","))
+    xf = a[3] if len(a) > 3 else 0
+    a = a[:3]
+    variants["ablate no-hash"] = a + (1 | xf | SKIP_HASH,)
+    variants["ablate no-parse"] = a + (1 | xf | SKIP_PARSE,)
+    variants["ablate no-store"] = a + (1 | xf | SKIP_STORE,)
+    variants["ablate phase-A only"] = a + (1 | xf | 0x800,)
+    variants["ablate stage-only"] = a + (1 | xf | SKIP_HASH | SKIP_PARSE | SKIP_STORE,)
     times = {k: [] for k in variants}
     for _ in range(args.rounds):
         for name, tun in variants.items():

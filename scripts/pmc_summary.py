@@ -6,7 +6,7 @@ import sys
 from collections import defaultdict
 from pathlib import Path
 
-VARIANTS = ["full", "no-parse", "stage-only", "no-hash"]
+VARIANTS = ["full", "no-parse", "stage-only", "no-hash", "phaseA-only"]
 
 
 def load(dirpath):
@@ -42,7 +42,7 @@ def main():
     if "full" in out and "SQ_INSTS_VALU" in out["full"]:
         f, s = out["full"], out.get("stage-only", {})
         print("\nper-wave-instruction deltas (full - stage-only):")
-        for c in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_WAVE_CYCLES", "SQ_WAIT_INST_ANY", "SQ_WAIT_ANY"):
+        for c in ("SQ_INSTS_VALU", "SQ_INSTS_SALU", "SQ_INSTS_LDS", "SQ_WAVE_CYCLES", "SQ_WAIT_INST_ANY", "SQ_WAIT_ANY", "SQ_BUSY_CYCLES", "SQ_ACTIVE_INST_VALU", "SQ_ACTIVE_INST_LDS", "SQ_LDS_BANK_CONFLICT", "SQ_WAIT_INST_LDS"):
             if c in f:
                 print(f"  {c:22s} full {f[c]:14.0f}  stage-only {s.get(c, 0):14.0f}  delta {f[c] - s.get(c, 0):14.0f}")
 

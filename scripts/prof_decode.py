@@ -18,7 +18,7 @@ import torch  # noqa: E402
 import bench  # noqa: E402
 import lsmgpu  # noqa: E402
 
-VARIANTS = [("full", 0), ("no-parse", 0x200), ("stage-only", 0x700), ("no-hash", 0x100)]
+VARIANTS = [("full", 0), ("no-parse", 0x200), ("stage-only", 0x700), ("no-hash", 0x100), ("phaseA-only", 0x800)]
 
 
 def main():
@@ -35,10 +35,11 @@ def main():
     out = dec.alloc_outputs(n_items, nb)
     dec.decode(enc["buf"], enc["block_off"], nb, out, n_items)
     torch.cuda.synchronize()
-    base = tuple(int(x) for x in args.tuning.split(","))
+    v = [int(x, 0) for x in args.tuning.split(",")]
+    base, xf = tuple(v[:3]), (v[3] if len(v) > 3 else 0)
     for _ in range(args.reps):
         for name, fl in VARIANTS:
-            dec.decode(enc["buf"], enc["block_off"], nb, out, n_items, tuning=base + (1 | fl,))
+            dec.decode(enc["buf"], enc["block_off"], nb, out, n_items, tuning=base + (1 | xf | fl,))
     torch.cuda.synchronize()
     print("variants:", [v for v, _ in VARIANTS], "reps", args.reps, "blocks", nb)
 

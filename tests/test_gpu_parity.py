@@ -87,7 +87,7 @@ def test_decode_golden_blocks(gpu, golden_blocks):
             assert pyoracle.materialize(payload, one, case["restart_interval"]) == case_expected_items(case), case["name"]
 
 
-@pytest.mark.parametrize("tuning", [None, (1, 256, 64), (4, 4096, 64), (64, 65536, 2048)])
+@pytest.mark.parametrize("tuning", [None, (1, 256, 64), (4, 4096, 64), (63, 65536, 2048)])
 def test_decode_golden_blocks_tunings(gpu, golden_blocks, tuning):
     """Staged path, direct-from-HBM path (tiny stage) and large groups agree."""
     blocks = [bytes.fromhex(c["block"]) for c in golden_blocks]
