@@ -109,8 +109,8 @@ typedef struct lsm_block_params {
 
 /* Tuning knobs for the decode kernel (0 = library default). */
 typedef struct lsm_decode_tuning {
-    uint32_t blocks_per_wave;  /* consecutive blocks one wave owns (1..63) */
-    uint32_t stage_bytes;      /* LDS bytes per wave for staged block bytes */
+    uint32_t blocks_per_wave;  /* consecutive blocks one workgroup owns (1..63) */
+    uint32_t stage_bytes;      /* LDS bytes per workgroup for staged block bytes (<= 65536) */
     uint32_t tile_items;       /* LDS output tile capacity in items */
     uint32_t flags;            /* LSM_DECODE_ITEM_START_VALID: d_item_start already holds the
                                   prefix sum of this batch (skip the count + scan pass) */

@@ -18,9 +18,9 @@ int set_hip_error(hipError_t e, const char* where) {
   return LSM_HIP_ERROR;
 }
 
-constexpr uint32_t kDefaultBlocksPerWave = 32;
-constexpr uint32_t kDefaultStageBytes = 16384;
-constexpr uint32_t kDefaultTileItems = 384;
+constexpr uint32_t kDefaultBlocksPerWave = 48;  // per 4-wave workgroup
+constexpr uint32_t kDefaultStageBytes = 65536;
+constexpr uint32_t kDefaultTileItems = 1024;
 
 }  // namespace
 
@@ -163,3 +163,9 @@ int lsm_xxh3_128_batch(const uint8_t* d_data, const uint64_t* d_off, uint32_t n,
 }
 
 }  // extern "C"
+
+/* Diagnostic (not part of the public header): phase timers of decode launches
+ * run with tuning flag 0x2000, summed clock64() cycles per phase and wave. */
+extern "C" int lsm_diag_decode_timers(uint64_t* out, int n, int reset) {
+  return lsmgpu::read_decode_timers(out, n, reset != 0) == hipSuccess ? LSM_OK : LSM_HIP_ERROR;
+}

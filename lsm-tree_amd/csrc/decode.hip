@@ -31,13 +31,15 @@ namespace lsmgpu {
 // Diagnostic-only flags (lsm_decode_tuning.flags high bits): drop one phase to
 // price it in a profile.  Outputs are NOT valid with any of them set.
 constexpr uint32_t kDiagSkipHash = 0x100, kDiagSkipParse = 0x200, kDiagSkipStore = 0x400,
-                   kDiagSkipPhaseB = 0x800, kDiagNoPipe = 0x1000;
+                   kDiagSkipPhaseB = 0x800;
 
 constexpr uint32_t kMaxGroup = 32;  // blocks per staged group
 constexpr uint32_t kStagePad = 256;  // readable LDS bytes past the span (fast parsers read <= 138)
 
-// Phase-A record descriptor (one u64 per group item, LDS): image offsets of
-// the record start, of where it must end, and of its restart head's key.
+// Record descriptor (one u64 per group item, LDS), written by phase A, read
+// by phase B: image offsets of the record start, of where it must end (the
+// next record's start, or the interval's end for its last record) and of its
+// restart head's key; [48,53) group block, 53 restart head, 54 valid.
 constexpr int kRecEndShift = 16, kRecKeyShift = 32, kRecBlockShift = 48;
 constexpr uint64_t kRecRestart = 1ULL << 53, kRecValid = 1ULL << 54;
 
@@ -53,6 +55,8 @@ struct alignas(16) BlockMeta {
   uint32_t ri, step, bin_len, bin_off, item_count;
   uint32_t item0;     // first output index relative to the group base
   uint32_t chain0;    // exclusive prefix of restart intervals in the group
+  int32_t hdr_st;     // header-level status (gates the payload checksum)
+  uint32_t ck_bad;    // payload checksum mismatch
 };
 static_assert(sizeof(BlockMeta) == 80, "BlockMeta layout");
 
@@ -65,15 +69,24 @@ __device__ __forceinline__ void wave_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
+// Workgroup barrier for LDS hand-offs only: waits for this wave's LDS ops
+// (lgkmcnt), not for its global stores, which __syncthreads' release fence
+// would drain (vmcnt(0)) before every phase.
+__device__ __forceinline__ void lds_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
 __device__ __forceinline__ void emit_global(const lsm_parsed_items& o, uint64_t i, const ItemFields& f) {
-  if (o.seqno) o.seqno[i] = f.seqno;
-  if (o.key_off) o.key_off[i] = f.key_off;
-  if (o.val_off) o.val_off[i] = f.val_off;
-  if (o.val_len) o.val_len[i] = f.val_len;
-  if (o.key_len) o.key_len[i] = f.key_len;
-  if (o.prefix_len) o.prefix_len[i] = f.prefix_len;
-  if (o.vtype) o.vtype[i] = f.vtype;
-  if (o.handle_off) o.handle_off[i] = f.handle_off;
+  if (o.seqno) gstore(o.seqno, i, f.seqno);
+  if (o.key_off) gstore(o.key_off, i, f.key_off);
+  if (o.val_off) gstore(o.val_off, i, f.val_off);
+  if (o.val_len) gstore(o.val_len, i, f.val_len);
+  if (o.key_len) gstore(o.key_len, i, f.key_len);
+  if (o.prefix_len) gstore(o.prefix_len, i, f.prefix_len);
+  if (o.vtype) gstore(o.vtype, i, f.vtype);
+  if (o.handle_off) gstore(o.handle_off, i, f.handle_off);
 }
 
 // Lane-level: header checks in oracle order (header.rs:116-169).
@@ -165,16 +178,45 @@ __device__ __forceinline__ uint64_t rec_desc(uint32_t a, uint32_t end, uint32_t 
   return (uint64_t)a | ((uint64_t)end << kRecEndShift) | ((uint64_t)key << kRecKeyShift) | tag;
 }
 
-// Phase A: lane = restart interval c of the group; one descriptor per record
-// (start, required end, head key — image offsets) into rec[].  The walk only
-// measures record lengths; phase B parses every record in full and checks
-// the chain.  The step loop is wave-uniform: lanes past their interval's end
-// compute on a harmless position and store to the scratch slot rec[dummy], so
-// the only branches are the rare long-suffix read and the Cursor fallback.
+// Predicted header shape of a non-restart record: n1 seqno bytes, n2 shared
+// bytes, 1 key-length byte.  msk = MSB bits of header bytes 1..hdr-1, pat =
+// where their LEB terminators must be; a record matches iff (~h & msk) == pat.
+struct Shape {
+  uint32_t hdr, kshift;
+  uint64_t msk, pat;
+};
+__device__ __forceinline__ Shape make_shape(uint32_t n1, uint32_t n2) {
+  Shape s;
+  s.hdr = n1 + n2 + 2;  // <= 8
+  s.kshift = 8 * (s.hdr - 1);
+  s.msk = 0x8080808080808000ULL & (s.hdr >= 8 ? ~0ULL : ((1ULL << (8 * s.hdr)) - 1));
+  s.pat = (0x80ULL << (8 * n1)) | (0x80ULL << (8 * (n1 + n2))) | (0x80ULL << (8 * (s.hdr - 1)));
+  return s;
+}
+
+// Record length from the key length and the two bytes z after the key
+// (1-2 byte value length; tombstones carry none).
+__device__ __forceinline__ uint32_t rec_len(uint32_t vt, uint32_t q, uint32_t z) {
+  const bool tomb = vt - 1u < 2u;
+  const bool two = (z & 0x80) != 0;
+  const uint32_t vl = two ? ((z & 0x7F) | ((z >> 1) & 0x3F80)) : (z & 0x7F);
+  return q + (tomb ? 0u : vl + 1u + (two ? 1u : 0u));
+}
+
+// Phase A: lane = restart interval.  Walks record BOUNDARIES only and writes
+// one descriptor per record; phase B parses every record in full and checks
+// that it ends exactly where its descriptor says, so a boundary computed
+// here from a malformed record can only turn into a PARSE status.  The step
+// is kept short because it runs as one wave's serial instruction stream:
+// the key length is read at the PREDICTED header length (the previous
+// record's shape, checked with one mask compare) and the value length from
+// the same 16-byte LDS window; only a shape change, a long key suffix or a
+// long varint leaves the straight path.  The loop is wave-uniform: lanes
+// past their interval's end store to rec[dummy].
 __device__ __forceinline__ void phase_a(const uint8_t* img, BlockMeta* meta, const uint8_t* owner, uint64_t* rec,
-                                        uint32_t total, uint32_t dummy) {
-  const int lane = threadIdx.x;
-  for (uint32_t c0 = 0; c0 < total; c0 += kWave) {
+                                        uint32_t c_first, uint32_t c_step, uint32_t total, uint32_t dummy) {
+  const int lane = threadIdx.x & (kWave - 1);
+  for (uint32_t c0 = c_first; c0 < total; c0 += c_step) {
     const uint32_t c = c0 + lane;
     const bool live = c < total;
     const uint32_t j = live ? owner[c] : 0;
@@ -182,80 +224,85 @@ __device__ __forceinline__ void phase_a(const uint8_t* img, BlockMeta* meta, con
     const TrailerInfo t = trailer_of(m);
     const uint32_t p0 = m.p0, rec_end = m.rec_end;
     const uint32_t r = live ? c - m.chain0 : 0;
-    const bool last = r + 1 == t.bin_len;
+    const bool last_iv = r + 1 == t.bin_len;
     const uint32_t s_rel = bin_get(img, p0, t, r);
-    const uint32_t e_rel = last ? t.rec_end : bin_get(img, p0, t, r + 1);
-    bool ok = s_rel < t.rec_end && e_rel <= t.rec_end;  // records lie before the marker
-    const uint32_t count = last ? t.item_count - r * t.ri : t.ri;
-    const uint32_t steps = (live && ok) ? count - 1 : 0;  // record lengths to measure
+    const uint32_t e_rel = last_iv ? t.rec_end : bin_get(img, p0, t, r + 1);
+    // records lie before the marker; the first one at payload offset 0
+    bool ok = s_rel < t.rec_end && e_rel <= t.rec_end && (r != 0 || s_rel == 0);
+    const uint32_t count = (live && ok) ? (last_iv ? t.item_count - r * t.ri : t.ri) : 0;
+    if (live && !ok) atomicCAS(&meta[j].st, ST_OK, ST_PARSE);
     const uint32_t ib0 = m.item0 + r * t.ri;
     const uint64_t tag = ((uint64_t)j << kRecBlockShift) | kRecValid;
+    const uint32_t stop = p0 + e_rel;
     uint32_t a = p0 + (ok ? s_rel : 0), key = a;
-    const uint32_t max_steps = wave_max_u32(steps);
-    if (max_steps) {
-      // restart head (full key: value length read separately)
-      {
-        const bool act = steps > 0;
-        const Win16u w = ld_win16u(img + a);
-        const RecHead hd = rec_head(w.lo, true);
-        const uint32_t z = ld_u16u(img + a + hd.q);
-        uint32_t n4, vl;
-        const bool vl_ok = rec_vlen(z, is_tombstone(hd.vt), n4, vl);
-        uint32_t nxt = a + hd.q + n4 + vl;
-        key = a + hd.hdr;
-        if (act && !(hd.ok && vl_ok && valid_vtype(hd.vt))) {
-          ItemFields tmp;
-          uint32_t tnext;
-          const bool sok = parse_data_slow(img, p0, a - p0, t.rec_end, true, 0, &tmp, &tnext);
-          nxt = sok ? p0 + tnext : rec_end;
-          key = p0 + tmp.key_off;
-        }
-        ok = ok && (!act || nxt < rec_end);
-        const bool go = act && ok;
-        rec[go ? ib0 : dummy] = rec_desc(a, nxt, key, tag | kRecRestart);
-        a = go ? nxt : a;
+    const uint32_t max_count = __builtin_amdgcn_readfirstlane(wave_max_u32(count));
+    if (!max_count) continue;
+    Shape sp;
+    {  // restart head (full key: the value length is read separately)
+      const Win16u w = ld_win16u(img + a);
+      const RecHead hd = rec_head(w.lo, true);
+      uint32_t nxt = a + rec_len(hd.vt, hd.q, ld_u16u(img + a + hd.q));
+      key = a + hd.hdr;
+      sp = make_shape(min(hd.e1 >> 3, 5u), 1);
+      const bool fast = hd.ok && valid_vtype(hd.vt) && m.type != 1;
+      if (count > 1 && !fast) {
+        ItemFields tmp;
+        uint32_t tnext;
+        const bool sok = parse_data_slow(img, p0, a - p0, t.rec_end, true, 0, &tmp, &tnext);
+        nxt = sok ? p0 + tnext : rec_end;
+        key = p0 + tmp.key_off;
       }
-      for (uint32_t jj = 1; jj < max_steps; ++jj) {
-        const bool act = jj < steps && ok;
-        uint32_t len, hdr;
-        uint32_t nxt = a;
-        if (data_record_len_fast(img + a, false, len, hdr)) {
-          nxt = a + len;
-        } else if (act) {
+      const bool act = count > 0;
+      if (count > 1) ok = nxt < rec_end;
+      rec[act ? ib0 : dummy] = rec_desc(a, count == 1 ? stop : nxt, key, tag | kRecRestart);
+      a = (act && ok) ? nxt : a;
+    }
+    for (uint32_t jj = 1; jj < max_count; ++jj) {
+      const bool act = jj < count && ok;
+      const Win16u w = ld_win16u(img + a);
+      const uint32_t klen = (uint32_t)(w.lo >> sp.kshift) & 0x7F;
+      const uint32_t q = sp.hdr + klen;
+      uint32_t z = win16u_u16(w, min(q, 14u));
+      if (q > 14) z = ld_u16u(img + a + q);  // long key suffix: one more LDS read
+      uint32_t nxt = a + rec_len((uint32_t)w.lo & 0xFF, q, z);
+      if (act && (~w.lo & sp.msk) != sp.pat) {  // the header shape changed
+        const RecHead hd = rec_head(w.lo, false);
+        if (hd.ok) sp = make_shape(hd.e1 >> 3, (hd.e2 - hd.e1) >> 3);
+        nxt = a + rec_len(hd.vt, hd.q, ld_u16u(img + a + hd.q));
+        if (!hd.ok) {  // seqno >= 2^49, shared >= 2^21 or key length >= 128
           ItemFields tmp;
           uint32_t tnext;
           const bool sok = parse_data_slow(img, p0, a - p0, t.rec_end, false, key - p0, &tmp, &tnext);
           nxt = sok ? p0 + tnext : rec_end;
         }
-        ok = ok && (!act || nxt < rec_end);
-        const bool go = act && ok;
-        rec[go ? ib0 + jj : dummy] = rec_desc(a, nxt, key, tag);
-        a = go ? nxt : a;
       }
+      const bool last = jj + 1 == count;
+      ok = ok && (!act || last || nxt < rec_end);
+      rec[act ? ib0 + jj : dummy] = rec_desc(a, last ? stop : nxt, key, tag);
+      a = (act && ok) ? nxt : a;
     }
-    // the interval's last record must end where the next interval (or the marker) begins
-    if (live && ok) rec[ib0 + count - 1] = rec_desc(a, p0 + e_rel, key, tag | (count == 1 ? kRecRestart : 0));
-    if (live && !ok) atomicCAS(&meta[j].st, ST_OK, ST_PARSE);
+    if (count && !ok) atomicCAS(&meta[j].st, ST_OK, ST_PARSE);  // walked off the record area
   }
 }
 
-// Phase B: lane = record.  Full parse + validation of every descriptor, then
-// coalesced stores of all fields (a failed block's outputs are unspecified,
-// so lanes store unconditionally).
+// Phase B: thread = record.  Full parse + validation of every descriptor
+// (the oracle's parse_data_item checks, and the record must end exactly at
+// the descriptor's end), then coalesced stores of all fields.
 __device__ __forceinline__ void phase_b(const DecodeParams& P, const uint8_t* img, BlockMeta* meta,
                                         const uint64_t* rec, uint32_t n_items, uint32_t g_item0) {
-  const int lane = threadIdx.x;
+  const uint32_t tid = threadIdx.x, nthr = blockDim.x;
   const bool all_fields = P.out.seqno && P.out.key_off && P.out.val_off && P.out.val_len && P.out.key_len &&
                           P.out.prefix_len && P.out.vtype;
   const bool store = !(P.flags & kDiagSkipStore);
-  for (uint32_t i0 = 0; i0 < n_items; i0 += kWave) {
-    const uint32_t i = i0 + lane;
+  for (uint32_t i0 = 0; i0 < n_items; i0 += nthr) {
+    const uint32_t i = i0 + tid;
     if (i >= n_items) break;
     const uint64_t d = rec[i];
+    if (!(d & kRecValid)) continue;  // not reached: its block has failed
     const uint32_t j = (uint32_t)(d >> kRecBlockShift) & 31;
     const u32x4 hot = *reinterpret_cast<const u32x4*>(&meta[j]);  // p0, rec_end, st, type
     const uint32_t p0 = hot.x, end = hot.y - p0;
-    const bool live = (d & kRecValid) && (int32_t)hot.z == ST_OK;
+    const bool live = (int32_t)hot.z == ST_OK;
     const uint32_t a = ((uint32_t)d & 0xFFFF) - p0;
     const uint32_t want = ((uint32_t)(d >> kRecEndShift) & 0xFFFF) - p0;
     const uint32_t base_key = ((uint32_t)(d >> kRecKeyShift) & 0xFFFF) - p0;
@@ -276,14 +323,14 @@ __device__ __forceinline__ void phase_b(const DecodeParams& P, const uint8_t* im
     if (!store) continue;
     const uint64_t gi = (uint64_t)g_item0 + i;
     if (all_fields) {  // common case: no per-field null checks
-      P.out.seqno[gi] = f.seqno;
-      P.out.key_off[gi] = f.key_off;
-      P.out.val_off[gi] = f.val_off;
-      P.out.val_len[gi] = f.val_len;
-      P.out.key_len[gi] = f.key_len;
-      P.out.prefix_len[gi] = f.prefix_len;
-      P.out.vtype[gi] = f.vtype;
-      if (P.out.handle_off) P.out.handle_off[gi] = f.handle_off;
+      gstore(P.out.seqno, gi, f.seqno);
+      gstore(P.out.key_off, gi, f.key_off);
+      gstore(P.out.val_off, gi, f.val_off);
+      gstore(P.out.val_len, gi, f.val_len);
+      gstore(P.out.key_len, gi, f.key_len);
+      gstore(P.out.prefix_len, gi, f.prefix_len);
+      gstore(P.out.vtype, gi, f.vtype);
+      if (P.out.handle_off) gstore(P.out.handle_off, gi, f.handle_off);
     } else {
       emit_global(P.out, gi, f);
     }
@@ -299,7 +346,7 @@ __device__ __forceinline__ bool walk_interval(const uint8_t* base, uint32_t p0, 
   const uint32_t start = bin_get(base, p0, t, r);
   const uint32_t stop = last ? t.rec_end : bin_get(base, p0, t, r + 1);
   const uint32_t count = last ? t.item_count - r * t.ri : t.ri;
-  if (start > t.rec_end || stop > t.rec_end) return false;
+  if (start > t.rec_end || stop > t.rec_end || (r == 0 && start != 0)) return false;
   uint32_t base_key = 0, pos = start;
   ItemFields f;
   for (uint32_t j = 0; j < count; ++j) {
@@ -315,12 +362,12 @@ __device__ __forceinline__ bool walk_interval(const uint8_t* base, uint32_t p0, 
 // One block straight from HBM (blocks larger than the LDS stage).
 __device__ __noinline__ void decode_block_direct(const DecodeParams& P, uint32_t b, BlockMeta* meta) {
   const int lane = threadIdx.x;
-  const uint64_t off = P.block_off[b], end = P.block_off[b + 1];
+  const uint64_t off = gload(P.block_off, b), end = gload(P.block_off, b + 1);
   const uint8_t* base = P.blocks + (off & ~15ULL);
   const uint32_t hb = (uint32_t)(off & 15);
   const uint64_t len = end >= off ? end - off : 0;
-  const uint64_t item_base = P.item_start[b];
-  const uint32_t cap = P.item_start[b + 1] - P.item_start[b];
+  const uint64_t item_base = gload(P.item_start, b);
+  const uint32_t cap = gload(P.item_start, b + 1) - gload(P.item_start, b);
   if (lane == 0) meta_header(base, hb, len, meta[0]);
   wave_sync();
   if (meta[0].st == ST_OK) {
@@ -341,18 +388,16 @@ __device__ __noinline__ void decode_block_direct(const DecodeParams& P, uint32_t
     if (!ok) atomicCAS(&meta[0].st, ST_OK, ST_PARSE);
   }
   wave_sync();
-  if (lane == 0) P.status[b] = meta[0].st;
+  if (lane == 0) gstore(P.status, b, meta[0].st);
   wave_sync();
 }
 
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef const __attribute__((address_space(1))) void gbl_void_t;
 
-constexpr uint32_t kPipeChunks = 16;  // dwordx4 per lane held in flight: 16 KiB per wave
-
 // A group: the longest run of consecutive blocks from b that fits the stage
-// (k == 0: block b alone is too large and takes the direct path).  Lane j
-// holds block b+j's handle and item range.
+// (k == 0: block b alone is too large and takes the direct path).  Lane j of
+// every wave holds block b+j's handle and item range.
 struct Group {
   uint32_t b, k, g_item0, n_items;
   uint64_t span0, span1;
@@ -363,7 +408,7 @@ struct Group {
 // offr / itr: lane l holds block_off / item_start of block b_begin + l.
 __device__ __forceinline__ Group form_group(const DecodeParams& P, uint32_t b, uint32_t b_begin, uint32_t b_end,
                                             uint32_t gmax, uint64_t offr, uint32_t itr) {
-  const int lane = threadIdx.x;
+  const int lane = threadIdx.x & (kWave - 1);
   Group G;
   G.b = b;
   const uint32_t li = b - b_begin + lane;
@@ -385,64 +430,26 @@ __device__ __forceinline__ Group form_group(const DecodeParams& P, uint32_t b, u
   return G;
 }
 
-// Steps 3-7 on a group whose bytes are in img.
-__device__ __forceinline__ void process_group(const DecodeParams& P, const Group& G, const uint8_t* img,
-                                              BlockMeta* meta, uint64_t* rec, uint8_t* owner) {
-  const int lane = threadIdx.x;
-  const uint32_t k = G.k;
-  // ---- 3. lane j: header of block b+j
-  if ((uint32_t)lane < k) {
-    BlockMeta m;
-    meta_header(img, (uint32_t)(G.off_j - G.span0), G.end_j - G.off_j, m);
-    m.item0 = G.it0_j - G.g_item0;
-    meta[lane] = m;
-  }
-  wave_sync();
-  // ---- 4. payload checksums: DPP row g hashes blocks g, g+4, ...
-  if (!(P.flags & kDiagSkipHash)) {
-    const uint32_t g = lane >> 4;
-    for (uint32_t j = g; j < k; j += 4) {
-      if (meta[j].st != ST_OK) continue;
-      const uint32_t hb = meta[j].hb, len = meta[j].len;
-      uint64_t lo, hi;
-      xxh3_128_row(img, hb + kHdrLen, len - kHdrLen, lo, hi);
-      if ((lane & 15) == 0 && (lo != meta[j].ck_lo || hi != meta[j].ck_hi)) meta[j].st = ST_CKSUM;
-    }
-    wave_sync();
-  }
-  // ---- 5. trailers + restart-interval numbering; owner[c] = block of interval c
-  uint32_t chains = 0;
-  BlockMeta m;
-  if ((uint32_t)lane < k) {
-    m = meta[lane];
-    meta_trailer(img, P.expect_type, G.it1_j - G.it0_j, m);
-    chains = m.st == ST_OK ? m.bin_len : 0;
-  }
-  const uint32_t incl = wave_incl_scan_u32(chains);
-  const uint32_t total = (P.flags & kDiagSkipParse) ? 0 : wave_readlane_u32(incl, 63);
-  if ((uint32_t)lane < k) {
-    m.chain0 = incl - chains;
-    meta[lane] = m;
-    if (total)
-      for (uint32_t r = 0; r < chains; ++r) owner[m.chain0 + r] = (uint8_t)lane;
-  }
-  wave_sync();
-  // ---- 6. phase A: lane = restart interval, record boundaries only
-  phase_a(img, meta, owner, rec, total, P.tile_items);
-  wave_sync();
-  // ---- 7. phase B: lane = record; full parse + validation; coalesced stores
-  if (!(P.flags & (kDiagSkipParse | kDiagSkipPhaseB))) phase_b(P, img, meta, rec, G.n_items, G.g_item0);
-  wave_sync();
-  if ((uint32_t)lane < k) P.status[G.b + lane] = meta[lane].st;
-  wave_sync();
-}
+// Workgroup = kGroupWaves waves sharing one LDS stage of up to 64 KiB (16
+// 4-KiB blocks, ~64 restart intervals).  Per group:
+//   all waves   LDS-DMA of the span (wave w moves 1-KiB pieces w, w+4, ...)
+//   wave 0      headers + trailers (lane j = block j), interval numbering
+//   wave pa     phase A over all intervals (every lane walks one interval)
+//   other waves payload checksums (12 DPP rows, block j on row j mod 12)
+//   all waves   phase B (thread = record), coalesced SoA stores
+// pa rotates with the group index so the serial walk lands on each SIMD in
+// turn.  Phase A needs only the trailer, not the checksum, so it runs
+// concurrently with the hash; statuses merge in oracle order at the end.
+constexpr uint32_t kGroupWaves = 4;
 
-// kPipe (stage <= 16 KiB): the next group's span is loaded into registers
-// (16 x dwordx4 per lane) while the current group is processed, so HBM
-// latency overlaps the parse; the landed registers are written to LDS at the
-// top of the next iteration.  !kPipe (larger stages): LDS-DMA, one wait.
-template <bool kPipe>
-__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 8))) void decode_blocks_kernel(DecodeParams P) {
+// Diagnostic phase timers (flag kDiagTimers): per workgroup clock64() deltas,
+// summed over the grid; read back with lsm_diag_decode_timers (abi.hip).
+constexpr uint32_t kDiagTimers = 0x2000;
+enum : int { kTmForm, kTmDma, kTmHdr, kTmA, kTmHash, kTmSplit, kTmB, kTmTail, kTmGroups, kTmN };
+__device__ unsigned long long g_decode_timers[kTmN];
+
+template <bool kTimed>
+__global__ __launch_bounds__(kGroupWaves * kWave) void decode_blocks_kernel(DecodeParams P) {
   // LDS: [meta: G x 80 B][rec: u64 per item + 1 scratch][owner: u8 per item][staged bytes + pad]
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint32_t gmax = min(kMaxGroup, P.blocks_per_wave);
@@ -450,74 +457,123 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 8))) void
   uint64_t* rec = reinterpret_cast<uint64_t*>(smem + gmax * (uint32_t)sizeof(BlockMeta));
   uint8_t* owner = reinterpret_cast<uint8_t*>(rec) + ((8 * (P.tile_items + 1) + 15) & ~15u);
   uint8_t* img = owner + ((P.tile_items + 15) & ~15u);
-  const int lane = threadIdx.x;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid / kWave);
+  const int lane = tid & (kWave - 1);
   const uint32_t b_begin = blockIdx.x * P.blocks_per_wave;
   const uint32_t b_end = min(b_begin + P.blocks_per_wave, P.n_blocks);
-  // the wave's handles and item starts, once (blocks_per_wave <= 63)
+  // the workgroup's handles and item starts, once per wave (blocks_per_wave <= 63)
   uint64_t offr = 0;
   uint32_t itr = 0;
   if (b_begin + lane <= b_end) {
-    offr = P.block_off[b_begin + lane];
-    itr = P.item_start[b_begin + lane];
+    offr = gload(P.block_off, b_begin + lane);
+    itr = gload(P.item_start, b_begin + lane);
   }
-  u32x4 R[kPipeChunks];
-  Group cur = form_group(P, b_begin, b_begin, b_end, gmax, offr, itr);
-  if constexpr (kPipe) {
-    if (cur.k) {
-      const uint32_t chunks = (uint32_t)((cur.span1 - cur.span0) >> 4);
-      const u32x4* src = reinterpret_cast<const u32x4*>(P.blocks + cur.span0) + lane;
-#pragma unroll
-      for (uint32_t i = 0; i < kPipeChunks; ++i)
-        if (i * kWave + lane < chunks) R[i] = __builtin_nontemporal_load(src + i * kWave);
-    }
+  uint32_t iter = 0;
+  constexpr bool timed = kTimed;
+  uint64_t tm[kTmN] = {};
+  uint64_t t0 = 0;
+  if constexpr (timed) asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t0)::"memory");
+#define LSM_TICK(slot)                                                                     \
+  if constexpr (timed) {                                                                   \
+    uint64_t t1;                                                                           \
+    __builtin_amdgcn_sched_barrier(0);                                                     \
+    asm volatile("s_memtime %0\n\ts_waitcnt lgkmcnt(0)" : "=s"(t1)::"memory");             \
+    __builtin_amdgcn_sched_barrier(0);                                                     \
+    tm[slot] += t1 - t0;                                                                   \
+    t0 = t1;                                                                               \
   }
-  while (cur.b < b_end) {
-    if (cur.k == 0) {
-      decode_block_direct(P, cur.b, meta);
-      cur = form_group(P, cur.b + 1, b_begin, b_end, gmax, offr, itr);
-      if constexpr (kPipe) {
-        if (cur.k) {
-          const uint32_t chunks = (uint32_t)((cur.span1 - cur.span0) >> 4);
-          const u32x4* src = reinterpret_cast<const u32x4*>(P.blocks + cur.span0) + lane;
-#pragma unroll
-          for (uint32_t i = 0; i < kPipeChunks; ++i)
-            if (i * kWave + lane < chunks) R[i] = __builtin_nontemporal_load(src + i * kWave);
-        }
-      }
+  for (uint32_t b = b_begin; b < b_end; ++iter) {
+    const Group G = form_group(P, b, b_begin, b_end, gmax, offr, itr);
+    LSM_TICK(kTmForm);
+    if (G.k == 0) {
+      if (wave == 0) decode_block_direct(P, b, meta);
+      lds_barrier();
+      b += 1;
       continue;
     }
-    const uint32_t chunks = (uint32_t)((cur.span1 - cur.span0) >> 4);
-    if constexpr (kPipe) {
-      // land the prefetched span, then start the next one
-      u32x4* dst = reinterpret_cast<u32x4*>(img) + lane;
-#pragma unroll
-      for (uint32_t i = 0; i < kPipeChunks; ++i)
-        if (i * kWave + lane < chunks) dst[i * kWave] = R[i];
-      const Group nxt = form_group(P, cur.b + cur.k, b_begin, b_end, gmax, offr, itr);
-      if (nxt.b < b_end && nxt.k) {
-        const uint32_t nchunks = (uint32_t)((nxt.span1 - nxt.span0) >> 4);
-        const u32x4* src = reinterpret_cast<const u32x4*>(P.blocks + nxt.span0) + lane;
-#pragma unroll
-        for (uint32_t i = 0; i < kPipeChunks; ++i)
-          if (i * kWave + lane < nchunks) R[i] = __builtin_nontemporal_load(src + i * kWave);
-      }
-      for (uint32_t i = lane; i < cur.n_items; i += kWave) rec[i] = 0;
-      wave_sync();
-      process_group(P, cur, img, meta, rec, owner);
-      cur = nxt;
-    } else {
-      const uint8_t* src = P.blocks + cur.span0 + 16 * lane;
-      for (uint32_t i = 0; i * kWave < chunks; ++i) {
+    const uint32_t k = G.k;
+    // ---- 1. stage the span HBM -> LDS (LDS-DMA), clear the record descriptors
+    {
+      const uint32_t chunks = (uint32_t)((G.span1 - G.span0) >> 4);
+      const uint8_t* src = P.blocks + G.span0 + 16 * lane;
+      for (uint32_t i = wave; i * kWave < chunks; i += kGroupWaves) {
         if (i * kWave + lane < chunks)
           __builtin_amdgcn_global_load_lds((gbl_void_t*)(src + 1024 * i), (lds_void_t*)(img + 1024 * i), 16, 0, 0);
       }
-      for (uint32_t i = lane; i < cur.n_items; i += kWave) rec[i] = 0;
-      __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0): the DMA has landed
-      wave_sync();
-      process_group(P, cur, img, meta, rec, owner);
-      cur = form_group(P, cur.b + cur.k, b_begin, b_end, gmax, offr, itr);
+      for (uint32_t i = tid; i < G.n_items; i += kGroupWaves * kWave) rec[i] = 0;
+      __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0): this wave's DMA has landed
+      lds_barrier();
     }
+    LSM_TICK(kTmDma);
+    // ---- 2. wave 0: headers, trailers, restart-interval numbering; owner[c] = block of interval c
+    if (wave == 0) {
+      uint32_t chains = 0;
+      BlockMeta m;
+      if ((uint32_t)lane < k) {
+        meta_header(img, (uint32_t)(G.off_j - G.span0), G.end_j - G.off_j, m);
+        m.item0 = G.it0_j - G.g_item0;
+        m.hdr_st = m.st;
+        m.ck_bad = 0;
+        meta_trailer(img, P.expect_type, G.it1_j - G.it0_j, m);
+        chains = m.st == ST_OK ? m.bin_len : 0;
+      }
+      const uint32_t incl = wave_incl_scan_u32(chains);
+      if ((uint32_t)lane < k) {
+        m.chain0 = incl - chains;
+        meta[lane] = m;
+        for (uint32_t r = 0; r < chains; ++r) owner[m.chain0 + r] = (uint8_t)lane;
+      }
+    }
+    lds_barrier();
+    LSM_TICK(kTmHdr);
+    // ---- 3. phase A on nA waves (64 intervals each)  ||  payload checksums on the others
+    {
+      const uint32_t total = (P.flags & kDiagSkipParse) ? 0
+                             : meta[k - 1].chain0 + (meta[k - 1].st == ST_OK ? meta[k - 1].bin_len : 0);
+      const uint32_t nA = min((total + kWave - 1) / kWave, kGroupWaves - 1);
+      const uint32_t role = (wave + kGroupWaves - iter % kGroupWaves) % kGroupWaves;  // rotates per group
+      if (role < nA) {
+        phase_a(img, meta, owner, rec, role * kWave, nA * kWave, total, P.tile_items);
+        LSM_TICK(kTmA);
+      } else if (!(P.flags & kDiagSkipHash)) {
+        const uint32_t rows = (kGroupWaves - nA) * 4;
+        for (uint32_t jb = (role - nA) * 4 + (lane >> 4); jb < k; jb += rows) {
+          if (meta[jb].hdr_st != ST_OK) continue;
+          const uint32_t hb = meta[jb].hb, len = meta[jb].len;
+          uint64_t lo, hi;
+          xxh3_128_row(img, hb + kHdrLen, len - kHdrLen, lo, hi);
+          if ((lane & 15) == 0 && (lo != meta[jb].ck_lo || hi != meta[jb].ck_hi)) meta[jb].ck_bad = 1;
+        }
+        LSM_TICK(kTmHash);
+      }
+    }
+    lds_barrier();
+    LSM_TICK(kTmSplit);
+    // ---- 4. phase B: thread = record; full parse + validation; coalesced stores
+    if (!(P.flags & (kDiagSkipParse | kDiagSkipPhaseB))) phase_b(P, img, meta, rec, G.n_items, G.g_item0);
+    LSM_TICK(kTmB);
+    lds_barrier();
+    if (wave == 0 && (uint32_t)lane < k) {
+      const BlockMeta& m = meta[lane];
+      gstore(P.status, b + lane, m.hdr_st != ST_OK ? m.hdr_st : (m.ck_bad ? (int32_t)ST_CKSUM : m.st));
+    }
+    b += k;
+    if constexpr (timed) tm[kTmGroups] += 1;
+    LSM_TICK(kTmTail);
   }
+#undef LSM_TICK
+  if (timed && lane == 0) {
+    // each wave adds its own view; phase A / hash slots only from the waves that ran them
+    for (int i = 0; i < kTmN; ++i) atomicAdd(&g_decode_timers[i], (unsigned long long)tm[i]);
+  }
+}
+
+hipError_t read_decode_timers(uint64_t* host, int n, bool reset) {
+  hipError_t e = hipMemcpyFromSymbol(host, HIP_SYMBOL(g_decode_timers), sizeof(uint64_t) * (n < kTmN ? n : kTmN));
+  if (e != hipSuccess || !reset) return e;
+  static const unsigned long long zero[kTmN] = {};
+  return hipMemcpyToSymbol(HIP_SYMBOL(g_decode_timers), zero, sizeof(zero));
 }
 
 // item counts from the trailers (trailer.rs:57-75), same rule as
@@ -572,13 +628,16 @@ hipError_t launch_decode(const DecodeParams& P0, void* ws, hipStream_t st) {
   if (lds > 64 * 1024) {
     hipError_t e = hipFuncSetAttribute((const void*)decode_blocks_kernel<false>,
                                        hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
+    if (e == hipSuccess)
+      e = hipFuncSetAttribute((const void*)decode_blocks_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
+                              (int)lds);
     if (e != hipSuccess) return e;
   }
   const uint32_t grid = (P.n_blocks + P.blocks_per_wave - 1) / P.blocks_per_wave;
-  if (P.stage_bytes <= kPipeChunks * 1024 && !(P.flags & kDiagNoPipe))
-    hipLaunchKernelGGL(decode_blocks_kernel<true>, dim3(grid), dim3(64), lds, st, P);
+  if (P.flags & kDiagTimers)
+    hipLaunchKernelGGL(decode_blocks_kernel<true>, dim3(grid), dim3(kGroupWaves * kWave), lds, st, P);
   else
-    hipLaunchKernelGGL(decode_blocks_kernel<false>, dim3(grid), dim3(64), lds, st, P);
+    hipLaunchKernelGGL(decode_blocks_kernel<false>, dim3(grid), dim3(kGroupWaves * kWave), lds, st, P);
   return hipGetLastError();
 }
 

@@ -27,6 +27,7 @@ struct DecodeParams {
 size_t decode_workspace_size(uint32_t n_blocks);
 uint32_t decode_lds_bytes(uint32_t stage_bytes, uint32_t tile_items, uint32_t blocks_per_wave);
 hipError_t launch_decode(const DecodeParams& P, void* workspace, hipStream_t st);
+hipError_t read_decode_timers(uint64_t* host, int n, bool reset);  // diagnostic
 
 hipError_t launch_xxh3_128_batch(const uint8_t* data, const uint64_t* off, uint32_t n, uint64_t* out,
                                  hipStream_t st);

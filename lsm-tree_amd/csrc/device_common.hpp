@@ -21,6 +21,18 @@ namespace lsmgpu {
 
 constexpr int kWave = 64;
 typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));
+
+// Explicit global-address-space access.  Generic (flat) pointers compile to
+// flat_load/flat_store, which count on lgkmcnt as well as vmcnt: every LDS
+// wait after a flat store would also wait for the store to reach memory.
+template <class T>
+__device__ __forceinline__ void gstore(T* p, uint64_t i, T v) {
+  ((__attribute__((address_space(1))) T*)p)[i] = v;
+}
+template <class T>
+__device__ __forceinline__ T gload(const T* p, uint64_t i) {
+  return ((const __attribute__((address_space(1))) T*)p)[i];
+}
 constexpr uint32_t kHdrLen = 33;
 constexpr uint32_t kTrailerLen = 31;
 constexpr uint8_t kTrailerMarker = 0xFF;

@@ -29,7 +29,7 @@ def main():
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--rounds", type=int, default=3)
     ap.add_argument("--tunings", default="32,16384,384;32,8192,192;32,12288,256;32,24576,640;16,16384,384")
-    ap.add_argument("--ablate", default="32,16384,384")
+    ap.add_argument("--ablate", default="48,65536,1024")
     ap.add_argument("--workload", default="counter", choices=["counter", "prefix16k"])
     args = ap.parse_args()
     torch.cuda.set_device(0)

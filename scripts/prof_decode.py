@@ -24,7 +24,7 @@ VARIANTS = [("full", 0), ("no-parse", 0x200), ("stage-only", 0x700), ("no-hash",
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--blocks", type=int, default=1 << 18)
-    ap.add_argument("--tuning", default="32,16384,384")
+    ap.add_argument("--tuning", default="48,65536,1024")
     ap.add_argument("--reps", type=int, default=2)
     args = ap.parse_args()
     torch.cuda.set_device(0)

@@ -287,3 +287,71 @@ def test_round_trip_tombstones_and_big_seqnos(gpu):
         g = gpu_decode(gpu, buf, off)
         parsed, item_start, status = pyoracle.decode_blocks(buf, off)
         compare_decode(g, parsed, item_start, status)
+
+
+def _mixed_items(n, seed):
+    """Sorted items whose seqno varint length varies record to record (1-9
+    bytes), keys 1-200 bytes (2-byte key lengths), values up to 300 bytes,
+    all four value types: every header shape the decoder distinguishes."""
+    rng = random.Random(seed)
+    raw = {}
+    while len(raw) < n:
+        k = bytes(rng.choice(b"abcdefgh") for _ in range(rng.choice([rng.randint(1, 12), rng.randint(1, 200)])))
+        s = rng.choice([rng.randint(0, 127), rng.randint(128, 1 << 14), rng.randint(1 << 14, 1 << 28),
+                        rng.getrandbits(63)])
+        t = rng.choice((0, 0, 0, 1, 2, 4))
+        v = b"" if t in (1, 2) else bytes(rng.getrandbits(8) for _ in range(rng.choice([rng.randint(0, 20),
+                                                                                         rng.randint(0, 300)])))
+        raw[(k, s)] = (v, t)
+    keys = sorted(raw, key=lambda ks: (ks[0], -ks[1]))
+    return pyoracle.Items.from_list([(k, raw[(k, s)][0], s, raw[(k, s)][1]) for k, s in keys])
+
+
+def _fuzz_blocks():
+    """Valid payloads, then one structural mutation each (record bytes,
+    varint continuation bits, binary-index entries incl. the first, item
+    count, trailer marker), re-sealed with a correct checksum."""
+    items = _mixed_items(6000, seed=21)
+    rng = random.Random(77)
+    blocks = []
+    first = 0
+    while first < items.n:
+        cnt = min(rng.randint(1, 40), items.n - first)
+        ri = rng.choice([1, 2, 4, 16, 32])
+        payload = bytearray(pyoracle.data_block_encode(items, first, cnt, restart_interval=ri,
+                                                       hash_ratio=rng.choice([0.0, 1.0])))
+        first += cnt
+        bin_len = int.from_bytes(payload[-29:-25], "little")
+        bin_off = int.from_bytes(payload[-25:-21], "little")
+        step = payload[-30]
+        rec_end = bin_off - 1
+        kind = rng.randrange(8)
+        if kind == 1 and rec_end > 0:
+            payload[rng.randrange(rec_end)] = rng.getrandbits(8)
+        elif kind == 2 and rec_end > 0:
+            payload[rng.randrange(rec_end)] |= 0x80
+        elif kind == 3:
+            r = rng.randrange(bin_len)
+            v = int.from_bytes(payload[bin_off + r * step:bin_off + (r + 1) * step], "little")
+            v = max(0, v + rng.choice([-2, -1, 1, 2]))
+            payload[bin_off + r * step:bin_off + (r + 1) * step] = (v & ((1 << (8 * step)) - 1)).to_bytes(step, "little")
+        elif kind == 4:
+            payload[-4] = (payload[-4] + rng.choice([1, 255])) & 0xFF
+        elif kind == 5:
+            payload[rec_end] = rng.getrandbits(8)
+        elif kind == 6 and rec_end > 1:
+            for _ in range(2):
+                payload[rng.randrange(rec_end)] ^= 1 << rng.randrange(8)
+        blocks.append(pyoracle.block_write(bytes(payload)))
+    return pack(blocks)
+
+
+def test_resealed_mutation_fuzz(gpu):
+    """The parser itself must reject or accept exactly as the oracle does."""
+    buf, off = _fuzz_blocks()
+    blocks = off[1:]
+    parsed, item_start, status = pyoracle.decode_blocks(buf, off)
+    assert (status == 0).sum() > len(blocks) // 4 and (status == 5).sum() > len(blocks) // 10
+    for tuning in (None, (1, 256, 64), (8, 8192, 256)):
+        g = gpu_decode(gpu, buf, off, tuning=tuning)
+        compare_decode(g, parsed, item_start, status)
