@@ -60,6 +60,18 @@ struct alignas(16) BlockMeta {
 };
 static_assert(sizeof(BlockMeta) == 80, "BlockMeta layout");
 
+// The kernel's DecodeParams in the kernarg segment.  Out-of-line helpers take
+// this pointer: taking the address of the by-value kernel parameter instead
+// makes the compiler copy it to scratch and reload its fields from there
+// (vmcnt waits in the hot loops).
+typedef const __attribute__((address_space(4))) DecodeParams* KArgs;
+__device__ __forceinline__ KArgs kargs() { return (KArgs)__builtin_amdgcn_kernarg_segment_ptr(); }
+__device__ __forceinline__ DecodeParams load_params(KArgs Pk) {
+  DecodeParams P;
+  __builtin_memcpy(&P, (const void*)Pk, sizeof(P));
+  return P;
+}
+
 __device__ __forceinline__ void wave_sync() {
   // Single-wave workgroups: LDS operations of a wave complete in order, so a
   // compiler barrier is all cross-lane LDS hand-offs need (no s_barrier, and
@@ -168,6 +180,19 @@ __device__ __forceinline__ bool parse_record(const uint8_t* base, uint32_t p0, u
   return ok;
 }
 
+// Out-of-line record walk that returns in registers (no address-taken
+// locals: results passed through scratch would put vmcnt waits — which also
+// drain the output stores — on the hot loops).  0 = malformed, else
+// bit 63 | key_off << 32 | next (payload-relative).
+__device__ __noinline__ uint64_t data_slow_next(const uint8_t* base, uint32_t p0, uint32_t pos, uint32_t end,
+                                                bool restart, uint32_t base_key) {
+  Cursor c;
+  c.init(base, p0, pos, end);
+  ItemFields f;
+  if (!parse_data_record(c, restart, base_key, f)) return 0;
+  return (1ULL << 63) | ((uint64_t)f.key_off << 32) | c.pos;
+}
+
 __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
 #pragma unroll
   for (int o = 1; o < kWave; o <<= 1) v = max(v, (uint32_t)__shfl_xor((int)v, o));
@@ -246,11 +271,9 @@ __device__ __forceinline__ void phase_a(const uint8_t* img, BlockMeta* meta, con
       sp = make_shape(min(hd.e1 >> 3, 5u), 1);
       const bool fast = hd.ok && valid_vtype(hd.vt) && m.type != 1;
       if (count > 1 && !fast) {
-        ItemFields tmp;
-        uint32_t tnext;
-        const bool sok = parse_data_slow(img, p0, a - p0, t.rec_end, true, 0, &tmp, &tnext);
-        nxt = sok ? p0 + tnext : rec_end;
-        key = p0 + tmp.key_off;
+        const uint64_t r2 = data_slow_next(img, p0, a - p0, t.rec_end, true, 0);
+        nxt = r2 ? p0 + (uint32_t)r2 : rec_end;
+        key = p0 + ((uint32_t)(r2 >> 32) & 0x7FFFFFFF);
       }
       const bool act = count > 0;
       if (count > 1) ok = nxt < rec_end;
@@ -270,10 +293,8 @@ __device__ __forceinline__ void phase_a(const uint8_t* img, BlockMeta* meta, con
         if (hd.ok) sp = make_shape(hd.e1 >> 3, (hd.e2 - hd.e1) >> 3);
         nxt = a + rec_len(hd.vt, hd.q, ld_u16u(img + a + hd.q));
         if (!hd.ok) {  // seqno >= 2^49, shared >= 2^21 or key length >= 128
-          ItemFields tmp;
-          uint32_t tnext;
-          const bool sok = parse_data_slow(img, p0, a - p0, t.rec_end, false, key - p0, &tmp, &tnext);
-          nxt = sok ? p0 + tnext : rec_end;
+          const uint64_t r2 = data_slow_next(img, p0, a - p0, t.rec_end, false, key - p0);
+          nxt = r2 ? p0 + (uint32_t)r2 : rec_end;
         }
       }
       const bool last = jj + 1 == count;
@@ -283,6 +304,40 @@ __device__ __forceinline__ void phase_a(const uint8_t* img, BlockMeta* meta, con
     }
     if (count && !ok) atomicCAS(&meta[j].st, ST_OK, ST_PARSE);  // walked off the record area
   }
+}
+
+__device__ __forceinline__ void store_fields(const DecodeParams& P, bool all_fields, uint64_t gi,
+                                             const ItemFields& f) {
+  if (all_fields) {  // common case: no per-field null checks
+    gstore(P.out.seqno, gi, f.seqno);
+    gstore(P.out.key_off, gi, f.key_off);
+    gstore(P.out.val_off, gi, f.val_off);
+    gstore(P.out.val_len, gi, f.val_len);
+    gstore(P.out.key_len, gi, f.key_len);
+    gstore(P.out.prefix_len, gi, f.prefix_len);
+    gstore(P.out.vtype, gi, f.vtype);
+    if (P.out.handle_off) gstore(P.out.handle_off, gi, f.handle_off);
+  } else {
+    emit_global(P.out, gi, f);
+  }
+}
+
+// Cursor parse + stores of one record, out of line (rare shapes, index
+// blocks).  Returns whether it parsed and ended at want.
+__device__ __noinline__ bool slow_record(KArgs Pk, const uint8_t* img, uint32_t p0, uint32_t a, uint32_t end,
+                                         uint32_t type, bool restart, uint32_t base_key, uint32_t want,
+                                         uint64_t gi) {
+  const DecodeParams P = load_params(Pk);
+  Cursor c;
+  c.init(img, p0, a, end);
+  ItemFields f;
+  const bool ok = type == 1 ? parse_index_record(c, f) : parse_data_record(c, restart, base_key, f);
+  if (ok && !(P.flags & kDiagSkipStore)) {
+    const bool all_fields = P.out.seqno && P.out.key_off && P.out.val_off && P.out.val_len && P.out.key_len &&
+                            P.out.prefix_len && P.out.vtype;
+    store_fields(P, all_fields, gi, f);
+  }
+  return ok && c.pos == want;
 }
 
 // Phase B: thread = record.  Full parse + validation of every descriptor
@@ -302,38 +357,25 @@ __device__ __forceinline__ void phase_b(const DecodeParams& P, const uint8_t* im
     const uint32_t j = (uint32_t)(d >> kRecBlockShift) & 31;
     const u32x4 hot = *reinterpret_cast<const u32x4*>(&meta[j]);  // p0, rec_end, st, type
     const uint32_t p0 = hot.x, end = hot.y - p0;
-    const bool live = (int32_t)hot.z == ST_OK;
+    if ((int32_t)hot.z != ST_OK) continue;  // block already failed: outputs unspecified
     const uint32_t a = ((uint32_t)d & 0xFFFF) - p0;
     const uint32_t want = ((uint32_t)(d >> kRecEndShift) & 0xFFFF) - p0;
     const uint32_t base_key = ((uint32_t)(d >> kRecKeyShift) & 0xFFFF) - p0;
     const bool restart = (d & kRecRestart) != 0;
+    const uint64_t gi = (uint64_t)g_item0 + i;
     ItemFields f;
     uint32_t next;
-    const int rc = parse_data_fast(img, p0, live ? a : 0, end, restart, base_key, f, next);
-    bool good = rc > 0 && next == want && hot.w != 1;
-    if (live && (rc == 0 || hot.w == 1)) {
-      ItemFields tmp;  // only the out-of-line paths take an address (keeps f in registers)
-      uint32_t tnext;
-      const bool sok = hot.w == 1 ? parse_index_slow(img, p0, a, end, &tmp, &tnext)
-                                  : parse_data_slow(img, p0, a, end, restart, base_key, &tmp, &tnext);
-      good = sok && tnext == want;
-      f = tmp;
-    }
-    if (live && !good) atomicCAS(&meta[j].st, ST_OK, ST_PARSE);
-    if (!store) continue;
-    const uint64_t gi = (uint64_t)g_item0 + i;
-    if (all_fields) {  // common case: no per-field null checks
-      gstore(P.out.seqno, gi, f.seqno);
-      gstore(P.out.key_off, gi, f.key_off);
-      gstore(P.out.val_off, gi, f.val_off);
-      gstore(P.out.val_len, gi, f.val_len);
-      gstore(P.out.key_len, gi, f.key_len);
-      gstore(P.out.prefix_len, gi, f.prefix_len);
-      gstore(P.out.vtype, gi, f.vtype);
-      if (P.out.handle_off) gstore(P.out.handle_off, gi, f.handle_off);
+    const int rc = hot.w == 1 ? 0 : parse_data_fast(img, p0, a, end, restart, base_key, f, next);
+    bool good;
+    if (rc > 0) {
+      good = next == want;
+      if (store) store_fields(P, all_fields, gi, f);
+    } else if (rc == 0) {
+      good = slow_record(kargs(), img, p0, a, end, hot.w, restart, base_key, want, gi);
     } else {
-      emit_global(P.out, gi, f);
+      good = false;
     }
+    if (!good) atomicCAS(&meta[j].st, ST_OK, ST_PARSE);
   }
 }
 
@@ -360,7 +402,8 @@ __device__ __forceinline__ bool walk_interval(const uint8_t* base, uint32_t p0, 
 }
 
 // One block straight from HBM (blocks larger than the LDS stage).
-__device__ __noinline__ void decode_block_direct(const DecodeParams& P, uint32_t b, BlockMeta* meta) {
+__device__ __noinline__ void decode_block_direct(KArgs Pk, uint32_t b, BlockMeta* meta) {
+  const DecodeParams P = load_params(Pk);
   const int lane = threadIdx.x;
   const uint64_t off = gload(P.block_off, b), end = gload(P.block_off, b + 1);
   const uint8_t* base = P.blocks + (off & ~15ULL);
@@ -487,7 +530,7 @@ __global__ __launch_bounds__(kGroupWaves * kWave) void decode_blocks_kernel(Deco
     const Group G = form_group(P, b, b_begin, b_end, gmax, offr, itr);
     LSM_TICK(kTmForm);
     if (G.k == 0) {
-      if (wave == 0) decode_block_direct(P, b, meta);
+      if (wave == 0) decode_block_direct(kargs(), b, meta);
       lds_barrier();
       b += 1;
       continue;
