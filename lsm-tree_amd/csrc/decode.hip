@@ -34,6 +34,11 @@ constexpr uint32_t kDiagSkipHash = 0x100, kDiagSkipParse = 0x200, kDiagSkipStore
                    kDiagSkipPhaseB = 0x800;
 
 constexpr uint32_t kMaxGroup = 32;  // blocks per staged group
+// Internal status: the block needs the general path (index block, a record
+// shape the straight-line parsers do not take, a block larger than the
+// stage).  The main kernel lists it; decode_deferred_kernel re-decodes it
+// from HBM with the LEB cursor and writes the final status.
+constexpr int32_t ST_DEFER = 0x7F;
 constexpr uint32_t kStagePad = 256;  // readable LDS bytes past the span (fast parsers read <= 138)
 
 // Record descriptor (one u64 per group item, LDS), written by phase A, read
@@ -263,25 +268,21 @@ __device__ __forceinline__ void phase_a(const uint8_t* img, BlockMeta* meta, con
     const uint32_t max_count = __builtin_amdgcn_readfirstlane(wave_max_u32(count));
     if (!max_count) continue;
     Shape sp;
+    bool defer = false;  // a record shape the straight path does not take: whole block to the general path
     {  // restart head (full key: the value length is read separately)
       const Win16u w = ld_win16u(img + a);
       const RecHead hd = rec_head(w.lo, true);
-      uint32_t nxt = a + rec_len(hd.vt, hd.q, ld_u16u(img + a + hd.q));
+      const uint32_t nxt = a + rec_len(hd.vt, hd.q, ld_u16u(img + a + hd.q));
       key = a + hd.hdr;
       sp = make_shape(min(hd.e1 >> 3, 5u), 1);
-      const bool fast = hd.ok && valid_vtype(hd.vt) && m.type != 1;
-      if (count > 1 && !fast) {
-        const uint64_t r2 = data_slow_next(img, p0, a - p0, t.rec_end, true, 0);
-        nxt = r2 ? p0 + (uint32_t)r2 : rec_end;
-        key = p0 + ((uint32_t)(r2 >> 32) & 0x7FFFFFFF);
-      }
-      const bool act = count > 0;
-      if (count > 1) ok = nxt < rec_end;
+      defer = count > 1 && !(hd.ok && valid_vtype(hd.vt));
+      const bool act = count > 0 && !defer;
+      if (count > 1 && act) ok = nxt < rec_end;
       rec[act ? ib0 : dummy] = rec_desc(a, count == 1 ? stop : nxt, key, tag | kRecRestart);
       a = (act && ok) ? nxt : a;
     }
     for (uint32_t jj = 1; jj < max_count; ++jj) {
-      const bool act = jj < count && ok;
+      bool act = jj < count && ok && !defer;
       const Win16u w = ld_win16u(img + a);
       const uint32_t klen = (uint32_t)(w.lo >> sp.kshift) & 0x7F;
       const uint32_t q = sp.hdr + klen;
@@ -291,24 +292,27 @@ __device__ __forceinline__ void phase_a(const uint8_t* img, BlockMeta* meta, con
       if (act && (~w.lo & sp.msk) != sp.pat) {  // the header shape changed
         const RecHead hd = rec_head(w.lo, false);
         if (hd.ok) sp = make_shape(hd.e1 >> 3, (hd.e2 - hd.e1) >> 3);
+        defer = !hd.ok;  // seqno >= 2^49, shared >= 2^21 or key length >= 128
         nxt = a + rec_len(hd.vt, hd.q, ld_u16u(img + a + hd.q));
-        if (!hd.ok) {  // seqno >= 2^49, shared >= 2^21 or key length >= 128
-          const uint64_t r2 = data_slow_next(img, p0, a - p0, t.rec_end, false, key - p0);
-          nxt = r2 ? p0 + (uint32_t)r2 : rec_end;
-        }
+        act = hd.ok;
       }
       const bool last = jj + 1 == count;
       ok = ok && (!act || last || nxt < rec_end);
       rec[act ? ib0 + jj : dummy] = rec_desc(a, last ? stop : nxt, key, tag);
       a = (act && ok) ? nxt : a;
     }
-    if (count && !ok) atomicCAS(&meta[j].st, ST_OK, ST_PARSE);  // walked off the record area
+    if (defer) meta[j].st = ST_DEFER;                             // wins over PARSE
+    else if (count && !ok) atomicCAS(&meta[j].st, ST_OK, ST_PARSE);  // walked off the record area
   }
+}
+
+__host__ __device__ __forceinline__ bool all_fields(const lsm_parsed_items& o) {
+  return o.seqno && o.key_off && o.val_off && o.val_len && o.key_len && o.prefix_len && o.vtype && o.handle_off;
 }
 
 __device__ __forceinline__ void store_fields(const DecodeParams& P, bool all_fields, uint64_t gi,
                                              const ItemFields& f) {
-  if (all_fields) {  // common case: no per-field null checks
+  if (all_fields) {  // every output array present: no per-field null checks
     gstore(P.out.seqno, gi, f.seqno);
     gstore(P.out.key_off, gi, f.key_off);
     gstore(P.out.val_off, gi, f.val_off);
@@ -316,38 +320,20 @@ __device__ __forceinline__ void store_fields(const DecodeParams& P, bool all_fie
     gstore(P.out.key_len, gi, f.key_len);
     gstore(P.out.prefix_len, gi, f.prefix_len);
     gstore(P.out.vtype, gi, f.vtype);
-    if (P.out.handle_off) gstore(P.out.handle_off, gi, f.handle_off);
+    gstore(P.out.handle_off, gi, f.handle_off);
   } else {
     emit_global(P.out, gi, f);
   }
 }
 
-// Cursor parse + stores of one record, out of line (rare shapes, index
-// blocks).  Returns whether it parsed and ended at want.
-__device__ __noinline__ bool slow_record(KArgs Pk, const uint8_t* img, uint32_t p0, uint32_t a, uint32_t end,
-                                         uint32_t type, bool restart, uint32_t base_key, uint32_t want,
-                                         uint64_t gi) {
-  const DecodeParams P = load_params(Pk);
-  Cursor c;
-  c.init(img, p0, a, end);
-  ItemFields f;
-  const bool ok = type == 1 ? parse_index_record(c, f) : parse_data_record(c, restart, base_key, f);
-  if (ok && !(P.flags & kDiagSkipStore)) {
-    const bool all_fields = P.out.seqno && P.out.key_off && P.out.val_off && P.out.val_len && P.out.key_len &&
-                            P.out.prefix_len && P.out.vtype;
-    store_fields(P, all_fields, gi, f);
-  }
-  return ok && c.pos == want;
-}
-
 // Phase B: thread = record.  Full parse + validation of every descriptor
 // (the oracle's parse_data_item checks, and the record must end exactly at
 // the descriptor's end), then coalesced stores of all fields.
+template <bool kAllFields>
 __device__ __forceinline__ void phase_b(const DecodeParams& P, const uint8_t* img, BlockMeta* meta,
                                         const uint64_t* rec, uint32_t n_items, uint32_t g_item0) {
   const uint32_t tid = threadIdx.x, nthr = blockDim.x;
-  const bool all_fields = P.out.seqno && P.out.key_off && P.out.val_off && P.out.val_len && P.out.key_len &&
-                          P.out.prefix_len && P.out.vtype;
+  constexpr bool all_fields = kAllFields;
   const bool store = !(P.flags & kDiagSkipStore);
   for (uint32_t i0 = 0; i0 < n_items; i0 += nthr) {
     const uint32_t i = i0 + tid;
@@ -365,17 +351,10 @@ __device__ __forceinline__ void phase_b(const DecodeParams& P, const uint8_t* im
     const uint64_t gi = (uint64_t)g_item0 + i;
     ItemFields f;
     uint32_t next;
-    const int rc = hot.w == 1 ? 0 : parse_data_fast(img, p0, a, end, restart, base_key, f, next);
-    bool good;
-    if (rc > 0) {
-      good = next == want;
-      if (store) store_fields(P, all_fields, gi, f);
-    } else if (rc == 0) {
-      good = slow_record(kargs(), img, p0, a, end, hot.w, restart, base_key, want, gi);
-    } else {
-      good = false;
-    }
-    if (!good) atomicCAS(&meta[j].st, ST_OK, ST_PARSE);
+    const int rc = parse_data_fast(img, p0, a, end, restart, base_key, f, next);
+    if (rc > 0 && store) store_fields(P, all_fields, gi, f);
+    if (rc == 0) meta[j].st = ST_DEFER;  // wins over PARSE
+    else if (rc < 0 || next != want) atomicCAS(&meta[j].st, ST_OK, ST_PARSE);
   }
 }
 
@@ -402,8 +381,7 @@ __device__ __forceinline__ bool walk_interval(const uint8_t* base, uint32_t p0, 
 }
 
 // One block straight from HBM (blocks larger than the LDS stage).
-__device__ __noinline__ void decode_block_direct(KArgs Pk, uint32_t b, BlockMeta* meta) {
-  const DecodeParams P = load_params(Pk);
+__device__ __forceinline__ void decode_block_direct(const DecodeParams& P, uint32_t b, BlockMeta* meta) {
   const int lane = threadIdx.x;
   const uint64_t off = gload(P.block_off, b), end = gload(P.block_off, b + 1);
   const uint8_t* base = P.blocks + (off & ~15ULL);
@@ -473,6 +451,20 @@ __device__ __forceinline__ Group form_group(const DecodeParams& P, uint32_t b, u
   return G;
 }
 
+// Deferred-block list in the workspace: [count u32][pad][index u32 x n_blocks].
+__device__ __forceinline__ void defer_block(const DecodeParams& P, uint32_t b) {
+  const uint32_t slot = atomicAdd(P.defer_count, 1u);
+  gstore(P.defer_list, slot, b);
+}
+
+// General path for the deferred blocks: one wave per block, straight from
+// HBM, Cursor fallback for every record shape (decode_block_direct).
+__global__ __launch_bounds__(kWave) void decode_deferred_kernel(DecodeParams P) {
+  __shared__ BlockMeta meta[1];
+  const uint32_t n = gload(P.defer_count, 0);
+  for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) decode_block_direct(P, gload(P.defer_list, i), meta);
+}
+
 // Workgroup = kGroupWaves waves sharing one LDS stage of up to 64 KiB (16
 // 4-KiB blocks, ~64 restart intervals).  Per group:
 //   all waves   LDS-DMA of the span (wave w moves 1-KiB pieces w, w+4, ...)
@@ -491,7 +483,7 @@ constexpr uint32_t kDiagTimers = 0x2000;
 enum : int { kTmForm, kTmDma, kTmHdr, kTmA, kTmHash, kTmSplit, kTmB, kTmTail, kTmGroups, kTmN };
 __device__ unsigned long long g_decode_timers[kTmN];
 
-template <bool kTimed>
+template <bool kTimed, bool kAllFields>
 __global__ __launch_bounds__(kGroupWaves * kWave) void decode_blocks_kernel(DecodeParams P) {
   // LDS: [meta: G x 80 B][rec: u64 per item + 1 scratch][owner: u8 per item][staged bytes + pad]
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -529,9 +521,8 @@ __global__ __launch_bounds__(kGroupWaves * kWave) void decode_blocks_kernel(Deco
   for (uint32_t b = b_begin; b < b_end; ++iter) {
     const Group G = form_group(P, b, b_begin, b_end, gmax, offr, itr);
     LSM_TICK(kTmForm);
-    if (G.k == 0) {
-      if (wave == 0) decode_block_direct(kargs(), b, meta);
-      lds_barrier();
+    if (G.k == 0) {  // larger than the stage: general path
+      if (tid == 0) defer_block(P, b);
       b += 1;
       continue;
     }
@@ -559,6 +550,7 @@ __global__ __launch_bounds__(kGroupWaves * kWave) void decode_blocks_kernel(Deco
         m.hdr_st = m.st;
         m.ck_bad = 0;
         meta_trailer(img, P.expect_type, G.it1_j - G.it0_j, m);
+        if (m.st == ST_OK && m.type == 1) m.st = ST_DEFER;  // index blocks: general path
         chains = m.st == ST_OK ? m.bin_len : 0;
       }
       const uint32_t incl = wave_incl_scan_u32(chains);
@@ -594,12 +586,14 @@ __global__ __launch_bounds__(kGroupWaves * kWave) void decode_blocks_kernel(Deco
     lds_barrier();
     LSM_TICK(kTmSplit);
     // ---- 4. phase B: thread = record; full parse + validation; coalesced stores
-    if (!(P.flags & (kDiagSkipParse | kDiagSkipPhaseB))) phase_b(P, img, meta, rec, G.n_items, G.g_item0);
+    if (!(P.flags & (kDiagSkipParse | kDiagSkipPhaseB))) phase_b<kAllFields>(P, img, meta, rec, G.n_items, G.g_item0);
     LSM_TICK(kTmB);
     lds_barrier();
     if (wave == 0 && (uint32_t)lane < k) {
       const BlockMeta& m = meta[lane];
-      gstore(P.status, b + lane, m.hdr_st != ST_OK ? m.hdr_st : (m.ck_bad ? (int32_t)ST_CKSUM : m.st));
+      const int32_t st = m.hdr_st != ST_OK ? m.hdr_st : (m.ck_bad ? (int32_t)ST_CKSUM : m.st);
+      if (st == ST_DEFER) defer_block(P, b + lane);
+      else gstore(P.status, b + lane, st);
     }
     b += k;
     if constexpr (timed) tm[kTmGroups] += 1;
@@ -647,8 +641,12 @@ struct ItemStartOut {
   }
 };
 
+static size_t counts_bytes(uint32_t n_blocks) { return ((size_t)n_blocks * 8 + 255) / 256 * 256; }
+static size_t tiles_bytes(uint32_t n_blocks) { return (scan_tiles(n_blocks) * 8 + 255) / 256 * 256; }
+static size_t defer_bytes(uint32_t n_blocks) { return ((size_t)n_blocks * 4 + 256 + 255) / 256 * 256; }
+
 size_t decode_workspace_size(uint32_t n_blocks) {
-  return ((size_t)n_blocks * 8 + 255) / 256 * 256 + (scan_tiles(n_blocks) * 8 + 255) / 256 * 256;
+  return counts_bytes(n_blocks) + tiles_bytes(n_blocks) + defer_bytes(n_blocks);
 }
 
 uint32_t decode_lds_bytes(uint32_t stage_bytes, uint32_t tile_items, uint32_t blocks_per_wave) {
@@ -660,7 +658,14 @@ uint32_t decode_lds_bytes(uint32_t stage_bytes, uint32_t tile_items, uint32_t bl
 hipError_t launch_decode(const DecodeParams& P0, void* ws, hipStream_t st) {
   DecodeParams P = P0;
   uint64_t* counts = (uint64_t*)ws;
-  uint64_t* tiles = (uint64_t*)((uint8_t*)ws + ((size_t)P.n_blocks * 8 + 255) / 256 * 256);
+  uint64_t* tiles = (uint64_t*)((uint8_t*)ws + counts_bytes(P.n_blocks));
+  uint8_t* dws = (uint8_t*)ws + counts_bytes(P.n_blocks) + tiles_bytes(P.n_blocks);
+  P.defer_count = (uint32_t*)dws;
+  P.defer_list = (uint32_t*)(dws + 256);
+  {
+    hipError_t e = hipMemsetAsync(P.defer_count, 0, 4, st);
+    if (e != hipSuccess) return e;
+  }
   if (!(P.flags & LSM_DECODE_ITEM_START_VALID)) {
     hipLaunchKernelGGL(trailer_counts_kernel, dim3((P.n_blocks + 255) / 256), dim3(256), 0, st, P.blocks,
                        P.block_off, P.n_blocks, counts);
@@ -668,19 +673,28 @@ hipError_t launch_decode(const DecodeParams& P0, void* ws, hipStream_t st) {
     if (e != hipSuccess) return e;
   }
   const uint32_t lds = decode_lds_bytes(P.stage_bytes, P.tile_items, P.blocks_per_wave);
+  const bool timed = (P.flags & kDiagTimers) != 0, all = all_fields(P.out);
+  const void* fn = timed ? (all ? (const void*)decode_blocks_kernel<true, true> : (const void*)decode_blocks_kernel<true, false>)
+                         : (all ? (const void*)decode_blocks_kernel<false, true> : (const void*)decode_blocks_kernel<false, false>);
   if (lds > 64 * 1024) {
-    hipError_t e = hipFuncSetAttribute((const void*)decode_blocks_kernel<false>,
-                                       hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
-    if (e == hipSuccess)
-      e = hipFuncSetAttribute((const void*)decode_blocks_kernel<true>, hipFuncAttributeMaxDynamicSharedMemorySize,
-                              (int)lds);
+    hipError_t e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)lds);
     if (e != hipSuccess) return e;
   }
   const uint32_t grid = (P.n_blocks + P.blocks_per_wave - 1) / P.blocks_per_wave;
-  if (P.flags & kDiagTimers)
-    hipLaunchKernelGGL(decode_blocks_kernel<true>, dim3(grid), dim3(kGroupWaves * kWave), lds, st, P);
+  if (timed && all)
+    hipLaunchKernelGGL((decode_blocks_kernel<true, true>), dim3(grid), dim3(kGroupWaves * kWave), lds, st, P);
+  else if (timed)
+    hipLaunchKernelGGL((decode_blocks_kernel<true, false>), dim3(grid), dim3(kGroupWaves * kWave), lds, st, P);
+  else if (all)
+    hipLaunchKernelGGL((decode_blocks_kernel<false, true>), dim3(grid), dim3(kGroupWaves * kWave), lds, st, P);
   else
-    hipLaunchKernelGGL(decode_blocks_kernel<false>, dim3(grid), dim3(kGroupWaves * kWave), lds, st, P);
+    hipLaunchKernelGGL((decode_blocks_kernel<false, false>), dim3(grid), dim3(kGroupWaves * kWave), lds, st, P);
+  {
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+  }
+  const uint32_t dgrid = P.n_blocks < 4096 ? P.n_blocks : 4096;
+  if (dgrid) hipLaunchKernelGGL(decode_deferred_kernel, dim3(dgrid), dim3(kWave), 0, st, P);
   return hipGetLastError();
 }
 

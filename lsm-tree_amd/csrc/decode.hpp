@@ -22,6 +22,8 @@ struct DecodeParams {
   uint32_t stage_bytes;
   uint32_t tile_items;
   uint32_t flags;
+  uint32_t* defer_count;  // workspace: blocks handed to the general path
+  uint32_t* defer_list;
 };
 
 size_t decode_workspace_size(uint32_t n_blocks);
