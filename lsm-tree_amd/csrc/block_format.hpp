@@ -107,23 +107,13 @@ __device__ __forceinline__ bool parse_data_record(Cursor& c, bool restart, uint3
 
 // ---------------------------------------------------------------- fast path
 // The common record header (vtype, seqno <= 7 LEB bytes, shared <= 3 LEB
-// bytes, 1-byte key length) lies in the 8 bytes at the record start: one
-// unaligned 64-bit load (gfx950 serves unaligned ds_read_b64 and
-// global_load_dwordx2) decoded with bit tricks, then one dependent 16-bit load
-// at start + header + key length for a 1-2 byte value length.  Any other shape
+// bytes, 1-byte key length) lies in the 8 bytes at the record start, read as
+// aligned dwords + v_alignbyte (measured faster than unaligned ds_read_b64 /
+// b128 on gfx950) and decoded with bit tricks, then one dependent read at
+// start + header + key length for a 1-2 byte value length.  Any other shape
 // (seqno >= 2^49, key length >= 128, value length >= 2^14) takes the Cursor.
 // Loads may run up to 138 bytes past the record start; callers guarantee that
 // many readable bytes (LDS stage padding) or clamp (see parse_data_fast).
-__device__ __forceinline__ uint64_t ld_u64u(const uint8_t* p) {
-  uint64_t v;
-  __builtin_memcpy(&v, p, 8);
-  return v;
-}
-__device__ __forceinline__ uint32_t ld_u16u(const uint8_t* p) {
-  uint16_t v;
-  __builtin_memcpy(&v, p, 2);
-  return v;
-}
 __device__ __forceinline__ uint64_t leb_val8(uint64_t x, uint32_t n) {  // n in 1..8
   if (n < 8) x &= (1ULL << (8 * n)) - 1;
   x = ((x & 0x7F007F007F007F00ULL) >> 1) | (x & 0x007F007F007F007FULL);
@@ -155,17 +145,8 @@ __device__ __forceinline__ RecHead rec_head(uint64_t h, bool restart) {
   r.q = r.hdr + r.klen;  // <= 136
   return r;
 }
-// 16 bytes at p as two u64 (one unaligned ds_read_b128 / global_load_dwordx4)
-struct Win16u {
-  uint64_t lo, hi;
-};
-__device__ __forceinline__ Win16u ld_win16u(const uint8_t* p) {
-  Win16u w;
-  __builtin_memcpy(&w, p, 16);
-  return w;
-}
 // two bytes at offset q (q <= 14) of the window, branch-free
-__device__ __forceinline__ uint32_t win16u_u16(const Win16u& w, uint32_t q) {
+__device__ __forceinline__ uint32_t win16_u16(const Win16& w, uint32_t q) {
   const uint32_t d0 = (uint32_t)w.lo, d1 = (uint32_t)(w.lo >> 32), d2 = (uint32_t)w.hi, d3 = (uint32_t)(w.hi >> 32);
   const uint32_t qi = q >> 2;
   const uint32_t lo = qi == 0 ? d0 : qi == 1 ? d1 : qi == 2 ? d2 : d3;
@@ -187,10 +168,10 @@ __device__ __forceinline__ bool rec_vlen(uint32_t z, bool tomb, uint32_t& n4, ui
 __device__ __forceinline__ int parse_data_fast(const uint8_t* base, uint32_t p0, uint32_t pos, uint32_t end,
                                                bool restart, uint32_t base_key_off, ItemFields& f,
                                                uint32_t& next) {
-  const uint64_t h = ld_u64u(base + p0 + min(pos, end));  // >= 33 block bytes follow the marker
+  const uint64_t h = read_u64_unaligned(base, p0 + min(pos, end));  // >= 33 block bytes follow the marker
   const RecHead r = rec_head(h, restart);
   const bool tomb = is_tombstone(r.vt);
-  const uint32_t z = ld_u16u(base + p0 + min(pos + r.q, end));
+  const uint32_t z = read_u16_unaligned(base, p0 + min(pos + r.q, end));
   uint32_t n4, vl;
   const bool vl_ok = rec_vlen(z, tomb, n4, vl);
   const uint64_t seq = leb_val8(h >> 8, r.e1 >> 3);
@@ -210,23 +191,6 @@ __device__ __forceinline__ int parse_data_fast(const uint8_t* base, uint32_t p0,
   next = val_off + vl;
   const bool fast = r.ok && vl_ok;
   return (pos >= end || !valid_vtype(r.vt)) ? -1 : (!fast ? 0 : (bad ? -1 : 1));
-}
-
-// Record length only (decode phase A), at p with >= 138 readable bytes.
-// false = not the fast shape (caller takes the Cursor path).  A wrong length
-// for a malformed record is harmless: phase B re-parses every record and
-// checks it ends where the next begins.
-__device__ __forceinline__ bool data_record_len_fast(const uint8_t* p, bool restart, uint32_t& len,
-                                                     uint32_t& hdr) {
-  const Win16u w = ld_win16u(p);
-  const RecHead r = rec_head(w.lo, restart);
-  uint32_t z = win16u_u16(w, min(r.q, 14u));
-  if (r.q > 14) z = ld_u16u(p + r.q);  // long key suffix: one more LDS read
-  uint32_t n4, vl;
-  const bool vl_ok = rec_vlen(z, is_tombstone(r.vt), n4, vl);
-  len = r.q + n4 + vl;
-  hdr = r.hdr;
-  return r.ok && vl_ok && valid_vtype(r.vt);
 }
 
 // KeyedBlockHandle::parse_full, src/table/index_block/block_handle.rs:175-206.

@@ -270,9 +270,9 @@ __device__ __forceinline__ void phase_a(const uint8_t* img, BlockMeta* meta, con
     Shape sp;
     bool defer = false;  // a record shape the straight path does not take: whole block to the general path
     {  // restart head (full key: the value length is read separately)
-      const Win16u w = ld_win16u(img + a);
+      const Win16 w = read_win16(img, a);
       const RecHead hd = rec_head(w.lo, true);
-      const uint32_t nxt = a + rec_len(hd.vt, hd.q, ld_u16u(img + a + hd.q));
+      const uint32_t nxt = a + rec_len(hd.vt, hd.q, read_u16_unaligned(img, a + hd.q));
       key = a + hd.hdr;
       sp = make_shape(min(hd.e1 >> 3, 5u), 1);
       defer = count > 1 && !(hd.ok && valid_vtype(hd.vt));
@@ -283,17 +283,17 @@ __device__ __forceinline__ void phase_a(const uint8_t* img, BlockMeta* meta, con
     }
     for (uint32_t jj = 1; jj < max_count; ++jj) {
       bool act = jj < count && ok && !defer;
-      const Win16u w = ld_win16u(img + a);
+      const Win16 w = read_win16(img, a);
       const uint32_t klen = (uint32_t)(w.lo >> sp.kshift) & 0x7F;
       const uint32_t q = sp.hdr + klen;
-      uint32_t z = win16u_u16(w, min(q, 14u));
-      if (q > 14) z = ld_u16u(img + a + q);  // long key suffix: one more LDS read
+      uint32_t z = win16_u16(w, min(q, 14u));
+      if (q > 14) z = read_u16_unaligned(img, a + q);  // long key suffix: one more LDS read
       uint32_t nxt = a + rec_len((uint32_t)w.lo & 0xFF, q, z);
       if (act && (~w.lo & sp.msk) != sp.pat) {  // the header shape changed
         const RecHead hd = rec_head(w.lo, false);
         if (hd.ok) sp = make_shape(hd.e1 >> 3, (hd.e2 - hd.e1) >> 3);
         defer = !hd.ok;  // seqno >= 2^49, shared >= 2^21 or key length >= 128
-        nxt = a + rec_len(hd.vt, hd.q, ld_u16u(img + a + hd.q));
+        nxt = a + rec_len(hd.vt, hd.q, read_u16_unaligned(img, a + hd.q));
         act = hd.ok;
       }
       const bool last = jj + 1 == count;

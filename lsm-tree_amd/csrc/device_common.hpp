@@ -144,6 +144,11 @@ __device__ __forceinline__ uint32_t read_u32_unaligned(const uint8_t* base, uint
   const uint32_t a = pos & ~3u, s = pos & 3u;
   return alignbyte(ld32(base, a + 4), ld32(base, a), s);
 }
+__device__ __forceinline__ uint64_t read_u64_unaligned(const uint8_t* base, uint32_t pos) {
+  const uint32_t a = pos & ~3u, s = pos & 3u;
+  const uint32_t d0 = ld32(base, a), d1 = ld32(base, a + 4), d2 = ld32(base, a + 8);
+  return (uint64_t)alignbyte(d1, d0, s) | ((uint64_t)alignbyte(d2, d1, s) << 32);
+}
 __device__ __forceinline__ uint16_t read_u16_unaligned(const uint8_t* base, uint32_t pos) {
   return (uint16_t)(read_u32_unaligned(base, pos) & 0xFFFF);
 }
