@@ -26,6 +26,7 @@ def main():
     ap.add_argument("--blocks", type=int, default=1 << 18)
     ap.add_argument("--tuning", default="48,65536,1024")
     ap.add_argument("--reps", type=int, default=2)
+    ap.add_argument("--variants", default=",".join(v for v, _ in VARIANTS))
     args = ap.parse_args()
     torch.cuda.set_device(0)
     nb = args.blocks
@@ -37,11 +38,13 @@ def main():
     torch.cuda.synchronize()
     v = [int(x, 0) for x in args.tuning.split(",")]
     base, xf = tuple(v[:3]), (v[3] if len(v) > 3 else 0)
+    chosen = [(v, f) for v, f in VARIANTS if v in args.variants.split(",")]
     for _ in range(args.reps):
-        for name, fl in VARIANTS:
+        for name, fl in chosen:
             dec.decode(enc["buf"], enc["block_off"], nb, out, n_items, tuning=base + (1 | xf | fl,))
     torch.cuda.synchronize()
-    print("variants:", [v for v, _ in VARIANTS], "reps", args.reps, "blocks", nb)
+    print("variants:", [v for v, _ in chosen], "reps", args.reps, "blocks", nb, "bytes",
+          int(enc["block_off"][nb].item()), "items", n_items)
 
 
 if __name__ == "__main__":

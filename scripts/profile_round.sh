@@ -1,0 +1,24 @@
+#!/bin/bash
+# Round profile: rocprofv3 kernel-trace stats of a short bench run, and the
+# two PMC passes (separate runs, no tracing domains) for HBM traffic.
+# Usage (on the GPU box): scripts/profile_round.sh rNN
+set -e
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+export TMPDIR=/tmp
+R=${1:-r01}
+OUT=gpurun_out/prof_$R
+mkdir -p $OUT
+timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/kt -o bench --output-format csv -- \
+  python3 bench.py --steps 10 --warmup 2 --no-cpu > $OUT/bench_kt.log 2>&1
+NB=1048576
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o pmc -- \
+  python3 scripts/prof_decode.py --variants full --reps 4 --blocks $NB > $OUT/fetch.log 2>&1
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o pmc -- \
+  python3 scripts/prof_decode.py --variants full --reps 4 --blocks $NB > $OUT/write.log 2>&1
+line=$(grep "^variants:" $OUT/fetch.log)
+BYTES=$(echo "$line" | sed 's/.* bytes \([0-9]*\) items.*/\1/')
+ITEMS=$(echo "$line" | sed 's/.* items \([0-9]*\).*/\1/')
+python3 scripts/traffic_summary.py $OUT/fetch $OUT/write $NB $BYTES $ITEMS > $OUT/traffic.json
+cat $OUT/traffic.json
+find $OUT/kt -name "*kernel_stats.csv" -exec cp {} $OUT/kernel_stats.csv \;
+head -20 $OUT/kernel_stats.csv
