@@ -254,8 +254,10 @@ struct HeaderInfo {
   uint32_t data_length;
   uint32_t type;
 };
-__device__ __forceinline__ int32_t check_header(const uint8_t* base, uint32_t hb, uint64_t len,
-                                                HeaderInfo& h) {
+// Header fields and the structural checks before the header checksum
+// (header.rs:116-169 order); check_header adds the checksum.
+__device__ __forceinline__ int32_t check_header_fields(const uint8_t* base, uint32_t hb, uint64_t len,
+                                                       HeaderInfo& h) {
   if (len < 4) return ST_TRUNCATED;
   const uint32_t magic = read_u32_unaligned(base, hb);
   if (magic != 0x034D534CU) return ST_BAD_MAGIC;  // "LSM\x03", file.rs:8
@@ -263,14 +265,23 @@ __device__ __forceinline__ int32_t check_header(const uint8_t* base, uint32_t hb
   h.type = read_u32_unaligned(base, hb + 4) & 0xFF;
   if (h.type > 3) return ST_BAD_TYPE;
   if (len < kHdrLen) return ST_TRUNCATED;
-  uint64_t lo, hi;
-  xxh3_128_short(29, BaseReader8{base, hb}, BaseReader64{base, hb}, lo, hi);
-  if ((uint32_t)lo != read_u32_unaligned(base, hb + 29)) return ST_HDR_CKSUM;
   BaseReader64 r{base, hb};
   h.ck_lo = r(5);
   h.ck_hi = r(13);
   h.data_length = read_u32_unaligned(base, hb + 21);
   return ST_OK;
+}
+// header checksum: low 32 bits of xxh3_128 over the first 29 header bytes
+__device__ __forceinline__ bool header_cksum_ok(const uint8_t* base, uint32_t hb) {
+  uint64_t lo, hi;
+  xxh3_128_short(29, BaseReader8{base, hb}, BaseReader64{base, hb}, lo, hi);
+  return (uint32_t)lo == read_u32_unaligned(base, hb + 29);
+}
+__device__ __forceinline__ int32_t check_header(const uint8_t* base, uint32_t hb, uint64_t len,
+                                                HeaderInfo& h) {
+  const int32_t st = check_header_fields(base, hb, len, h);
+  if (st != ST_OK) return st;
+  return header_cksum_ok(base, hb) ? ST_OK : ST_HDR_CKSUM;
 }
 
 }  // namespace lsmgpu

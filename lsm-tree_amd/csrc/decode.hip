@@ -31,7 +31,7 @@ namespace lsmgpu {
 // Diagnostic-only flags (lsm_decode_tuning.flags high bits): drop one phase to
 // price it in a profile.  Outputs are NOT valid with any of them set.
 constexpr uint32_t kDiagSkipHash = 0x100, kDiagSkipParse = 0x200, kDiagSkipStore = 0x400,
-                   kDiagSkipPhaseB = 0x800;
+                   kDiagSkipPhaseB = 0x800, kPrioA = 0x4000;
 
 constexpr uint32_t kMaxGroup = 32;  // blocks per staged group
 // Internal status: the block needs the general path (index block, a record
@@ -44,8 +44,10 @@ constexpr uint32_t kStagePad = 256;  // readable LDS bytes past the span (fast p
 // Record descriptor (one u64 per group item, LDS), written by phase A, read
 // by phase B: image offsets of the record start, of where it must end (the
 // next record's start, or the interval's end for its last record) and of its
-// restart head's key; [48,53) group block, 53 restart head, 54 valid.
-constexpr int kRecEndShift = 16, kRecKeyShift = 32, kRecBlockShift = 48;
+// restart head's key; [48,53) group block, 53 restart head, 54 valid,
+// [55,58) seqno bytes and [58,60) shared bytes of a header shape phase A has
+// verified (0 = not verified: phase B decodes the header itself).
+constexpr int kRecEndShift = 16, kRecKeyShift = 32, kRecBlockShift = 48, kRecN1Shift = 55, kRecN2Shift = 58;
 constexpr uint64_t kRecRestart = 1ULL << 53, kRecValid = 1ULL << 54;
 
 struct alignas(16) BlockMeta {
@@ -60,8 +62,9 @@ struct alignas(16) BlockMeta {
   uint32_t ri, step, bin_len, bin_off, item_count;
   uint32_t item0;     // first output index relative to the group base
   uint32_t chain0;    // exclusive prefix of restart intervals in the group
-  int32_t hdr_st;     // header-level status (gates the payload checksum)
-  uint32_t ck_bad;    // payload checksum mismatch
+  int32_t hdr_st;     // header-level status before the header checksum (gates hashing)
+  uint16_t ck_bad;    // payload checksum mismatch
+  uint16_t hck_bad;   // header checksum mismatch
 };
 static_assert(sizeof(BlockMeta) == 80, "BlockMeta layout");
 
@@ -114,6 +117,21 @@ __device__ __forceinline__ void meta_header(const uint8_t* base, uint32_t hb, ui
   m.rec_end = 0;
   m.len = (uint32_t)len;
   m.st = (len > 0xFFFFFF00ULL) ? ST_TRUNCATED : check_header(base, hb, len, h);
+  m.ck_lo = h.ck_lo;
+  m.ck_hi = h.ck_hi;
+  m.type = h.type;
+  m.item_count = h.data_length;  // stash data_length until meta_trailer
+  m.chain0 = 0;
+}
+
+// Staged kernel: the same without the header checksum (the hash waves check it).
+__device__ __forceinline__ void meta_header_fields(const uint8_t* base, uint32_t hb, uint64_t len, BlockMeta& m) {
+  HeaderInfo h;
+  m.hb = hb;
+  m.p0 = hb + kHdrLen;
+  m.rec_end = 0;
+  m.len = (uint32_t)len;
+  m.st = (len > 0xFFFFFF00ULL) ? ST_TRUNCATED : check_header_fields(base, hb, len, h);
   m.ck_lo = h.ck_lo;
   m.ck_hi = h.ck_hi;
   m.type = h.type;
@@ -214,14 +232,25 @@ __device__ __forceinline__ uint64_t rec_desc(uint32_t a, uint32_t end, uint32_t 
 struct Shape {
   uint32_t hdr, kshift;
   uint64_t msk, pat;
+  uint64_t bits;  // descriptor shape bits
 };
 __device__ __forceinline__ Shape make_shape(uint32_t n1, uint32_t n2) {
   Shape s;
+  s.bits = ((uint64_t)n1 << kRecN1Shift) | ((uint64_t)n2 << kRecN2Shift);
   s.hdr = n1 + n2 + 2;  // <= 8
   s.kshift = 8 * (s.hdr - 1);
   s.msk = 0x8080808080808000ULL & (s.hdr >= 8 ? ~0ULL : ((1ULL << (8 * s.hdr)) - 1));
   s.pat = (0x80ULL << (8 * n1)) | (0x80ULL << (8 * (n1 + n2))) | (0x80ULL << (8 * (s.hdr - 1)));
   return s;
+}
+
+// Value length from the two bytes z after the key; ok = 1-2 byte varint.
+__device__ __forceinline__ void rec_value(uint32_t vt, uint32_t z, uint32_t& n4, uint32_t& vl, bool& ok) {
+  const bool tomb = vt - 1u < 2u;
+  const bool two = (z & 0x80) != 0;
+  ok = tomb || (z & 0x8080) != 0x8080;
+  n4 = tomb ? 0 : (two ? 2 : 1);
+  vl = tomb ? 0 : (two ? ((z & 0x7F) | ((z >> 1) & 0x3F80)) : (z & 0x7F));
 }
 
 // Record length from the key length and the two bytes z after the key
@@ -278,7 +307,8 @@ __device__ __forceinline__ void phase_a(const uint8_t* img, BlockMeta* meta, con
       defer = count > 1 && !(hd.ok && valid_vtype(hd.vt));
       const bool act = count > 0 && !defer;
       if (count > 1 && act) ok = nxt < rec_end;
-      rec[act ? ib0 : dummy] = rec_desc(a, count == 1 ? stop : nxt, key, tag | kRecRestart);
+      const uint64_t rbits = (count > 1) ? ((uint64_t)(hd.e1 >> 3) << kRecN1Shift) : 0;  // verified only if walked
+      rec[act ? ib0 : dummy] = rec_desc(a, count == 1 ? stop : nxt, key, tag | kRecRestart | rbits);
       a = (act && ok) ? nxt : a;
     }
     for (uint32_t jj = 1; jj < max_count; ++jj) {
@@ -298,7 +328,7 @@ __device__ __forceinline__ void phase_a(const uint8_t* img, BlockMeta* meta, con
       }
       const bool last = jj + 1 == count;
       ok = ok && (!act || last || nxt < rec_end);
-      rec[act ? ib0 + jj : dummy] = rec_desc(a, last ? stop : nxt, key, tag);
+      rec[act ? ib0 + jj : dummy] = rec_desc(a, last ? stop : nxt, key, tag | sp.bits);
       a = (act && ok) ? nxt : a;
     }
     if (defer) meta[j].st = ST_DEFER;                             // wins over PARSE
@@ -306,8 +336,39 @@ __device__ __forceinline__ void phase_a(const uint8_t* img, BlockMeta* meta, con
   }
 }
 
+// parse_data_fast for a record whose header shape (n1 seqno bytes, n2 shared
+// bytes, 1-byte key length) phase A has already verified bit for bit.
+__device__ __forceinline__ int parse_data_shape(const uint8_t* base, uint32_t p0, uint32_t pos, uint32_t end,
+                                                bool restart, uint32_t base_key_off, uint32_t n1, uint32_t n2,
+                                                ItemFields& f, uint32_t& next) {
+  const uint64_t h = read_u64_unaligned(base, p0 + pos);
+  const uint32_t hdr = n1 + (restart ? 0u : n2) + 2;
+  const uint32_t klen = (uint32_t)(h >> (8 * (hdr - 1))) & 0x7F;
+  const uint32_t q = hdr + klen;
+  const uint32_t vt = (uint32_t)h & 0xFF;
+  uint32_t n4, vl;
+  bool vl_ok;
+  rec_value(vt, read_u16_unaligned(base, p0 + min(pos + q, end)), n4, vl, vl_ok);
+  const uint32_t shared = restart ? 0u : (uint32_t)leb_val8(h >> (8 * (n1 + 1)), n2) & 0xFFFF;
+  const uint32_t val_off = pos + q + n4;
+  f.seqno = leb_val8(h >> 8, n1);
+  f.handle_off = 0;
+  f.key_off = pos + hdr;
+  f.key_len = (uint16_t)klen;
+  f.prefix_len = (uint16_t)shared;
+  f.val_off = val_off;
+  f.val_len = vl;
+  f.vtype = (uint8_t)vt;
+  next = val_off + vl;
+  const bool bad = (pos + q + n4 > end) || ((uint64_t)val_off + vl > end) ||
+                   (!restart && (uint64_t)base_key_off + shared > end);
+  return !valid_vtype(vt) ? -1 : (!vl_ok ? 0 : (bad ? -1 : 1));
+}
+
+// The seven data-block fields present (handle_off is an index-block field,
+// stored only when requested).
 __host__ __device__ __forceinline__ bool all_fields(const lsm_parsed_items& o) {
-  return o.seqno && o.key_off && o.val_off && o.val_len && o.key_len && o.prefix_len && o.vtype && o.handle_off;
+  return o.seqno && o.key_off && o.val_off && o.val_len && o.key_len && o.prefix_len && o.vtype;
 }
 
 __device__ __forceinline__ void store_fields(const DecodeParams& P, bool all_fields, uint64_t gi,
@@ -320,7 +381,7 @@ __device__ __forceinline__ void store_fields(const DecodeParams& P, bool all_fie
     gstore(P.out.key_len, gi, f.key_len);
     gstore(P.out.prefix_len, gi, f.prefix_len);
     gstore(P.out.vtype, gi, f.vtype);
-    gstore(P.out.handle_off, gi, f.handle_off);
+    if (P.out.handle_off) gstore(P.out.handle_off, gi, f.handle_off);
   } else {
     emit_global(P.out, gi, f);
   }
@@ -351,7 +412,9 @@ __device__ __forceinline__ void phase_b(const DecodeParams& P, const uint8_t* im
     const uint64_t gi = (uint64_t)g_item0 + i;
     ItemFields f;
     uint32_t next;
-    const int rc = parse_data_fast(img, p0, a, end, restart, base_key, f, next);
+    const uint32_t n1 = (uint32_t)(d >> kRecN1Shift) & 7, n2 = (uint32_t)(d >> kRecN2Shift) & 3;
+    const int rc = n1 ? parse_data_shape(img, p0, a, end, restart, base_key, n1, n2, f, next)
+                      : parse_data_fast(img, p0, a, end, restart, base_key, f, next);
     if (rc > 0 && store) store_fields(P, all_fields, gi, f);
     if (rc == 0) meta[j].st = ST_DEFER;  // wins over PARSE
     else if (rc < 0 || next != want) atomicCAS(&meta[j].st, ST_OK, ST_PARSE);
@@ -545,10 +608,11 @@ __global__ __launch_bounds__(kGroupWaves * kWave) void decode_blocks_kernel(Deco
       uint32_t chains = 0;
       BlockMeta m;
       if ((uint32_t)lane < k) {
-        meta_header(img, (uint32_t)(G.off_j - G.span0), G.end_j - G.off_j, m);
+        meta_header_fields(img, (uint32_t)(G.off_j - G.span0), G.end_j - G.off_j, m);
         m.item0 = G.it0_j - G.g_item0;
         m.hdr_st = m.st;
         m.ck_bad = 0;
+        m.hck_bad = 0;
         meta_trailer(img, P.expect_type, G.it1_j - G.it0_j, m);
         if (m.st == ST_OK && m.type == 1) m.st = ST_DEFER;  // index blocks: general path
         chains = m.st == ST_OK ? m.bin_len : 0;
@@ -569,7 +633,11 @@ __global__ __launch_bounds__(kGroupWaves * kWave) void decode_blocks_kernel(Deco
       const uint32_t nA = min((total + kWave - 1) / kWave, kGroupWaves - 1);
       const uint32_t role = (wave + kGroupWaves - iter % kGroupWaves) % kGroupWaves;  // rotates per group
       if (role < nA) {
+        // the serial walk is the group's critical path: let it win issue
+        // arbitration against the other workgroup's waves on this SIMD
+        if (P.flags & kPrioA) __builtin_amdgcn_s_setprio(3);
         phase_a(img, meta, owner, rec, role * kWave, nA * kWave, total, P.tile_items);
+        if (P.flags & kPrioA) __builtin_amdgcn_s_setprio(0);
         LSM_TICK(kTmA);
       } else if (!(P.flags & kDiagSkipHash)) {
         const uint32_t rows = (kGroupWaves - nA) * 4;
@@ -578,7 +646,11 @@ __global__ __launch_bounds__(kGroupWaves * kWave) void decode_blocks_kernel(Deco
           const uint32_t hb = meta[jb].hb, len = meta[jb].len;
           uint64_t lo, hi;
           xxh3_128_row(img, hb + kHdrLen, len - kHdrLen, lo, hi);
-          if ((lane & 15) == 0 && (lo != meta[jb].ck_lo || hi != meta[jb].ck_hi)) meta[jb].ck_bad = 1;
+          const bool hck = header_cksum_ok(img, hb);
+          if ((lane & 15) == 0) {
+            meta[jb].ck_bad = lo != meta[jb].ck_lo || hi != meta[jb].ck_hi;
+            meta[jb].hck_bad = !hck;
+          }
         }
         LSM_TICK(kTmHash);
       }
@@ -591,7 +663,10 @@ __global__ __launch_bounds__(kGroupWaves * kWave) void decode_blocks_kernel(Deco
     lds_barrier();
     if (wave == 0 && (uint32_t)lane < k) {
       const BlockMeta& m = meta[lane];
-      const int32_t st = m.hdr_st != ST_OK ? m.hdr_st : (m.ck_bad ? (int32_t)ST_CKSUM : m.st);
+      const int32_t st = m.hdr_st != ST_OK ? m.hdr_st
+                         : m.hck_bad ? (int32_t)ST_HDR_CKSUM
+                         : m.ck_bad  ? (int32_t)ST_CKSUM
+                                     : m.st;
       if (st == ST_DEFER) defer_block(P, b + lane);
       else gstore(P.status, b + lane, st);
     }

@@ -58,6 +58,7 @@ def main():
     variants["ablate no-parse"] = a + (1 | xf | SKIP_PARSE,)
     variants["ablate no-store"] = a + (1 | xf | SKIP_STORE,)
     variants["ablate phase-A only"] = a + (1 | xf | 0x800,)
+    variants["ablate A no-hash"] = a + (1 | xf | 0x800 | SKIP_HASH,)
     variants["ablate stage-only"] = a + (1 | xf | SKIP_HASH | SKIP_PARSE | SKIP_STORE,)
     times = {k: [] for k in variants}
     for _ in range(args.rounds):
