@@ -269,3 +269,21 @@ def items_to_device(items_np, device="cuda"):
     d["handle_off"] = torch.from_numpy(items_np.handle_off.view(np.int64)).to(device)
     d["handle_size"] = torch.from_numpy(items_np.handle_size.view(np.int32)).to(device)
     return d
+
+
+def shard_blocks(block_off, world):
+    """Split n blocks into `world` contiguous shards of about equal BYTES
+    (blocks are independent, so shards need no exchange).
+    block_off: host array-like of n+1 offsets.  Returns world+1 block indices
+    b[0]=0 <= b[1] <= ... <= b[world]=n; rank r decodes blocks [b[r], b[r+1])."""
+    import numpy as np
+    off = np.asarray(block_off, dtype=np.uint64)
+    n = len(off) - 1
+    total = int(off[-1] - off[0])
+    bounds = [0]
+    for r in range(1, world):
+        target = int(off[0]) + total * r // world
+        b = int(np.searchsorted(off[:n], np.uint64(target), side="left"))
+        bounds.append(max(bounds[-1], min(b, n)))
+    bounds.append(n)
+    return bounds
