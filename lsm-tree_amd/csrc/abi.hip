@@ -19,7 +19,7 @@ int set_hip_error(hipError_t e, const char* where) {
 }
 
 constexpr uint32_t kDefaultBlocksPerWave = 48;  // per 4-wave workgroup
-constexpr uint32_t kDefaultStageBytes = lsmgpu::kMaxStageBytes;
+constexpr uint32_t kDefaultStageBytes = 65536;
 constexpr uint32_t kDefaultTileItems = 1024;
 
 }  // namespace
@@ -86,8 +86,7 @@ int lsm_decode_blocks_tuned(const uint8_t* d_blocks, const uint64_t* d_block_off
   P.tile_items = (tuning && tuning->tile_items) ? tuning->tile_items : kDefaultTileItems;
   P.flags = tuning ? tuning->flags : 0;
   P.stage_bytes = (P.stage_bytes + 15) & ~15u;
-  if (P.tile_items > 8192 || P.stage_bytes < 256 || P.stage_bytes > lsmgpu::kMaxStageBytes ||
-      P.blocks_per_wave > 63)
+  if (P.tile_items > 8192 || P.stage_bytes < 256 || P.stage_bytes > 65536 || P.blocks_per_wave > 63)
     return LSM_BAD_ARG;
   const uint32_t lds = lsmgpu::decode_lds_bytes(P.stage_bytes, P.tile_items, P.blocks_per_wave);
   if (lds > 160 * 1024) return LSM_BAD_ARG;

@@ -514,47 +514,7 @@ __device__ __forceinline__ Group form_group(const DecodeParams& P, uint32_t b, u
   return G;
 }
 
-constexpr uint32_t kGroupWaves = 4;
-constexpr uint32_t kPrefetch = 16;  // 1-KiB pieces per wave: 4 waves x 16 KiB = a 64 KiB stage
-static_assert(kPrefetch * kGroupWaves * 1024 == kMaxStageBytes, "stage = prefetch capacity");
-
-// Unconditional, clamped accesses (lanes past the span repeat its last
-// granule): conditional loads into a register array make the allocator keep
-// extra copies of it.
-__device__ __forceinline__ void prefetch_span(const DecodeParams& P, const Group& G, uint32_t wave, int lane,
-                                              u32x4 (&R)[kPrefetch]) {
-  if (G.k == 0) return;
-  const uint32_t last = (uint32_t)((G.span1 - G.span0) >> 4) - 1;
-  const __attribute__((address_space(1))) uint8_t* src = (const __attribute__((address_space(1))) uint8_t*)(P.blocks + G.span0);
-#pragma unroll
-  for (uint32_t i = 0; i < kPrefetch; ++i) {
-    const uint32_t o = 16u * min((wave + kGroupWaves * i) * kWave + lane, last);  // 32-bit lane offset: saddr form
-    R[i] = __builtin_nontemporal_load((const __attribute__((address_space(1))) u32x4*)(src + o));
-  }
-}
-__device__ __forceinline__ void land_span(const Group& G, uint32_t wave, int lane, const u32x4 (&R)[kPrefetch],
-                                          uint8_t* img) {
-  const uint32_t last = (uint32_t)((G.span1 - G.span0) >> 4) - 1;
-  u32x4* dst = reinterpret_cast<u32x4*>(img);
-#pragma unroll
-  for (uint32_t i = 0; i < kPrefetch; ++i) dst[min((wave + kGroupWaves * i) * kWave + lane, last)] = R[i];
-}
-
 // Deferred-block list in the workspace: [count u32][pad][index u32 x n_blocks].
-__device__ __forceinline__ void defer_block(const DecodeParams& P, uint32_t b);
-
-// The next group at or after block b; blocks too large for the stage on
-// their own are handed to the general path on the way (k == 0: no more).
-__device__ __forceinline__ Group next_group(const DecodeParams& P, uint32_t b, uint32_t b_begin, uint32_t b_end,
-                                            uint32_t gmax, uint64_t offr, uint32_t itr) {
-  Group G = form_group(P, b, b_begin, b_end, gmax, offr, itr);
-  while (G.k == 0 && b < b_end) {
-    if (threadIdx.x == 0) defer_block(P, b);
-    G = form_group(P, ++b, b_begin, b_end, gmax, offr, itr);
-  }
-  return G;
-}
-
 __device__ __forceinline__ void defer_block(const DecodeParams& P, uint32_t b) {
   const uint32_t slot = atomicAdd(P.defer_count, 1u);
   gstore(P.defer_list, slot, b);
@@ -578,6 +538,7 @@ __global__ __launch_bounds__(kWave) void decode_deferred_kernel(DecodeParams P) 
 // pa rotates with the group index so the serial walk lands on each SIMD in
 // turn.  Phase A needs only the trailer, not the checksum, so it runs
 // concurrently with the hash; statuses merge in oracle order at the end.
+constexpr uint32_t kGroupWaves = 8;
 
 // Diagnostic phase timers (flag kDiagTimers): per workgroup clock64() deltas,
 // summed over the grid; read back with lsm_diag_decode_timers (abi.hip).
@@ -586,7 +547,7 @@ enum : int { kTmForm, kTmDma, kTmHdr, kTmA, kTmHash, kTmSplit, kTmB, kTmTail, kT
 __device__ unsigned long long g_decode_timers[kTmN];
 
 template <bool kTimed, bool kAllFields>
-__global__ __launch_bounds__(kGroupWaves * kWave) __attribute__((amdgpu_waves_per_eu(2))) void decode_blocks_kernel(DecodeParams P) {
+__global__ __launch_bounds__(kGroupWaves * kWave) __attribute__((amdgpu_waves_per_eu(4))) void decode_blocks_kernel(DecodeParams P) {
   // LDS: [meta: G x 80 B][rec: u64 per item + 1 scratch][owner: u8 per item][staged bytes + pad]
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint32_t gmax = min(kMaxGroup, P.blocks_per_wave);
@@ -606,8 +567,7 @@ __global__ __launch_bounds__(kGroupWaves * kWave) __attribute__((amdgpu_waves_pe
     offr = gload(P.block_off, b_begin + lane);
     itr = gload(P.item_start, b_begin + lane);
   }
-  // XXH3 long-path secret words in LDS: the hash loop then issues no global
-  // loads, which would otherwise wait (vmcnt is in order) for the prefetch.
+  // XXH3 long-path secret words in LDS (read per use by the lean row hash).
   LongSecret* ls = reinterpret_cast<LongSecret*>(img + ((P.stage_bytes + 15) & ~15u) + kStagePad);
   if (tid < sizeof(LongSecret) / 8)
     reinterpret_cast<uint64_t*>(ls)[tid] = reinterpret_cast<const uint64_t*>(&kLongSecret)[tid];
@@ -625,22 +585,27 @@ __global__ __launch_bounds__(kGroupWaves * kWave) __attribute__((amdgpu_waves_pe
     tm[slot] += t1 - t0;                                                                   \
     t0 = t1;                                                                               \
   }
-  // The next group's span is prefetched into registers (wave w holds 1-KiB
-  // pieces w, w+4, ... : 16 x dwordx4 per lane for a 64 KiB stage) while the
-  // current group is processed, and written to LDS at the top of the next
-  // iteration: HBM latency overlaps the walk, the hash and the stores.
-  u32x4 R[kPrefetch];
-  Group G = next_group(P, b_begin, b_begin, b_end, gmax, offr, itr);
-  prefetch_span(P, G, wave, lane, R);
-  while (G.k) {
+  for (uint32_t b = b_begin; b < b_end; ++iter) {
+    const Group G = form_group(P, b, b_begin, b_end, gmax, offr, itr);
     LSM_TICK(kTmForm);
-    const uint32_t b = G.b, k = G.k;
-    // ---- 1. land the prefetched span in LDS, prefetch the next group, clear the descriptors
-    land_span(G, wave, lane, R, img);
-    const Group N = next_group(P, b + k, b_begin, b_end, gmax, offr, itr);
-    prefetch_span(P, N, wave, lane, R);
-    for (uint32_t i = tid; i < G.n_items; i += kGroupWaves * kWave) rec[i] = 0;
-    lds_barrier();
+    if (G.k == 0) {  // larger than the stage: general path
+      if (tid == 0) defer_block(P, b);
+      b += 1;
+      continue;
+    }
+    const uint32_t k = G.k;
+    // ---- 1. stage the span HBM -> LDS (LDS-DMA), clear the record descriptors
+    {
+      const uint32_t chunks = (uint32_t)((G.span1 - G.span0) >> 4);
+      const uint8_t* src = P.blocks + G.span0 + 16 * lane;
+      for (uint32_t i = wave; i * kWave < chunks; i += kGroupWaves) {
+        if (i * kWave + lane < chunks)
+          __builtin_amdgcn_global_load_lds((gbl_void_t*)(src + 1024 * i), (lds_void_t*)(img + 1024 * i), 16, 0, 0);
+      }
+      for (uint32_t i = tid; i < G.n_items; i += kGroupWaves * kWave) rec[i] = 0;
+      __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0): this wave's DMA has landed
+      lds_barrier();
+    }
     LSM_TICK(kTmDma);
     // ---- 2. wave 0: headers, trailers, restart-interval numbering; owner[c] = block of interval c
     if (wave == 0) {
@@ -685,7 +650,7 @@ __global__ __launch_bounds__(kGroupWaves * kWave) __attribute__((amdgpu_waves_pe
           const uint32_t hb = meta[jb].hb, len = meta[jb].len;
           uint64_t lo, hi;
           const uint32_t plen = len - kHdrLen;
-          if (plen > 240) xxh3_128_row_long(img, hb + kHdrLen, plen, ls, lo, hi);
+          if (plen > 240) xxh3_128_row_long_lean(img, hb + kHdrLen, plen, ls, lo, hi);
           else xxh3_128_short(plen, BaseReader8{img, hb + kHdrLen}, BaseReader64{img, hb + kHdrLen}, lo, hi);
           const bool hck = header_cksum_ok(img, hb);
           if ((lane & 15) == 0) {
@@ -711,9 +676,7 @@ __global__ __launch_bounds__(kGroupWaves * kWave) __attribute__((amdgpu_waves_pe
       if (st == ST_DEFER) defer_block(P, b + lane);
       else gstore(P.status, b + lane, st);
     }
-    lds_barrier();  // the stage and descriptors are free for the next group
-    G = N;
-    ++iter;
+    b += k;
     if constexpr (timed) tm[kTmGroups] += 1;
     LSM_TICK(kTmTail);
   }

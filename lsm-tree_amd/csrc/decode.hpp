@@ -8,10 +8,6 @@
 
 namespace lsmgpu {
 
-// Largest LDS stage (bytes of one group's span) the decode kernel supports:
-// 4 waves x 16 KiB of register prefetch (decode.hip kPrefetch).
-constexpr uint32_t kMaxStageBytes = 65536;
-
 struct DecodeParams {
   const uint8_t* blocks;
   const uint64_t* block_off;

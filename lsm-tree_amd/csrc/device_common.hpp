@@ -566,6 +566,56 @@ __device__ __forceinline__ void xxh3_128_row_long(const uint8_t* base, uint32_t 
   out_hi = xxh3_avalanche(~((uint64_t)len * P64_2) + thi);
 }
 
+// Register-lean variant of xxh3_128_row_long for kernels that run 4 waves per
+// SIMD: the stripe secret words are read from an LDS copy of LongSecret as
+// they are needed and one 16-byte window is in flight per step (occupancy
+// hides the LDS latency instead of registers).
+__device__ __forceinline__ void xxh3_128_row_long_lean(const uint8_t* base, uint32_t pos, uint32_t len,
+                                                       const LongSecret* ls, uint64_t& out_lo, uint64_t& out_hi) {
+  const int r = threadIdx.x & 15;
+  const int q = r & 3, s = r >> 2;
+  uint64_t a0 = q == 0 ? (uint64_t)P32_3 : q == 1 ? P64_2 : q == 2 ? P64_4 : P64_5;
+  uint64_t a1 = q == 0 ? P64_1 : q == 1 ? P64_3 : q == 2 ? (uint64_t)P32_2 : (uint64_t)P32_1;
+  const uint32_t nb_blocks = (len - 1) / 1024;
+  const uint64_t* acc = ls->acc + s + 2 * q;
+  for (uint32_t n = 0; n < nb_blocks; ++n) {
+    uint64_t c0 = 0, c1 = 0;
+#pragma unroll 2
+    for (int t = 0; t < 4; ++t) {
+      const Win16 w = read_win16(base, pos + n * 1024 + 256 * t + 16 * r);
+      stripe_part(w, acc[4 * t], acc[4 * t + 1], c0, c1);
+    }
+    c0 = row_quad_sum64(c0);
+    c1 = row_quad_sum64(c1);
+    a0 += c0; a0 ^= a0 >> 47; a0 ^= ls->acc[16 + 2 * q]; a0 *= P32_1;
+    a1 += c1; a1 ^= a1 >> 47; a1 ^= ls->acc[16 + 2 * q + 1]; a1 *= P32_1;
+  }
+  {
+    const uint32_t tail0 = nb_blocks * 1024;
+    const uint32_t nb_stripes = ((len - 1) - tail0) / 64;
+    uint64_t c0 = 0, c1 = 0;
+#pragma unroll 1
+    for (int t = 0; t < 4; ++t) {
+      if ((uint32_t)(4 * t + s) < nb_stripes) {
+        const Win16 w = read_win16(base, pos + tail0 + 256 * t + 16 * r);
+        stripe_part(w, acc[4 * t], acc[4 * t + 1], c0, c1);
+      }
+    }
+    if (r < 4) {  // last stripe: input[len-64 .. len), secret + 121
+      const Win16 w = read_win16(base, pos + len - 64 + 16 * r);
+      stripe_part(w, ls->last[2 * q], ls->last[2 * q + 1], c0, c1);
+    }
+    a0 += row_quad_sum64(c0);
+    a1 += row_quad_sum64(c1);
+  }
+  uint64_t tlo = mul_fold64(a0 ^ ls->mlo[2 * q], a1 ^ ls->mlo[2 * q + 1]);
+  uint64_t thi = mul_fold64(a0 ^ ls->mhi[2 * q], a1 ^ ls->mhi[2 * q + 1]);
+  tlo = quad_sum64(tlo);
+  thi = quad_sum64(thi);
+  out_lo = xxh3_avalanche((uint64_t)len * P64_1 + tlo);
+  out_hi = xxh3_avalanche(~((uint64_t)len * P64_2) + thi);
+}
+
 __device__ __forceinline__ void xxh3_128_row(const uint8_t* base, uint32_t pos, uint32_t len,
                                              uint64_t& lo, uint64_t& hi) {
   if (len > 240) {
