@@ -311,19 +311,29 @@ __device__ __forceinline__ void phase_a(const uint8_t* img, BlockMeta* meta, con
       rec[act ? ib0 : dummy] = rec_desc(a, count == 1 ? stop : nxt, key, tag | kRecRestart | rbits);
       a = (act && ok) ? nxt : a;
     }
+    // The value-length bytes are read at the PREDICTED key end (the previous
+    // record's header + key length: fixed-size keys and a stable shared
+    // prefix repeat it) in parallel with the header read, so the chain is one
+    // LDS round trip; a different key length costs one more read.
+    uint32_t qp = 0;
     for (uint32_t jj = 1; jj < max_count; ++jj) {
       bool act = jj < count && ok && !defer;
-      const Win16 w = read_win16(img, a);
-      const uint32_t klen = (uint32_t)(w.lo >> sp.kshift) & 0x7F;
+      const uint64_t h = read_u64_unaligned(img, a);
+      const uint32_t zp = read_u16_unaligned(img, a + qp);
+      const uint32_t klen = (uint32_t)(h >> sp.kshift) & 0x7F;
       const uint32_t q = sp.hdr + klen;
-      uint32_t z = win16_u16(w, min(q, 14u));
-      if (q > 14) z = read_u16_unaligned(img, a + q);  // long key suffix: one more LDS read
-      uint32_t nxt = a + rec_len((uint32_t)w.lo & 0xFF, q, z);
-      if (act && (~w.lo & sp.msk) != sp.pat) {  // the header shape changed
-        const RecHead hd = rec_head(w.lo, false);
+      uint32_t z = zp;
+      if (q != qp) {  // key length changed (or first record): read at the real key end
+        z = read_u16_unaligned(img, a + q);
+        qp = q;
+      }
+      uint32_t nxt = a + rec_len((uint32_t)h & 0xFF, q, z);
+      if (act && (~h & sp.msk) != sp.pat) {  // the header shape changed
+        const RecHead hd = rec_head(h, false);
         if (hd.ok) sp = make_shape(hd.e1 >> 3, (hd.e2 - hd.e1) >> 3);
         defer = !hd.ok;  // seqno >= 2^49, shared >= 2^21 or key length >= 128
         nxt = a + rec_len(hd.vt, hd.q, read_u16_unaligned(img, a + hd.q));
+        qp = hd.q;
         act = hd.ok;
       }
       const bool last = jj + 1 == count;
