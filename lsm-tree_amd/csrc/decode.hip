@@ -311,35 +311,36 @@ __device__ __forceinline__ void phase_a(const uint8_t* img, BlockMeta* meta, con
       rec[act ? ib0 : dummy] = rec_desc(a, count == 1 ? stop : nxt, key, tag | kRecRestart | rbits);
       a = (act && ok) ? nxt : a;
     }
-    // The value-length bytes are read at the PREDICTED key end (the previous
-    // record's header + key length: fixed-size keys and a stable shared
-    // prefix repeat it) in parallel with the header read, so the chain is one
-    // LDS round trip; a different key length costs one more read.
+    // The straight-line step, kept short because it is one wave's serial
+    // instruction stream: the key length is read at the header length of the
+    // previous record's shape and the value length at its key end (both
+    // loads issued together); a shape or key-length change takes the rare
+    // branch.  No bounds bookkeeping here: positions are clamped to the
+    // marker and phase B rejects any record that does not end where its
+    // descriptor says.
     uint32_t qp = 0;
+    uint32_t hi = (uint32_t)((((uint64_t)key << kRecKeyShift) | tag | sp.bits) >> 32);
+    const uint32_t dmy = dummy;
     for (uint32_t jj = 1; jj < max_count; ++jj) {
-      bool act = jj < count && ok && !defer;
       const uint64_t h = read_u64_unaligned(img, a);
-      const uint32_t zp = read_u16_unaligned(img, a + qp);
+      uint32_t z = read_u16_unaligned(img, a + qp);
       const uint32_t klen = (uint32_t)(h >> sp.kshift) & 0x7F;
-      const uint32_t q = sp.hdr + klen;
-      uint32_t z = zp;
-      if (q != qp) {  // key length changed (or first record): read at the real key end
-        z = read_u16_unaligned(img, a + q);
-        qp = q;
-      }
-      uint32_t nxt = a + rec_len((uint32_t)h & 0xFF, q, z);
-      if (act && (~h & sp.msk) != sp.pat) {  // the header shape changed
+      uint32_t q = sp.hdr + klen;
+      uint32_t vt = (uint32_t)h & 0xFF;
+      if (((~h & sp.msk) != sp.pat) | (q != qp)) {  // rare: header shape or key length changed
         const RecHead hd = rec_head(h, false);
         if (hd.ok) sp = make_shape(hd.e1 >> 3, (hd.e2 - hd.e1) >> 3);
-        defer = !hd.ok;  // seqno >= 2^49, shared >= 2^21 or key length >= 128
-        nxt = a + rec_len(hd.vt, hd.q, read_u16_unaligned(img, a + hd.q));
-        qp = hd.q;
-        act = hd.ok;
+        defer = defer || (jj < count && !hd.ok);  // seqno >= 2^49, shared >= 2^21 or key length >= 128
+        q = hd.q;
+        z = read_u16_unaligned(img, a + q);
+        qp = q;
+        hi = (uint32_t)((((uint64_t)key << kRecKeyShift) | tag | sp.bits) >> 32);
       }
-      const bool last = jj + 1 == count;
-      ok = ok && (!act || last || nxt < rec_end);
-      rec[act ? ib0 + jj : dummy] = rec_desc(a, last ? stop : nxt, key, tag | sp.bits);
-      a = (act && ok) ? nxt : a;
+      const uint32_t nxt = min(a + rec_len(vt, q, z), rec_end);
+      const bool act = jj < count && !defer;
+      const uint32_t end = jj + 1 == count ? stop : nxt;
+      rec[act ? ib0 + jj : dmy] = ((uint64_t)hi << 32) | (uint64_t)(a | (end << kRecEndShift));
+      a = act ? nxt : a;
     }
     if (defer) meta[j].st = ST_DEFER;                             // wins over PARSE
     else if (count && !ok) atomicCAS(&meta[j].st, ST_OK, ST_PARSE);  // walked off the record area

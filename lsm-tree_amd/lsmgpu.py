@@ -173,6 +173,8 @@ class Decoder:
 
     def decode(self, blocks, block_off, n_blocks, out, item_cap, expect_type=-1, tuning=None, stream=None):
         """Enqueue lsm_decode_blocks. blocks: uint8 cuda (padded); block_off: int64 cuda [n+1]."""
+        if tuning is None and os.environ.get("LSMGPU_DECODE_TUNING"):  # diagnostic override
+            tuning = tuple(int(x, 0) for x in os.environ["LSMGPU_DECODE_TUNING"].split(","))
         ws = self.workspace(n_blocks)
         ps = LsmParsed()
         for f, _ in PARSED_FIELDS:
