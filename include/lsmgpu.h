@@ -109,13 +109,22 @@ typedef struct lsm_block_params {
 
 /* Tuning knobs for the decode kernel (0 = library default). */
 typedef struct lsm_decode_tuning {
-    uint32_t blocks_per_wave;  /* consecutive blocks one workgroup owns (1..63) */
-    uint32_t stage_bytes;      /* LDS bytes per workgroup for staged block bytes (<= 65536) */
-    uint32_t tile_items;       /* LDS output tile capacity in items */
+    uint32_t blocks_per_wave;  /* LSM_DECODE_LEGACY only: consecutive blocks one workgroup owns (1..63) */
+    uint32_t stage_bytes;      /* LDS bytes per ring slot (default 32768; legacy: per stage, 65536) */
+    uint32_t tile_items;       /* items one slot (legacy: one stage) may hold (default 512) */
     uint32_t flags;            /* LSM_DECODE_ITEM_START_VALID: d_item_start already holds the
-                                  prefix sum of this batch (skip the count + scan pass) */
+                                  prefix sum of this batch (skip the count + scan pass);
+                                  LSM_DECODE_LEGACY / LSM_DECODE_RING: force the single-stage
+                                  kernel or the LDS-ring kernel (default: the faster one) */
+    uint32_t ring_slots;       /* LDS ring depth, 2..8 (default 4) */
+    uint32_t ring_walkers;     /* waves walking record boundaries (default 3) */
+    uint32_t ring_hashers;     /* waves verifying payload checksums (default 4); the other
+                                  16 - loaders - walkers - hashers waves parse and store */
+    uint32_t ring_loaders;     /* waves issuing the LDS-DMA of every group, 1..8 (default 4) */
 } lsm_decode_tuning;
 #define LSM_DECODE_ITEM_START_VALID 1u
+#define LSM_DECODE_LEGACY 0x10000u
+#define LSM_DECODE_RING 0x80000u
 
 int lsm_abi_version(void);
 const char* lsm_status_name(int status);

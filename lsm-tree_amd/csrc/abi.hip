@@ -18,9 +18,13 @@ int set_hip_error(hipError_t e, const char* where) {
   return LSM_HIP_ERROR;
 }
 
-constexpr uint32_t kDefaultBlocksPerWave = 48;  // per 4-wave workgroup
+// legacy single-stage kernel (LSM_DECODE_LEGACY)
+constexpr uint32_t kDefaultBlocksPerWave = 48;  // per workgroup
 constexpr uint32_t kDefaultStageBytes = 65536;
 constexpr uint32_t kDefaultTileItems = 1024;
+// ring kernel (default)
+constexpr uint32_t kRingSlotBytes = 32768, kRingTileItems = 512, kRingSlots = 4, kRingWalkers = 3,
+                   kRingHashers = 4, kRingLoaders = 4;
 
 }  // namespace
 
@@ -81,15 +85,29 @@ int lsm_decode_blocks_tuned(const uint8_t* d_blocks, const uint64_t* d_block_off
   P.item_start = d_item_start;
   P.item_start_w = d_item_start;
   P.status = d_status;
-  P.blocks_per_wave = (tuning && tuning->blocks_per_wave) ? tuning->blocks_per_wave : kDefaultBlocksPerWave;
-  P.stage_bytes = (tuning && tuning->stage_bytes) ? tuning->stage_bytes : kDefaultStageBytes;
-  P.tile_items = (tuning && tuning->tile_items) ? tuning->tile_items : kDefaultTileItems;
   P.flags = tuning ? tuning->flags : 0;
+  if (!(P.flags & (lsmgpu::kDecodeLegacy | lsmgpu::kDecodeRing)))
+    P.flags |= lsmgpu::kDecodeDefaultRing ? lsmgpu::kDecodeRing : lsmgpu::kDecodeLegacy;
+  const bool legacy = (P.flags & lsmgpu::kDecodeLegacy) != 0;
+  auto pick = [&](uint32_t v, uint32_t dflt) { return v ? v : dflt; };
+  P.blocks_per_wave = pick(tuning ? tuning->blocks_per_wave : 0, kDefaultBlocksPerWave);
+  P.stage_bytes = pick(tuning ? tuning->stage_bytes : 0, legacy ? kDefaultStageBytes : kRingSlotBytes);
+  P.tile_items = pick(tuning ? tuning->tile_items : 0, legacy ? kDefaultTileItems : kRingTileItems);
+  P.ring_slots = pick(tuning ? tuning->ring_slots : 0, kRingSlots);
+  P.ring_x = pick(tuning ? tuning->ring_walkers : 0, kRingWalkers);
+  P.ring_h = pick(tuning ? tuning->ring_hashers : 0, kRingHashers);
+  P.ring_l = pick(tuning ? tuning->ring_loaders : 0, kRingLoaders);
   P.stage_bytes = (P.stage_bytes + 15) & ~15u;
   if (P.tile_items > 8192 || P.stage_bytes < 256 || P.stage_bytes > 65536 || P.blocks_per_wave > 63)
     return LSM_BAD_ARG;
-  const uint32_t lds = lsmgpu::decode_lds_bytes(P.stage_bytes, P.tile_items, P.blocks_per_wave);
-  if (lds > 160 * 1024) return LSM_BAD_ARG;
+  if (legacy) {
+    if (lsmgpu::decode_lds_bytes(P.stage_bytes, P.tile_items, P.blocks_per_wave) > 160 * 1024) return LSM_BAD_ARG;
+  } else {
+    if (P.ring_slots < 2 || P.ring_slots > 8 || P.tile_items > 4096 || P.ring_l < 1 || P.ring_l > 8 ||
+        P.ring_l + P.ring_x + P.ring_h > lsmgpu::kRingWaves - 1)
+      return LSM_BAD_ARG;
+    if (lsmgpu::decode_ring_lds_bytes(P.ring_slots, P.stage_bytes, P.tile_items) > 160 * 1024) return LSM_BAD_ARG;
+  }
   hipError_t e = lsmgpu::launch_decode(P, d_workspace, (hipStream_t)stream);
   return e == hipSuccess ? LSM_OK : set_hip_error(e, "lsm_decode_blocks");
 }

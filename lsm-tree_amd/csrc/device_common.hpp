@@ -616,6 +616,70 @@ __device__ __forceinline__ void xxh3_128_row_long_lean(const uint8_t* base, uint
   out_hi = xxh3_avalanche(~((uint64_t)len * P64_2) + thi);
 }
 
+// Octet XXH3-128 (> 240 B): the 8 lanes of an aligned lane octet hash one
+// input, so a wave hashes eight blocks at once.  Lane r = lane & 7 owns
+// accumulator pair q = r >> 1 (acc[2q], acc[2q+1]) over stripes 2i + h of
+// every KiB, h = r & 1 (interleaved, so an octet reads 128 contiguous bytes
+// per step: no bank conflict between its halves).  Per KiB the two halves of
+// a pair meet in ONE DPP quad-perm step; each lane reads its 16-byte window
+// and its two secret words (one ds_read2_b64) per stripe.  All 8 lanes of the
+// octet must be active.
+template <int kCtrl>
+__device__ __forceinline__ uint64_t mov_dpp64(uint64_t v) {
+  const uint32_t lo = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)v, kCtrl, 0xF, 0xF, true);
+  const uint32_t hi = (uint32_t)__builtin_amdgcn_mov_dpp((int)(uint32_t)(v >> 32), kCtrl, 0xF, 0xF, true);
+  return (uint64_t)lo | ((uint64_t)hi << 32);
+}
+__device__ __forceinline__ void xxh3_128_oct_long(const uint8_t* base, uint32_t pos, uint32_t len,
+                                                  const LongSecret* ls, uint64_t& out_lo, uint64_t& out_hi) {
+  const int r = threadIdx.x & 7;
+  const int q = r >> 1, h = r & 1;
+  uint64_t a0 = q == 0 ? (uint64_t)P32_3 : q == 1 ? P64_2 : q == 2 ? P64_4 : P64_5;
+  uint64_t a1 = q == 0 ? P64_1 : q == 1 ? P64_3 : q == 2 ? (uint64_t)P32_2 : (uint64_t)P32_1;
+  const uint64_t scr0 = ls->acc[16 + 2 * q], scr1 = ls->acc[16 + 2 * q + 1];
+  const uint64_t* key = ls->acc + h + 2 * q;  // stripe 2i + h, pair q -> key[2i], key[2i + 1]
+  const uint32_t nb_blocks = (len - 1) / 1024;
+  const uint32_t lpos = pos + 64 * h + 16 * q;  // stripe h of KiB 0, this lane's 16 bytes
+  for (uint32_t n = 0; n < nb_blocks; ++n) {
+    uint64_t c0 = 0, c1 = 0;
+#pragma unroll 4
+    for (int i = 0; i < 8; ++i) {
+      const Win16 w = read_win16(base, lpos + 1024 * n + 128 * i);
+      stripe_part(w, key[2 * i], key[2 * i + 1], c0, c1);
+    }
+    c0 += mov_dpp64<0xB1>(c0);  // quad_perm [1,0,3,2]: the other half of the pair
+    c1 += mov_dpp64<0xB1>(c1);
+    a0 += c0; a0 ^= a0 >> 47; a0 ^= scr0; a0 *= P32_1;
+    a1 += c1; a1 ^= a1 >> 47; a1 ^= scr1; a1 *= P32_1;
+  }
+  {
+    const uint32_t tail0 = nb_blocks * 1024;
+    const uint32_t nb_stripes = ((len - 1) - tail0) / 64;
+    uint64_t c0 = 0, c1 = 0;
+#pragma unroll 1
+    for (uint32_t i = 0; i < 8; ++i) {
+      if (2 * i + h < nb_stripes) {
+        const Win16 w = read_win16(base, lpos + tail0 + 128 * i);
+        stripe_part(w, key[2 * i], key[2 * i + 1], c0, c1);
+      }
+    }
+    if (h == 0) {  // last stripe: input[len-64 .. len), secret + 121
+      const Win16 w = read_win16(base, pos + len - 64 + 16 * q);
+      stripe_part(w, ls->last[2 * q], ls->last[2 * q + 1], c0, c1);
+    }
+    a0 += c0 + mov_dpp64<0xB1>(c0);
+    a1 += c1 + mov_dpp64<0xB1>(c1);
+  }
+  uint64_t tlo = mul_fold64(a0 ^ ls->mlo[2 * q], a1 ^ ls->mlo[2 * q + 1]);
+  uint64_t thi = mul_fold64(a0 ^ ls->mhi[2 * q], a1 ^ ls->mhi[2 * q + 1]);
+  tlo += mov_dpp64<0x4E>(tlo);   // quad_perm [2,3,0,1]: pairs q ^ 1
+  thi += mov_dpp64<0x4E>(thi);
+  tlo += mov_dpp64<0x141>(tlo);  // row_half_mirror: the other quad of the octet (h-symmetric)
+  thi += mov_dpp64<0x141>(thi);
+  out_lo = xxh3_avalanche((uint64_t)len * P64_1 + tlo);
+  out_hi = xxh3_avalanche(~((uint64_t)len * P64_2) + thi);
+}
+
 __device__ __forceinline__ void xxh3_128_row(const uint8_t* base, uint32_t pos, uint32_t len,
                                              uint64_t& lo, uint64_t& hi) {
   if (len > 240) {

@@ -41,10 +41,13 @@ class LsmBlockParams(C.Structure):
 
 class LsmDecodeTuning(C.Structure):
     _fields_ = [("blocks_per_wave", C.c_uint32), ("stage_bytes", C.c_uint32), ("tile_items", C.c_uint32),
-                ("flags", C.c_uint32)]
+                ("flags", C.c_uint32), ("ring_slots", C.c_uint32), ("ring_walkers", C.c_uint32),
+                ("ring_hashers", C.c_uint32), ("ring_loaders", C.c_uint32)]
 
 
 DECODE_ITEM_START_VALID = 1
+DECODE_LEGACY = 0x10000  # force the single-stage kernel
+DECODE_RING = 0x80000  # force the LDS-ring kernel
 
 
 class LsmError(RuntimeError):

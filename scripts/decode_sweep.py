@@ -28,8 +28,8 @@ def main():
     ap.add_argument("--blocks", type=int, default=1 << 20)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--rounds", type=int, default=3)
-    ap.add_argument("--tunings", default="32,16384,384;32,8192,192;32,12288,256;32,24576,640;16,16384,384")
-    ap.add_argument("--ablate", default="48,65536,1024")
+    ap.add_argument("--tunings", default="48,65536,1024,0x10000;0,32768,512;0,32768,512,0x20000")
+    ap.add_argument("--ablate", default="0,32768,512")
     ap.add_argument("--workload", default="counter", choices=["counter", "prefix16k"])
     args = ap.parse_args()
     torch.cuda.set_device(0)
@@ -48,18 +48,21 @@ def main():
     assert int((out["status"][:nb] != 0).sum()) == 0
 
     variants = {}
+    def tun(v, extra=0):
+        v = list(v) + [0] * (7 - len(v))
+        v[3] |= 1 | extra
+        return tuple(v)
+
     for t in args.tunings.replace("/", ";").split(";"):
-        v = [int(x, 0) for x in t.split(",")]
-        variants[f"tune {t}"] = (v[0], v[1], v[2], 1 | (v[3] if len(v) > 3 else 0))
-    a = tuple(int(x, 0) for x in args.ablate.split(","))
-    xf = a[3] if len(a) > 3 else 0
-    a = a[:3]
-    variants["ablate no-hash"] = a + (1 | xf | SKIP_HASH,)
-    variants["ablate no-parse"] = a + (1 | xf | SKIP_PARSE,)
-    variants["ablate no-store"] = a + (1 | xf | SKIP_STORE,)
-    variants["ablate phase-A only"] = a + (1 | xf | 0x800,)
-    variants["ablate A no-hash"] = a + (1 | xf | 0x800 | SKIP_HASH,)
-    variants["ablate stage-only"] = a + (1 | xf | SKIP_HASH | SKIP_PARSE | SKIP_STORE,)
+        variants[f"tune {t}"] = tun([int(x, 0) for x in t.split(",")])
+    if args.ablate:
+        a = [int(x, 0) for x in args.ablate.split(",")]
+        variants["ablate no-hash"] = tun(a, SKIP_HASH)
+        variants["ablate no-parse"] = tun(a, SKIP_PARSE)
+        variants["ablate no-store"] = tun(a, SKIP_STORE)
+        variants["ablate phase-A only"] = tun(a, 0x800)
+        variants["ablate A no-hash"] = tun(a, 0x800 | SKIP_HASH)
+        variants["ablate stage-only"] = tun(a, SKIP_HASH | SKIP_PARSE | SKIP_STORE)
     times = {k: [] for k in variants}
     for _ in range(args.rounds):
         for name, tun in variants.items():

@@ -24,7 +24,7 @@ def main():
     for pdir in sorted(root.glob("p*")):
         if not pdir.is_dir():
             continue
-        rows = [r for r in load(pdir) if "decode_blocks_kernel" in r.get("Kernel_Name", "")]
+        rows = [r for r in load(pdir) if ("decode_blocks_kernel" in r.get("Kernel_Name", "") or "decode_ring_kernel" in r.get("Kernel_Name", ""))]
         by_disp = defaultdict(lambda: defaultdict(float))
         for r in rows:
             by_disp[int(r["Dispatch_Id"])][r["Counter_Name"]] += float(r["Counter_Value"])

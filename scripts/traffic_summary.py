@@ -18,7 +18,7 @@ def per_dispatch(d, counter):
     for f in Path(d).rglob("*counter_collection.csv"):
         with open(f) as fh:
             for r in csv.DictReader(fh):
-                if "decode_blocks_kernel" in r.get("Kernel_Name", "") and r["Counter_Name"] == counter:
+                if ("decode_blocks_kernel" in r.get("Kernel_Name", "") or "decode_ring_kernel" in r.get("Kernel_Name", "")) and r["Counter_Name"] == counter:
                     k = int(r["Dispatch_Id"])
                     vals[k] = vals.get(k, 0.0) + float(r["Counter_Value"])
     keys = sorted(vals)[1:]  # first dispatch: warm-up decode (computes item_start)

@@ -87,9 +87,25 @@ def test_decode_golden_blocks(gpu, golden_blocks):
             assert pyoracle.materialize(payload, one, case["restart_interval"]) == case_expected_items(case), case["name"]
 
 
-@pytest.mark.parametrize("tuning", [None, (1, 256, 64), (4, 4096, 64), (63, 65536, 2048)])
+LEG = 0x10000  # LSM_DECODE_LEGACY
+RING = 0x80000  # LSM_DECODE_RING
+# (blocks_per_wave, slot/stage bytes, tile items, flags, ring slots, planners, hashers, loaders)
+TUNINGS = [None,                                 # library default kernel
+           (0, 0, 0, RING),                      # ring defaults
+           (0, 256, 64, RING),                   # every block larger than a slot: general path
+           (0, 4096, 64, RING, 8, 1, 1),         # 8 small slots, 1 planner, 1 hasher, 10 parsers
+           (0, 65536, 1024, RING, 2, 5, 6),      # 2 x 64 KiB slots, 1 parser
+           (0, 32768, 512, RING, 4, 2, 2, 8),    # 8 loader waves
+           (0, 32768, 512, RING, 3, 3, 3, 1),    # a single loader wave
+           (0, 32768, 512, RING | 0x20000, 3),   # nt DMA, 3 slots
+           (0, 16384, 256, RING, 2, 1, 1),       # 2-slot ring
+           (48, 65536, 1024, LEG), (1, 256, 64, LEG), (63, 65536, 2048, LEG)]
+
+
+@pytest.mark.parametrize("tuning", TUNINGS)
 def test_decode_golden_blocks_tunings(gpu, golden_blocks, tuning):
-    """Staged path, direct-from-HBM path (tiny stage) and large groups agree."""
+    """Ring kernel under several slot/role shapes, the general path (tiny
+    slots) and the legacy single-stage kernel all agree with the oracle."""
     blocks = [bytes.fromhex(c["block"]) for c in golden_blocks]
     buf, off = pack(blocks)
     g = gpu_decode(gpu, buf, off, tuning=tuning)
