@@ -30,9 +30,17 @@
 
 namespace lsmgpu {
 
-constexpr uint32_t kPlanLarge = 1, kPlanBad = 2;
-constexpr uint32_t kE2Budget = 24 * 1024;  // LDS bytes per E2 wave
+// Block classes by the LDS image a block needs (e2_need): small blocks are
+// written by 4-wave workgroups with kImgSmall bytes of LDS per wave (8
+// workgroups per CU), medium and big ones by listed 1-wave workgroups, and
+// the rest straight in HBM (E3).
+constexpr uint32_t kPlanHuge = 1, kPlanBad = 2, kPlanMedium = 4, kPlanBig = 8;
+constexpr uint32_t kImgSmall = 5 * 1024;
+constexpr uint32_t kImgMedium = 20 * 1024;
+constexpr uint32_t kImgBig = 96 * 1024;
+constexpr uint32_t kSmallWaves = 4;
 constexpr uint32_t kE3HashChunk = 4096;    // buckets per LDS pass in E3
+enum : uint32_t { kListMedium = 0, kListBig = 1, kListHuge = 2, kLists = 3 };
 
 struct alignas(16) BlockPlan {
   uint32_t recs;      // bytes of all records
@@ -88,8 +96,8 @@ struct EncodeParams {
   uint16_t* shared;     // [n_items]
   uint64_t* sizes;      // [n_blocks]
   BlockPlan* plans;     // [n_blocks]
-  uint32_t* large_list; // [n_blocks]
-  uint32_t* large_count;
+  uint32_t* lists;      // [kLists][n_blocks]: medium, big, huge blocks
+  uint32_t* list_count; // [kLists]
 };
 
 __device__ __forceinline__ bool is_index(const EncodeParams& P) { return P.type == 1; }
@@ -114,20 +122,10 @@ __device__ __forceinline__ uint64_t record_len(const EncodeParams& P, uint64_t i
   return rec;
 }
 
-// LDS staging need of a block for E2 (see layout in encode_write_kernel).
-__device__ __forceinline__ uint64_t e2_need(const EncodeParams& P, uint32_t s, uint32_t e, uint64_t total,
-                                            uint32_t hash_w) {
-  const uint64_t ka = (uint64_t)(uintptr_t)P.it.keys + P.it.key_off[s];
-  const uint64_t kb = (uint64_t)(uintptr_t)P.it.keys + P.it.key_off[e];
-  uint64_t need = ((kb + 15) & ~15ULL) - (ka & ~15ULL) + 32;
-  if (!is_index(P)) {
-    const uint64_t va = (uint64_t)(uintptr_t)P.it.vals + P.it.val_off[s];
-    const uint64_t vb = (uint64_t)(uintptr_t)P.it.vals + P.it.val_off[e];
-    need += ((vb + 15) & ~15ULL) - (va & ~15ULL) + 32;
-  }
-  need += ((total + 16 + 15) & ~15ULL) + 32;
-  need += 8ULL * ((hash_w + 3) & ~3u);
-  return need;
+// LDS a block's image needs in E2: worst-case 16-B pad + the block + 32 B of
+// read slack for the window reads, then the hash-index vote arrays.
+__device__ __forceinline__ uint64_t e2_need(uint64_t total, uint32_t hash_w) {
+  return ((15 + total + 15) & ~15ULL) + 32 + 8ULL * ((hash_w + 3) & ~3u);
 }
 
 // ---------------------------------------------------------------- E1: sizes
@@ -178,10 +176,14 @@ __global__ __launch_bounds__(256) void encode_sizes_kernel(EncodeParams P) {
   if (bad) {
     flags = kPlanBad;
     P.status[b] = ST_BAD_ARG;
-  } else if (e2_need(P, s, e, total, hash_w) > kE2Budget) {
-    flags = kPlanLarge;
-    const uint32_t slot = atomicAdd(P.large_count, 1u);
-    P.large_list[slot] = b;
+  } else {
+    const uint64_t need = e2_need(total, hash_w);
+    if (need > kImgSmall) {
+      const uint32_t l = need <= kImgMedium ? kListMedium : need <= kImgBig ? kListBig : kListHuge;
+      flags = l == kListMedium ? kPlanMedium : l == kListBig ? kPlanBig : kPlanHuge;
+      const uint32_t slot = atomicAdd(&P.list_count[l], 1u);
+      P.lists[(size_t)l * P.n_blocks + slot] = b;
+    }
   }
   pl.recs = (uint32_t)carry;
   pl.bin_len = bin_len;
@@ -246,68 +248,124 @@ struct ByteWriter {
   }
 };
 
-// Source of item bytes: either staged LDS images or global arenas.
-struct ItemSrc {
-  const uint8_t* kbase;  // 16-aligned
-  uint64_t kshift;       // key i is at kbase + key_off[i] - kshift
-  const uint8_t* vbase;
-  uint64_t vshift;
+// n bytes from src (HBM, any alignment) to dst[d .. d + n) (any alignment).
+// Source: aligned 16-B windows, four (+1 lookahead) per round trip, moved to
+// the destination's dword phase with v_alignbyte; destination: dword stores,
+// at most 3 byte stores at either end (the seams shared with the records
+// written by the neighbouring lanes).
+__device__ __forceinline__ void copy_span(const uint8_t* src, uint8_t* dst, uint32_t d, uint32_t n) {
+  uint32_t h = (4u - (d & 3u)) & 3u;
+  if (h > n) h = n;
+  const uint32_t body = (n - h) >> 2;
+  if (body) {
+    const uint64_t ga = (uint64_t)(uintptr_t)(src + h);
+    const uint32_t sh = (uint32_t)ga & 3u;
+    const u32x4* W = reinterpret_cast<const u32x4*>(ga & ~15ULL);
+    const int off0 = (int)((ga >> 2) & 3);
+    // destination dword k = bytes of source dwords off0 + k and off0 + k + 1
+    const uint32_t nw = (off0 + body - 1 + (sh ? 1 : 0)) / 4 + 1;
+    uint32_t* D = reinterpret_cast<uint32_t*>(dst + d + h);
+    u32x4 cur = W[0];
+    for (uint32_t w0 = 0; w0 < nw; w0 += 4) {
+      u32x4 x1 = cur, x2 = cur, x3 = cur, x4 = cur;
+      if (w0 + 1 < nw) x1 = W[w0 + 1];
+      if (w0 + 2 < nw) x2 = W[w0 + 2];
+      if (w0 + 3 < nw) x3 = W[w0 + 3];
+      if (w0 + 4 < nw) x4 = W[w0 + 4];
+      const u32x4 win[5] = {cur, x1, x2, x3, x4};
+#pragma unroll
+      for (int q = 0; q < 4; ++q) {
+        const uint32_t c[5] = {win[q].x, win[q].y, win[q].z, win[q].w, win[q + 1].x};
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int k = (int)(4 * (w0 + q)) + j - off0;
+          if (k >= 0 && k < (int)body) D[k] = alignbyte(c[j + 1], c[j], sh);
+        }
+      }
+      cur = x4;
+    }
+  }
+  for (uint32_t k = 0; k < h; ++k) dst[d + k] = src[k];
+  for (uint32_t k = h + 4 * body; k < n; ++k) dst[d + k] = src[k];
+}
+
+// One item's fields, loaded once per lane (all loads independent).
+struct ItemMeta {
+  uint64_t ko, vo, seq;
+  uint32_t klen, vl, vt, sh;
 };
 
-__device__ __forceinline__ void write_record(const EncodeParams& P, const ItemSrc& src, uint64_t i, uint32_t j,
-                                             uint32_t ri, uint8_t* dst, uint32_t dpos) {
+__device__ __forceinline__ ItemMeta load_item(const EncodeParams& P, uint64_t i) {
+  ItemMeta m;
+  m.ko = P.it.key_off[i];
+  m.klen = (uint32_t)min(P.it.key_off[i + 1] - m.ko, (uint64_t)0xFFFF);
+  m.seq = P.it.seqno[i];
+  if (is_index(P)) {
+    m.vo = P.it.handle_off[i];
+    m.vl = P.it.handle_size[i];
+    m.vt = 0;
+    m.sh = 0;
+  } else {
+    m.vo = P.it.val_off[i];
+    m.vl = (uint32_t)(P.it.val_off[i + 1] - m.vo);
+    m.vt = P.it.vtype[i];
+    m.sh = P.shared[i];
+  }
+  return m;
+}
+
+__device__ __forceinline__ uint32_t item_record_len(const EncodeParams& P, const ItemMeta& m, bool head) {
+  if (is_index(P)) return 1 + leb_len(m.vo) + leb_len(m.vl) + leb_len(m.seq) + leb_len(m.klen) + m.klen;
+  uint32_t rec = 1 + leb_len(m.seq);
+  if (head) rec += leb_len(m.klen) + m.klen;
+  else rec += leb_len(m.sh) + leb_len(m.klen - m.sh) + (m.klen - m.sh);
+  if (!is_tombstone(m.vt)) rec += leb_len(m.vl) + m.vl;
+  return rec;
+}
+
+__device__ __forceinline__ void write_record(const EncodeParams& P, const ItemMeta& m, bool head, uint8_t* dst,
+                                             uint32_t dpos) {
   ByteWriter w;
   w.init(dst, dpos);
-  const uint64_t ko = P.it.key_off[i];
-  const uint32_t klen = (uint32_t)(P.it.key_off[i + 1] - ko);
-  const uint64_t seq = P.it.seqno[i];
-  const uint64_t kp = ko - src.kshift;  // position relative to kbase
-  const uint8_t* kb = src.kbase + (kp & ~15ULL);
-  const uint32_t kq = (uint32_t)(kp & 15);
   if (is_index(P)) {  // block_handle.rs:134-156
     w.byte(0);
-    w.leb(P.it.handle_off[i]);
-    w.leb(P.it.handle_size[i]);
-    w.leb(seq);
-    w.leb(klen);
-    w.copy(kb, kq, klen);
+    w.leb(m.vo);
+    w.leb(m.vl);
+    w.leb(m.seq);
+    w.leb(m.klen);
     w.finish();
+    copy_span(P.it.keys + m.ko, dst, w.pos, m.klen);
     return;
   }
-  const uint32_t vt = P.it.vtype[i];
-  w.byte(vt);
-  w.leb(seq);
-  if (j % ri == 0) {  // encode_full_into, data_block/mod.rs:195-219
-    w.leb(klen);
-    w.copy(kb, kq, klen);
-  } else {            // encode_truncated_into, data_block/mod.rs:221-264
-    const uint32_t sh = P.shared[i];
-    w.leb(sh);
-    w.leb(klen - sh);
-    w.copy(kb, kq + sh, klen - sh);
-  }
-  if (!is_tombstone(vt)) {
-    const uint64_t vo = P.it.val_off[i];
-    const uint32_t vl = (uint32_t)(P.it.val_off[i + 1] - vo);
-    w.leb(vl);
-    const uint64_t vp = vo - src.vshift;
-    w.copy(src.vbase + (vp & ~15ULL), (uint32_t)(vp & 15), vl);
+  w.byte(m.vt);
+  w.leb(m.seq);
+  uint32_t kfrom = 0;
+  if (head) {  // encode_full_into, data_block/mod.rs:195-219
+    w.leb(m.klen);
+  } else {     // encode_truncated_into, data_block/mod.rs:221-264
+    w.leb(m.sh);
+    w.leb(m.klen - m.sh);
+    kfrom = m.sh;
   }
   w.finish();
+  copy_span(P.it.keys + m.ko + kfrom, dst, w.pos, m.klen - kfrom);
+  if (!is_tombstone(m.vt)) {
+    w.init(dst, w.pos + m.klen - kfrom);
+    w.leb(m.vl);
+    w.finish();
+    copy_span(P.it.vals + m.vo, dst, w.pos, m.vl);
+  }
 }
 
 __device__ __forceinline__ void store_le(uint8_t* dst, uint32_t pos, uint64_t v, uint32_t n) {
   for (uint32_t k = 0; k < n; ++k) dst[pos + k] = (uint8_t)(v >> (8 * k));
 }
 
-// Hash-index bucket of a key (hash_index/mod.rs:35-41).
-__device__ __forceinline__ uint32_t key_bucket(const ItemSrc& src, const EncodeParams& P, uint64_t i,
-                                               uint32_t buckets) {
-  const uint64_t ko = P.it.key_off[i];
-  const uint32_t klen = (uint32_t)(P.it.key_off[i + 1] - ko);
-  const uint64_t kp = ko - src.kshift;
-  const uint8_t* kb = src.kbase + (kp & ~15ULL);
-  const uint32_t kq = (uint32_t)(kp & 15);
+// Hash-index bucket of a key (hash_index/mod.rs:35-41), key bytes from HBM.
+__device__ __forceinline__ uint32_t key_bucket(const EncodeParams& P, uint64_t ko, uint32_t klen, uint32_t buckets) {
+  const uint64_t ka = (uint64_t)(uintptr_t)P.it.keys + ko;
+  const uint8_t* kb = reinterpret_cast<const uint8_t*>(ka & ~15ULL);
+  const uint32_t kq = (uint32_t)(ka & 15);
   const uint64_t h = xxh3_64_any(klen, BaseReader8{kb, kq}, BaseReader64{kb, kq});
   return (uint32_t)(h % buckets);
 }
@@ -360,73 +418,42 @@ __device__ __forceinline__ void write_header_bytes(uint8_t* dst, uint32_t hp, ui
 }
 
 // ------------------------------------------------------ E2: LDS write pass
-__global__ __launch_bounds__(64) void encode_write_kernel(EncodeParams P) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  const uint32_t b = blockIdx.x;
-  const int lane = threadIdx.x;
-  const BlockPlan pl = P.plans[b];
-  const uint32_t flags = pl.step_flags >> 8, step = pl.step_flags & 0xFF;
-  if (flags) return;  // large (E3) or rejected
+// Wave-local ordering of LDS traffic between lanes (no workgroup barrier:
+// the waves of a workgroup write independent blocks).
+__device__ __forceinline__ void wave_lds_sync() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront", "local");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
+}
+
+// Block b assembled by one wave in the LDS image at `smem` (16-B aligned, at
+// least e2_need bytes): records straight from the item arenas, binary index,
+// hash-index votes, trailer, fused xxh3_128 + header, then one coalesced
+// 16 B/lane copy-out to the block's place in the packed output.
+__device__ __forceinline__ void write_block_lds(const EncodeParams& P, uint32_t b, uint8_t* smem) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t s = P.starts[b], e = P.starts[b + 1];
   const uint64_t dst_off = P.block_off[b], dst_end = P.block_off[b + 1];
+  const BlockPlan pl = P.plans[b];
+  const uint32_t step = pl.step_flags & 0xFF;
   if (dst_end > P.out_cap) {
     if (lane == 0) P.status[b] = ST_OVERFLOW;
     return;
   }
-  const uint32_t s = P.starts[b], e = P.starts[b + 1], n = e - s;
+  const uint32_t n = e - s;
   const uint32_t ri = is_index(P) ? 1 : P.ri;
   const uint32_t total = (uint32_t)(dst_end - dst_off);
   const uint32_t plen = total - kHdrLen;
-
-  // ---- LDS layout: [keys span][vals span][image][hash lo][hash hi]
-  const uint64_t ka = (uint64_t)(uintptr_t)P.it.keys + P.it.key_off[s];
-  const uint64_t kb = (uint64_t)(uintptr_t)P.it.keys + P.it.key_off[e];
-  const uint64_t k0 = ka & ~15ULL;
-  const uint32_t kbytes = (uint32_t)(((kb + 15) & ~15ULL) - k0);
-  uint8_t* kimg = smem;
-  uint32_t cur = kbytes + 32;
-  uint8_t* vimg = smem + cur;
-  uint64_t v0 = 0;
-  uint32_t vbytes = 0;
-  if (!is_index(P)) {
-    const uint64_t va = (uint64_t)(uintptr_t)P.it.vals + P.it.val_off[s];
-    const uint64_t vb = (uint64_t)(uintptr_t)P.it.vals + P.it.val_off[e];
-    v0 = va & ~15ULL;
-    vbytes = (uint32_t)(((vb + 15) & ~15ULL) - v0);
-    cur += vbytes + 32;
-  }
-  uint8_t* img = smem + cur;
   const uint64_t dabs = (uint64_t)(uintptr_t)P.out + dst_off;
   const uint32_t pad = (uint32_t)(dabs & 15);
-  cur += ((pad + total + 15) & ~15u) + 32;
-  uint32_t* hlo = reinterpret_cast<uint32_t*>(smem + cur);
+  uint8_t* img = smem;
+  uint32_t* hlo = reinterpret_cast<uint32_t*>(smem + ((pad + total + 15) & ~15u) + 32);
   uint32_t* hhi = hlo + ((pl.hash_w + 3) & ~3u);
-
-  // ---- stage key / value spans HBM -> LDS
-  {
-    const u32x4* src = reinterpret_cast<const u32x4*>(k0);
-    u32x4* dst = reinterpret_cast<u32x4*>(kimg);
-    for (uint32_t c = lane; c < (kbytes >> 4); c += kWave) dst[c] = src[c];
-    if (vbytes) {
-      const u32x4* vs = reinterpret_cast<const u32x4*>(v0);
-      u32x4* vd = reinterpret_cast<u32x4*>(vimg);
-      uint32_t c = lane;
-      for (; c + 3 * kWave < (vbytes >> 4); c += 4 * kWave) {
-        u32x4 a0 = vs[c], a1 = vs[c + kWave], a2 = vs[c + 2 * kWave], a3 = vs[c + 3 * kWave];
-        vd[c] = a0; vd[c + kWave] = a1; vd[c + 2 * kWave] = a2; vd[c + 3 * kWave] = a3;
-      }
-      for (; c < (vbytes >> 4); c += kWave) vd[c] = vs[c];
-    }
-    for (uint32_t k = lane; k < pl.hash_w; k += kWave) {
-      hlo[k] = 0xFFFFFFFFu;
-      hhi[k] = 0;
-    }
+  for (uint32_t k = lane; k < pl.hash_w; k += kWave) {
+    hlo[k] = 0xFFFFFFFFu;
+    hhi[k] = 0;
   }
-  __syncthreads();
-  ItemSrc src;
-  src.kbase = kimg;
-  src.kshift = k0 - (uint64_t)(uintptr_t)P.it.keys;
-  src.vbase = vimg;
-  src.vshift = v0 - (uint64_t)(uintptr_t)P.it.vals;
+  wave_lds_sync();
   const uint32_t p0 = pad + kHdrLen;  // payload start in the image
   const uint32_t bin_off = pl.recs + 1;
 
@@ -434,20 +461,20 @@ __global__ __launch_bounds__(64) void encode_write_kernel(EncodeParams P) {
   uint32_t carry = 0;
   for (uint32_t c = 0; c < n; c += kWave) {
     const uint32_t j = c + lane;
+    const uint64_t i = (uint64_t)s + j;
+    ItemMeta m;
     uint32_t rec = 0;
-    uint64_t i = (uint64_t)s + j;
     if (j < n) {
-      bool bad = false;
-      const uint32_t klen = (uint32_t)(P.it.key_off[i + 1] - P.it.key_off[i]);
-      rec = (uint32_t)record_len(P, i, j, klen, is_index(P) ? 0 : P.shared[i], bad);
+      m = load_item(P, i);
+      rec = item_record_len(P, m, j % ri == 0);
     }
     const uint32_t incl = wave_incl_scan_u32(rec);
     const uint32_t roff = carry + incl - rec;
     if (j < n) {
-      write_record(P, src, i, j, ri, img, p0 + roff);
+      write_record(P, m, j % ri == 0, img, p0 + roff);
       if (j % ri == 0) store_le(img, p0 + bin_off + (j / ri) * step, roff, step);
       if (pl.hash_w) {
-        const uint32_t bk = key_bucket(src, P, i, pl.hash_w);
+        const uint32_t bk = key_bucket(P, m.ko, m.klen, pl.hash_w);
         const uint32_t ridx = j / ri;
         atomicMin(&hlo[bk], ridx);
         atomicMax(&hhi[bk], ridx);
@@ -455,17 +482,17 @@ __global__ __launch_bounds__(64) void encode_write_kernel(EncodeParams P) {
     }
     carry += wave_bcast_u32(incl, 63);
   }
-  __syncthreads();
+  wave_lds_sync();
   if (lane == 0) img[p0 + pl.recs] = kTrailerMarker;
   const uint32_t hash_off = pl.hash_w ? bin_off + pl.bin_len * step : 0;
   for (uint32_t k = lane; k < pl.hash_w; k += kWave) img[p0 + hash_off + k] = (uint8_t)bucket_byte(hlo[k], hhi[k]);
   write_trailer_bytes(img, p0 + plen - kTrailerLen, ri, step, pl.bin_len, bin_off, pl.hash_w, hash_off, n);
-  __syncthreads();
+  wave_lds_sync();
   // ---- fused checksum + header
   uint64_t ck_lo, ck_hi;
   xxh3_128_wave(img, p0, plen, &kLongSecret, ck_lo, ck_hi);
   write_header_bytes(img, pad, P.type, ck_lo, ck_hi, plen);
-  __syncthreads();
+  wave_lds_sync();
   // ---- image -> HBM (16 B per lane; the two edge granules byte-wise)
   const uint32_t chunks = (pad + total + 15) >> 4;
   uint8_t* gdst = reinterpret_cast<uint8_t*>(dabs & ~15ULL);
@@ -480,13 +507,32 @@ __global__ __launch_bounds__(64) void encode_write_kernel(EncodeParams P) {
   if (lane == 0) P.status[b] = ST_OK;
 }
 
+// Small blocks: kSmallWaves waves per workgroup, one block per wave.
+__global__ __launch_bounds__(kSmallWaves * kWave) void encode_write_kernel(EncodeParams P) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const uint32_t b = blockIdx.x * kSmallWaves + wave;
+  if (b >= P.n_blocks) return;
+  if ((P.plans[b].step_flags >> 8) != 0) return;  // listed (medium / big / huge) or rejected
+  write_block_lds(P, b, smem + wave * kImgSmall);
+}
+
+// Listed medium / big blocks: one wave per workgroup, grid-stride over the list.
+__global__ __launch_bounds__(kWave) void encode_write_list_kernel(EncodeParams P, uint32_t list) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  const uint32_t count = P.list_count[list];
+  const uint32_t* L = P.lists + (size_t)list * P.n_blocks;
+  for (uint32_t li = blockIdx.x; li < count; li += gridDim.x) write_block_lds(P, L[li], smem);
+}
+
 // ----------------------------------------------------- E3: HBM write pass
 __global__ __launch_bounds__(64) void encode_large_kernel(EncodeParams P) {
   __shared__ uint32_t hlo[kE3HashChunk], hhi[kE3HashChunk];
   const int lane = threadIdx.x;
-  const uint32_t count = *P.large_count;
+  const uint32_t count = P.list_count[kListHuge];
+  const uint32_t* L = P.lists + (size_t)kListHuge * P.n_blocks;
   for (uint32_t li = blockIdx.x; li < count; li += gridDim.x) {
-    const uint32_t b = P.large_list[li];
+    const uint32_t b = L[li];
     const BlockPlan pl = P.plans[b];
     const uint32_t step = pl.step_flags & 0xFF;
     const uint64_t dst_off = P.block_off[b], dst_end = P.block_off[b + 1];
@@ -503,22 +549,20 @@ __global__ __launch_bounds__(64) void encode_large_kernel(EncodeParams P) {
     const uint32_t pad = (uint32_t)(dabs & 15);
     const uint32_t p0 = pad + kHdrLen;
     const uint32_t bin_off = pl.recs + 1;
-    ItemSrc src;
-    src.kbase = P.it.keys; src.kshift = 0; src.vbase = P.it.vals; src.vshift = 0;
     uint32_t carry = 0;
     for (uint32_t c = 0; c < n; c += kWave) {
       const uint32_t j = c + lane;
-      uint32_t rec = 0;
       const uint64_t i = (uint64_t)s + j;
+      ItemMeta m;
+      uint32_t rec = 0;
       if (j < n) {
-        bool bad = false;
-        const uint32_t klen = (uint32_t)(P.it.key_off[i + 1] - P.it.key_off[i]);
-        rec = (uint32_t)record_len(P, i, j, klen, is_index(P) ? 0 : P.shared[i], bad);
+        m = load_item(P, i);
+        rec = item_record_len(P, m, j % ri == 0);
       }
       const uint32_t incl = wave_incl_scan_u32(rec);
       const uint32_t roff = carry + incl - rec;
       if (j < n) {
-        write_record(P, src, i, j, ri, img, p0 + roff);
+        write_record(P, m, j % ri == 0, img, p0 + roff);
         if (j % ri == 0) store_le(img, p0 + bin_off + (j / ri) * step, roff, step);
       }
       carry += wave_bcast_u32(incl, 63);
@@ -529,7 +573,9 @@ __global__ __launch_bounds__(64) void encode_large_kernel(EncodeParams P) {
       for (uint32_t k = lane; k < lim; k += kWave) { hlo[k] = 0xFFFFFFFFu; hhi[k] = 0; }
       __syncthreads();
       for (uint32_t j = lane; j < n; j += kWave) {
-        const uint32_t bk = key_bucket(src, P, (uint64_t)s + j, pl.hash_w);
+        const uint64_t i = (uint64_t)s + j;
+        const uint64_t ko = P.it.key_off[i];
+        const uint32_t bk = key_bucket(P, ko, (uint32_t)(P.it.key_off[i + 1] - ko), pl.hash_w);
         if (bk >= base && bk < base + lim) {
           atomicMin(&hlo[bk - base], j / ri);
           atomicMax(&hhi[bk - base], j / ri);
@@ -560,7 +606,7 @@ static size_t al256(size_t x) { return (x + 255) / 256 * 256; }
 
 size_t encode_workspace_size(uint64_t n_items, uint32_t n_blocks) {
   return al256(n_items * 2) + al256((size_t)n_blocks * 8) + al256((size_t)n_blocks * sizeof(BlockPlan)) +
-         al256((size_t)n_blocks * 4) + 256 + al256(scan_tiles(n_blocks) * 8);
+         al256((size_t)n_blocks * 4 * kLists) + 256 + al256(scan_tiles(n_blocks) * 8);
 }
 
 uint64_t encode_bound(uint64_t n_items, uint32_t n_blocks, uint64_t key_bytes, uint64_t val_bytes,
@@ -590,15 +636,23 @@ hipError_t launch_encode(const lsm_items& items, const uint32_t* starts, uint32_
   P.shared = (uint16_t*)w; w += al256(items.n_items * 2);
   P.sizes = (uint64_t*)w; w += al256((size_t)n_blocks * 8);
   P.plans = (BlockPlan*)w; w += al256((size_t)n_blocks * sizeof(BlockPlan));
-  P.large_list = (uint32_t*)w; w += al256((size_t)n_blocks * 4);
-  P.large_count = (uint32_t*)w; w += 256;
+  P.lists = (uint32_t*)w; w += al256((size_t)n_blocks * 4 * kLists);
+  P.list_count = (uint32_t*)w; w += 256;
   uint64_t* tiles = (uint64_t*)w;
-  hipError_t e = hipMemsetAsync(P.large_count, 0, 16, st);
+  hipError_t e = hipMemsetAsync(P.list_count, 0, 16, st);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(encode_sizes_kernel, dim3((n_blocks + 3) / 4), dim3(256), 0, st, P);
   e = launch_excl_scan(P.sizes, n_blocks, tiles, BlockOffOut{block_off}, st);
   if (e != hipSuccess) return e;
-  hipLaunchKernelGGL(encode_write_kernel, dim3(n_blocks), dim3(64), kE2Budget, st, P);
+  static bool attrs = [] {
+    return hipFuncSetAttribute((const void*)encode_write_list_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
+                               (int)kImgBig) == hipSuccess;
+  }();
+  (void)attrs;
+  hipLaunchKernelGGL(encode_write_kernel, dim3((n_blocks + kSmallWaves - 1) / kSmallWaves), dim3(kSmallWaves * kWave),
+                     kSmallWaves * kImgSmall, st, P);
+  hipLaunchKernelGGL(encode_write_list_kernel, dim3(2048), dim3(kWave), kImgMedium, st, P, (uint32_t)kListMedium);
+  hipLaunchKernelGGL(encode_write_list_kernel, dim3(512), dim3(kWave), kImgBig, st, P, (uint32_t)kListBig);
   hipLaunchKernelGGL(encode_large_kernel, dim3(1024), dim3(64), 0, st, P);
   return hipGetLastError();
 }

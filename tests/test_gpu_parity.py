@@ -157,6 +157,28 @@ def test_encode_decode_random_batches(gpu, ri, ratio):
     compare_decode(g, parsed, item_start, status)
 
 
+@pytest.mark.parametrize("ratio", [0.0, 1.33])
+def test_encode_size_classes(gpu, ratio):
+    """Blocks in every encode class (LDS image <= 5 KiB, <= 20 KiB, <= 96 KiB,
+    HBM-direct beyond) with unaligned key/value arena offsets and long values,
+    bit-exact against the oracle."""
+    items = random_sorted_items(1500, seed=int(ratio * 100) + 5, kmax=40, vmax=700, big_seq=True)
+    rng = random.Random(77)
+    starts = [0]
+    for want in (3, 40, 9, 150, 1, 400, 25, 60, 700, 2, 110):  # ~0.3 .. 250 KiB blocks
+        starts.append(min(items.n, starts[-1] + want))
+    while starts[-1] < items.n:
+        starts.append(min(items.n, starts[-1] + rng.randint(1, 300)))
+    starts = np.array(starts, np.uint32)
+    ref_buf, ref_off = pyoracle.encode_blocks(items, starts, restart_interval=16, hash_ratio=ratio)
+    sizes = np.diff(ref_off.astype(np.int64))
+    assert sizes.max() > 100 * 1024 and sizes.min() < 4096
+    buf, off, st = _gpu_encode(gpu, items, starts, 16, ratio, 0)
+    assert (st == 0).all()
+    assert (off == ref_off).all()
+    assert buf.tobytes() == ref_buf.tobytes()
+
+
 def test_index_blocks(gpu):
     items = index_items(2000)
     starts = np.array(list(range(0, 2000, 97)) + [2000], np.uint32)
