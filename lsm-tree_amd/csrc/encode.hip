@@ -94,7 +94,7 @@ struct EncodeParams {
   uint64_t* block_off;
   int32_t* status;
   uint16_t* shared;     // [n_items]
-  uint64_t* sizes;      // [n_blocks]
+  uint64_t* sizes;      // [n_blocks] block bytes (E1) -> exclusive scan -> block_off
   BlockPlan* plans;     // [n_blocks]
   uint32_t* lists;      // [kLists][n_blocks]: medium, big, huge blocks
   uint32_t* list_count; // [kLists]
@@ -102,95 +102,10 @@ struct EncodeParams {
 
 __device__ __forceinline__ bool is_index(const EncodeParams& P) { return P.type == 1; }
 
-// Record length of item i (j = index within its block); sh = shared prefix.
-__device__ __forceinline__ uint64_t record_len(const EncodeParams& P, uint64_t i, uint32_t j, uint32_t klen,
-                                               uint32_t sh, bool& bad) {
-  const uint64_t seq = P.it.seqno[i];
-  if (is_index(P)) {
-    return 1 + leb_len(P.it.handle_off[i]) + leb_len(P.it.handle_size[i]) + leb_len(seq) + leb_len(klen) + klen;
-  }
-  const uint32_t vt = P.it.vtype[i];
-  if (!valid_vtype(vt)) bad = true;
-  uint64_t rec = 1 + leb_len(seq);
-  if (j % P.ri == 0) rec += leb_len(klen) + klen;
-  else rec += leb_len(sh) + leb_len(klen - sh) + (klen - sh);
-  if (!is_tombstone(vt)) {
-    const uint64_t vl = P.it.val_off[i + 1] - P.it.val_off[i];
-    if (vl > 0xFFFFFFFFULL) bad = true;
-    rec += leb_len(vl) + vl;
-  }
-  return rec;
-}
-
 // LDS a block's image needs in E2: worst-case 16-B pad + the block + 32 B of
 // read slack for the window reads, then the hash-index vote arrays.
 __device__ __forceinline__ uint64_t e2_need(uint64_t total, uint32_t hash_w) {
   return ((15 + total + 15) & ~15ULL) + 32 + 8ULL * ((hash_w + 3) & ~3u);
-}
-
-// ---------------------------------------------------------------- E1: sizes
-__global__ __launch_bounds__(256) void encode_sizes_kernel(EncodeParams P) {
-  const int lane = threadIdx.x & 63;
-  const uint32_t b = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (b >= P.n_blocks) return;
-  const uint32_t s = P.starts[b], e = P.starts[b + 1];
-  const uint32_t ri = is_index(P) ? 1 : P.ri;
-  bool bad = e <= s;
-  const uint32_t n = bad ? 0 : e - s;
-  uint64_t carry = 0, last_head = 0;
-  const uint32_t lh = n ? ((n - 1) / ri) * ri : 0;
-  for (uint32_t c = 0; c < n; c += kWave) {
-    const uint32_t j = c + lane;
-    uint64_t rec = 0;
-    if (j < n) {
-      const uint64_t i = (uint64_t)s + j;
-      const uint64_t ko = P.it.key_off[i];
-      const uint64_t kl64 = P.it.key_off[i + 1] - ko;
-      if (kl64 > 0xFFFF) bad = true;
-      const uint32_t klen = (uint32_t)min(kl64, (uint64_t)0xFFFF);
-      uint32_t sh = 0;
-      if (!is_index(P) && j % ri != 0) {
-        const uint64_t h = (uint64_t)s + (j / ri) * ri;
-        const uint64_t hko = P.it.key_off[h];
-        const uint32_t hkl = (uint32_t)min(P.it.key_off[h + 1] - hko, (uint64_t)0xFFFF);
-        sh = lcp_global(P.it.keys, hko, ko, min(hkl, klen));
-      }
-      if (!is_index(P)) P.shared[i] = (uint16_t)sh;
-      rec = record_len(P, i, j, klen, sh, bad);
-    }
-    const uint64_t incl = wave_incl_scan_u64(rec);
-    if (lh >= c && lh < c + kWave) last_head = carry + wave_bcast_u64(incl - rec, lh - c);
-    carry += wave_bcast_u64(incl, 63);
-  }
-  bad = __ballot(bad) != 0;
-  if (lane != 0) return;
-  BlockPlan pl;
-  const uint32_t bin_len = n ? (n + ri - 1) / ri : 0;
-  const uint32_t step = last_head <= 0xFFFF ? 2 : 4;
-  const uint32_t buckets = is_index(P) ? 0 : bucket_count(n, P.ratio);
-  const uint32_t hash_w = (buckets > 0 && bin_len <= kHashMaxPointers) ? buckets : 0;
-  const uint64_t payload = carry + 1 + (uint64_t)bin_len * step + hash_w + kTrailerLen;
-  const uint64_t total = kHdrLen + payload;
-  if (carry > 0xFFFFFFF0ULL || total > 0xFFFFFF00ULL) bad = true;
-  uint32_t flags = 0;
-  if (bad) {
-    flags = kPlanBad;
-    P.status[b] = ST_BAD_ARG;
-  } else {
-    const uint64_t need = e2_need(total, hash_w);
-    if (need > kImgSmall) {
-      const uint32_t l = need <= kImgMedium ? kListMedium : need <= kImgBig ? kListBig : kListHuge;
-      flags = l == kListMedium ? kPlanMedium : l == kListBig ? kPlanBig : kPlanHuge;
-      const uint32_t slot = atomicAdd(&P.list_count[l], 1u);
-      P.lists[(size_t)l * P.n_blocks + slot] = b;
-    }
-  }
-  pl.recs = (uint32_t)carry;
-  pl.bin_len = bin_len;
-  pl.hash_w = hash_w;
-  pl.step_flags = step | (flags << 8);
-  P.plans[b] = pl;
-  P.sizes[b] = bad ? 0 : total;
 }
 
 // ------------------------------------------------------- record assembly
@@ -248,46 +163,71 @@ struct ByteWriter {
   }
 };
 
-// n bytes from src (HBM, any alignment) to dst[d .. d + n) (any alignment).
-// Source: aligned 16-B windows, four (+1 lookahead) per round trip, moved to
-// the destination's dword phase with v_alignbyte; destination: dword stores,
-// at most 3 byte stores at either end (the seams shared with the records
-// written by the neighbouring lanes).
-__device__ __forceinline__ void copy_span(const uint8_t* src, uint8_t* dst, uint32_t d, uint32_t n) {
-  uint32_t h = (4u - (d & 3u)) & 3u;
-  if (h > n) h = n;
-  const uint32_t body = (n - h) >> 2;
-  if (body) {
-    const uint64_t ga = (uint64_t)(uintptr_t)(src + h);
-    const uint32_t sh = (uint32_t)ga & 3u;
-    const u32x4* W = reinterpret_cast<const u32x4*>(ga & ~15ULL);
-    const int off0 = (int)((ga >> 2) & 3);
-    // destination dword k = bytes of source dwords off0 + k and off0 + k + 1
-    const uint32_t nw = (off0 + body - 1 + (sh ? 1 : 0)) / 4 + 1;
-    uint32_t* D = reinterpret_cast<uint32_t*>(dst + d + h);
-    u32x4 cur = W[0];
-    for (uint32_t w0 = 0; w0 < nw; w0 += 4) {
-      u32x4 x1 = cur, x2 = cur, x3 = cur, x4 = cur;
-      if (w0 + 1 < nw) x1 = W[w0 + 1];
-      if (w0 + 2 < nw) x2 = W[w0 + 2];
-      if (w0 + 3 < nw) x3 = W[w0 + 3];
-      if (w0 + 4 < nw) x4 = W[w0 + 4];
-      const u32x4 win[5] = {cur, x1, x2, x3, x4};
+// Span copy src (HBM, any alignment) -> dst[d .. d + n) (any alignment), in
+// two steps so that all loads of a record are issued before its stores:
+// load() reads the aligned 16-B windows that hold bytes of the span (the
+// first K in registers; longer spans stream the rest at store time) and the
+// at most 3 + 3 edge bytes; store() writes the destination dwords wholly
+// inside the span (dword q, counted from d & ~3, is source bytes
+// [base + 4q, base + 4q + 4) relative to the first window, base = (src & 15)
+// - (d & 3), assembled with v_alignbyte) and the edge bytes, which share
+// their dword with the neighbouring record.
+template <int K>
+struct SpanCopy {
+  const u32x4* W;
+  uint32_t n, d, rel, nwin, h, tl, hb, tb;
+  u32x4 w[K];
+  __device__ __forceinline__ void load(const uint8_t* src, uint32_t n_, uint32_t d_) {
+    const uint64_t a = (uint64_t)(uintptr_t)src;
+    W = reinterpret_cast<const u32x4*>(a & ~15ULL);
+    n = n_;
+    d = d_;
+    rel = (uint32_t)(a & 15);
+    nwin = n_ ? ((rel + n_ - 1) >> 4) + 1 : 0;
 #pragma unroll
-      for (int q = 0; q < 4; ++q) {
-        const uint32_t c[5] = {win[q].x, win[q].y, win[q].z, win[q].w, win[q + 1].x};
+    for (int k = 0; k < K; ++k) w[k] = (uint32_t)k < nwin ? W[k] : u32x4{0, 0, 0, 0};
+    h = min(n_, (4u - (d_ & 3u)) & 3u);
+    tl = n_ > h ? (d_ + n_) & 3u : 0u;
+    hb = tb = 0;
+    for (uint32_t k = 0; k < h; ++k) hb |= (uint32_t)src[k] << (8 * k);
+    for (uint32_t k = 0; k < tl; ++k) tb |= (uint32_t)src[n_ - tl + k] << (8 * k);
+  }
+  __device__ __forceinline__ void emit(uint8_t* dst, int wi, const u32x4& cw, uint32_t next0, int t0, uint32_t sh,
+                                       uint32_t da, int qa, int qb) const {
+    const uint32_t c[5] = {cw.x, cw.y, cw.z, cw.w, next0};
 #pragma unroll
-        for (int j = 0; j < 4; ++j) {
-          const int k = (int)(4 * (w0 + q)) + j - off0;
-          if (k >= 0 && k < (int)body) D[k] = alignbyte(c[j + 1], c[j], sh);
-        }
-      }
-      cur = x4;
+    for (int j = 0; j < 4; ++j) {
+      const int q = 4 * wi + j - t0;
+      if (q >= qa && q <= qb) *reinterpret_cast<uint32_t*>(dst + da + 4 * q) = alignbyte(c[j + 1], c[j], sh);
     }
   }
-  for (uint32_t k = 0; k < h; ++k) dst[d + k] = src[k];
-  for (uint32_t k = h + 4 * body; k < n; ++k) dst[d + k] = src[k];
-}
+  __device__ __forceinline__ void store(uint8_t* dst) const {
+    for (uint32_t k = 0; k < h; ++k) dst[d + k] = (uint8_t)(hb >> (8 * k));
+    for (uint32_t k = 0; k < tl; ++k) dst[d + n - tl + k] = (uint8_t)(tb >> (8 * k));
+    const int qa = (d & 3) ? 1 : 0;
+    const int qb = (int)((d + n) >> 2) - (int)(d >> 2) - 1;
+    if (!n || qb < qa) return;
+    const int base = (int)rel - (int)(d & 3);
+    const int t0 = base >> 2;  // -1 when the destination phase runs ahead of the source
+    const uint32_t sh = (uint32_t)base & 3u;
+    const uint32_t da = d & ~3u;
+    // (t0 = -1 only when d & 3 > rel, and then dword 0 is an edge dword)
+#pragma unroll
+    for (int k = 0; k < K; ++k) {
+      if ((uint32_t)k < nwin) {
+        uint32_t nx = 0;
+        if (k + 1 < K) nx = w[k + 1].x;
+        else if ((uint32_t)(k + 1) < nwin) nx = W[k + 1].x;
+        emit(dst, k, w[k], nx, t0, sh, da, qa, qb);
+      }
+    }
+    for (uint32_t k = K; k < nwin; ++k) {  // spans longer than K windows
+      const u32x4 cw = W[k];
+      const uint32_t nx = k + 1 < nwin ? W[k + 1].x : 0;
+      emit(dst, (int)k, cw, nx, t0, sh, da, qa, qb);
+    }
+  }
+};
 
 // One item's fields, loaded once per lane (all loads independent).
 struct ItemMeta {
@@ -295,67 +235,104 @@ struct ItemMeta {
   uint32_t klen, vl, vt, sh;
 };
 
-__device__ __forceinline__ ItemMeta load_item(const EncodeParams& P, uint64_t i) {
+__device__ __forceinline__ ItemMeta load_item(const EncodeParams& P, uint64_t i, bool& bad) {
   ItemMeta m;
   m.ko = P.it.key_off[i];
-  m.klen = (uint32_t)min(P.it.key_off[i + 1] - m.ko, (uint64_t)0xFFFF);
+  const uint64_t kl = P.it.key_off[i + 1] - m.ko;
+  if (kl > 0xFFFF) bad = true;
+  m.klen = (uint32_t)min(kl, (uint64_t)0xFFFF);
   m.seq = P.it.seqno[i];
+  m.sh = 0;
   if (is_index(P)) {
     m.vo = P.it.handle_off[i];
     m.vl = P.it.handle_size[i];
     m.vt = 0;
-    m.sh = 0;
   } else {
     m.vo = P.it.val_off[i];
-    m.vl = (uint32_t)(P.it.val_off[i + 1] - m.vo);
+    const uint64_t vl = P.it.val_off[i + 1] - m.vo;
     m.vt = P.it.vtype[i];
-    m.sh = P.shared[i];
+    if (!valid_vtype(m.vt)) bad = true;
+    if (!is_tombstone(m.vt) && vl > 0xFFFFFFFFULL) bad = true;
+    m.vl = (uint32_t)vl;
   }
   return m;
 }
 
-__device__ __forceinline__ uint32_t item_record_len(const EncodeParams& P, const ItemMeta& m, bool head) {
-  if (is_index(P)) return 1 + leb_len(m.vo) + leb_len(m.vl) + leb_len(m.seq) + leb_len(m.klen) + m.klen;
-  uint32_t rec = 1 + leb_len(m.seq);
-  if (head) rec += leb_len(m.klen) + m.klen;
-  else rec += leb_len(m.sh) + leb_len(m.klen - m.sh) + (m.klen - m.sh);
-  if (!is_tombstone(m.vt)) rec += leb_len(m.vl) + m.vl;
+// Item j of the block starting at item s, with its shared prefix against the
+// restart head (encoder.rs:140-143, util.rs:125-130).
+__device__ __forceinline__ ItemMeta load_item_lcp(const EncodeParams& P, uint32_t s, uint32_t j, uint32_t ri,
+                                                  bool& bad) {
+  const uint64_t i = (uint64_t)s + j;
+  ItemMeta m = load_item(P, i, bad);
+  if (!is_index(P) && j % ri != 0) {
+    const uint64_t h = (uint64_t)s + (j / ri) * ri;
+    const uint64_t hko = P.it.key_off[h];
+    const uint32_t hkl = (uint32_t)min(P.it.key_off[h + 1] - hko, (uint64_t)0xFFFF);
+    m.sh = lcp_global(P.it.keys, hko, m.ko, min(hkl, m.klen));
+  }
+  return m;
+}
+
+__device__ __forceinline__ uint32_t head_len(const EncodeParams& P, const ItemMeta& m, bool head) {
+  if (is_index(P)) return 1 + leb_len(m.vo) + leb_len(m.vl) + leb_len(m.seq) + leb_len(m.klen);
+  return 1 + leb_len(m.seq) + (head ? leb_len(m.klen) : leb_len(m.sh) + leb_len(m.klen - m.sh));
+}
+
+__device__ __forceinline__ uint64_t item_record_len(const EncodeParams& P, const ItemMeta& m, bool head) {
+  uint64_t rec = head_len(P, m, head) + m.klen - (head ? 0 : m.sh);
+  if (!is_index(P) && !is_tombstone(m.vt)) rec += leb_len(m.vl) + (uint64_t)m.vl;
   return rec;
 }
 
-__device__ __forceinline__ void write_record(const EncodeParams& P, const ItemMeta& m, bool head, uint8_t* dst,
-                                             uint32_t dpos) {
-  ByteWriter w;
-  w.init(dst, dpos);
-  if (is_index(P)) {  // block_handle.rs:134-156
-    w.byte(0);
-    w.leb(m.vo);
-    w.leb(m.vl);
-    w.leb(m.seq);
-    w.leb(m.klen);
-    w.finish();
-    copy_span(P.it.keys + m.ko, dst, w.pos, m.klen);
-    return;
+// Byte stores of a LEB128 (varint-rs write_*_varint) / single bytes.
+__device__ __forceinline__ uint32_t put_leb(uint8_t* dst, uint32_t pos, uint64_t v) {
+  while (v >= 0x80) {
+    dst[pos++] = (uint8_t)(v | 0x80);
+    v >>= 7;
   }
-  w.byte(m.vt);
-  w.leb(m.seq);
-  uint32_t kfrom = 0;
-  if (head) {  // encode_full_into, data_block/mod.rs:195-219
-    w.leb(m.klen);
-  } else {     // encode_truncated_into, data_block/mod.rs:221-264
-    w.leb(m.sh);
-    w.leb(m.klen - m.sh);
-    kfrom = m.sh;
-  }
-  w.finish();
-  copy_span(P.it.keys + m.ko + kfrom, dst, w.pos, m.klen - kfrom);
-  if (!is_tombstone(m.vt)) {
-    w.init(dst, w.pos + m.klen - kfrom);
-    w.leb(m.vl);
-    w.finish();
-    copy_span(P.it.vals + m.vo, dst, w.pos, m.vl);
-  }
+  dst[pos++] = (uint8_t)v;
+  return pos;
 }
+
+// One record at dpos: issue() loads the key (suffix) and value spans, store()
+// writes the record (encode_full_into / encode_truncated_into,
+// data_block/mod.rs:195-264; index: block_handle.rs:134-156).
+struct RecordCopy {
+  SpanCopy<2> key;
+  SpanCopy<5> val;
+  uint32_t dpos;
+  __device__ __forceinline__ void issue(const EncodeParams& P, const ItemMeta& m, bool head, uint32_t dpos_) {
+    dpos = dpos_;
+    const uint32_t kfrom = head ? 0 : m.sh;
+    const uint32_t kpos = dpos_ + head_len(P, m, head);
+    key.load(P.it.keys + m.ko + kfrom, m.klen - kfrom, kpos);
+    const bool has_val = !is_index(P) && !is_tombstone(m.vt);
+    const uint32_t vpos = kpos + m.klen - kfrom + leb_len(m.vl);
+    val.load(P.it.vals + (has_val ? m.vo : 0), has_val ? m.vl : 0, vpos);
+  }
+  __device__ __forceinline__ void store(const EncodeParams& P, const ItemMeta& m, bool head, uint8_t* dst) const {
+    uint32_t pos = dpos;
+    if (is_index(P)) {
+      dst[pos++] = 0;
+      pos = put_leb(dst, pos, m.vo);
+      pos = put_leb(dst, pos, m.vl);
+      pos = put_leb(dst, pos, m.seq);
+      put_leb(dst, pos, m.klen);
+    } else {
+      dst[pos++] = (uint8_t)m.vt;
+      pos = put_leb(dst, pos, m.seq);
+      if (head) {
+        put_leb(dst, pos, m.klen);
+      } else {
+        pos = put_leb(dst, pos, m.sh);
+        put_leb(dst, pos, m.klen - m.sh);
+      }
+      if (!is_tombstone(m.vt)) put_leb(dst, key.d + key.n, m.vl);
+    }
+    key.store(dst);
+    val.store(dst);
+  }
+};
 
 __device__ __forceinline__ void store_le(uint8_t* dst, uint32_t pos, uint64_t v, uint32_t n) {
   for (uint32_t k = 0; k < n; ++k) dst[pos + k] = (uint8_t)(v >> (8 * k));
@@ -426,10 +403,39 @@ __device__ __forceinline__ void wave_lds_sync() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront", "local");
 }
 
-// Block b assembled by one wave in the LDS image at `smem` (16-B aligned, at
-// least e2_need bytes): records straight from the item arenas, binary index,
-// hash-index votes, trailer, fused xxh3_128 + header, then one coalesced
-// 16 B/lane copy-out to the block's place in the packed output.
+// Block tail in the image: marker, hash-index bytes, trailer, then the fused
+// xxh3_128 + header, and one coalesced 16 B/lane copy-out to the block's
+// place in the packed output.
+__device__ __forceinline__ void finish_block_lds(const EncodeParams& P, uint32_t b, const BlockPlan& pl, uint32_t n,
+                                                 uint32_t ri, uint8_t* img, const uint32_t* hlo, const uint32_t* hhi,
+                                                 uint32_t pad, uint32_t total, uint8_t* gdst) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t step = pl.step_flags & 0xFF;
+  const uint32_t plen = total - kHdrLen, p0 = pad + kHdrLen, bin_off = pl.recs + 1;
+  if (lane == 0) img[p0 + pl.recs] = kTrailerMarker;
+  const uint32_t hash_off = pl.hash_w ? bin_off + pl.bin_len * step : 0;
+  for (uint32_t k = lane; k < pl.hash_w; k += kWave) img[p0 + hash_off + k] = (uint8_t)bucket_byte(hlo[k], hhi[k]);
+  write_trailer_bytes(img, p0 + plen - kTrailerLen, ri, step, pl.bin_len, bin_off, pl.hash_w, hash_off, n);
+  wave_lds_sync();
+  uint64_t ck_lo, ck_hi;
+  xxh3_128_wave(img, p0, plen, &kLongSecret, ck_lo, ck_hi);
+  write_header_bytes(img, pad, P.type, ck_lo, ck_hi, plen);
+  wave_lds_sync();
+  const uint32_t chunks = (pad + total + 15) >> 4;
+  for (uint32_t c = lane; c < chunks; c += kWave) {
+    const uint32_t lo = c * 16, hi = lo + 16;
+    if (lo >= pad && hi <= pad + total) {
+      reinterpret_cast<u32x4*>(gdst)[c] = reinterpret_cast<const u32x4*>(img)[c];
+    } else {
+      for (uint32_t k = max(lo, pad); k < min(hi, pad + total); ++k) gdst[k] = img[k];
+    }
+  }
+  if (lane == 0) P.status[b] = ST_OK;
+}
+
+// Listed block b (any item count) assembled by one wave in the LDS image at
+// `smem` (16-B aligned, at least e2_need bytes); shared prefixes and the plan
+// come from the fused pass.
 __device__ __forceinline__ void write_block_lds(const EncodeParams& P, uint32_t b, uint8_t* smem) {
   const int lane = threadIdx.x & 63;
   const uint32_t s = P.starts[b], e = P.starts[b + 1];
@@ -443,7 +449,6 @@ __device__ __forceinline__ void write_block_lds(const EncodeParams& P, uint32_t 
   const uint32_t n = e - s;
   const uint32_t ri = is_index(P) ? 1 : P.ri;
   const uint32_t total = (uint32_t)(dst_end - dst_off);
-  const uint32_t plen = total - kHdrLen;
   const uint64_t dabs = (uint64_t)(uintptr_t)P.out + dst_off;
   const uint32_t pad = (uint32_t)(dabs & 15);
   uint8_t* img = smem;
@@ -454,67 +459,147 @@ __device__ __forceinline__ void write_block_lds(const EncodeParams& P, uint32_t 
     hhi[k] = 0;
   }
   wave_lds_sync();
-  const uint32_t p0 = pad + kHdrLen;  // payload start in the image
+  const uint32_t p0 = pad + kHdrLen;
   const uint32_t bin_off = pl.recs + 1;
-
-  // ---- records (+ binary index entries, hash-index votes)
   uint32_t carry = 0;
   for (uint32_t c = 0; c < n; c += kWave) {
     const uint32_t j = c + lane;
     const uint64_t i = (uint64_t)s + j;
+    const bool head = j % ri == 0;
     ItemMeta m;
+    RecordCopy rc;
     uint32_t rec = 0;
     if (j < n) {
-      m = load_item(P, i);
-      rec = item_record_len(P, m, j % ri == 0);
+      bool bad = false;
+      m = load_item(P, i, bad);
+      if (!is_index(P)) m.sh = P.shared[i];
+      rec = (uint32_t)item_record_len(P, m, head);
     }
     const uint32_t incl = wave_incl_scan_u32(rec);
     const uint32_t roff = carry + incl - rec;
     if (j < n) {
-      write_record(P, m, j % ri == 0, img, p0 + roff);
-      if (j % ri == 0) store_le(img, p0 + bin_off + (j / ri) * step, roff, step);
+      rc.issue(P, m, head, p0 + roff);
+      rc.store(P, m, head, img);
+      if (head) store_le(img, p0 + bin_off + (j / ri) * step, roff, step);
       if (pl.hash_w) {
         const uint32_t bk = key_bucket(P, m.ko, m.klen, pl.hash_w);
-        const uint32_t ridx = j / ri;
-        atomicMin(&hlo[bk], ridx);
-        atomicMax(&hhi[bk], ridx);
+        atomicMin(&hlo[bk], j / ri);
+        atomicMax(&hhi[bk], j / ri);
       }
     }
     carry += wave_bcast_u32(incl, 63);
   }
   wave_lds_sync();
-  if (lane == 0) img[p0 + pl.recs] = kTrailerMarker;
-  const uint32_t hash_off = pl.hash_w ? bin_off + pl.bin_len * step : 0;
-  for (uint32_t k = lane; k < pl.hash_w; k += kWave) img[p0 + hash_off + k] = (uint8_t)bucket_byte(hlo[k], hhi[k]);
-  write_trailer_bytes(img, p0 + plen - kTrailerLen, ri, step, pl.bin_len, bin_off, pl.hash_w, hash_off, n);
-  wave_lds_sync();
-  // ---- fused checksum + header
-  uint64_t ck_lo, ck_hi;
-  xxh3_128_wave(img, p0, plen, &kLongSecret, ck_lo, ck_hi);
-  write_header_bytes(img, pad, P.type, ck_lo, ck_hi, plen);
-  wave_lds_sync();
-  // ---- image -> HBM (16 B per lane; the two edge granules byte-wise)
-  const uint32_t chunks = (pad + total + 15) >> 4;
-  uint8_t* gdst = reinterpret_cast<uint8_t*>(dabs & ~15ULL);
-  for (uint32_t c = lane; c < chunks; c += kWave) {
-    const uint32_t lo = c * 16, hi = lo + 16;
-    if (lo >= pad && hi <= pad + total) {
-      reinterpret_cast<u32x4*>(gdst)[c] = reinterpret_cast<const u32x4*>(img)[c];
-    } else {
-      for (uint32_t k = max(lo, pad); k < min(hi, pad + total); ++k) gdst[k] = img[k];
-    }
-  }
-  if (lane == 0) P.status[b] = ST_OK;
+  finish_block_lds(P, b, pl, n, ri, img, hlo, hhi, pad, total, reinterpret_cast<uint8_t*>(dabs & ~15ULL));
 }
 
-// Small blocks: kSmallWaves waves per workgroup, one block per wave.
-__global__ __launch_bounds__(kSmallWaves * kWave) void encode_write_kernel(EncodeParams P) {
+// ---------------------------------------------------------------- E1: sizes
+// One wave per block: item fields, shared prefixes (stored for E2) and record
+// sizes -> block bytes, binary-index step, hash-index size, size class.
+__global__ __launch_bounds__(256) void encode_sizes_kernel(EncodeParams P) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t b = blockIdx.x * 4 + (threadIdx.x >> 6);
+  if (b >= P.n_blocks) return;
+  const uint32_t s = P.starts[b], e = P.starts[b + 1];
+  const uint32_t ri = is_index(P) ? 1 : P.ri;
+  bool bad = e <= s;
+  const uint32_t n = bad ? 0 : e - s;
+  uint64_t carry = 0, last_head = 0;
+  const uint32_t lh = n ? ((n - 1) / ri) * ri : 0;
+  for (uint32_t c = 0; c < n; c += kWave) {
+    const uint32_t j = c + lane;
+    uint64_t rec = 0;
+    if (j < n) {
+      const ItemMeta m = load_item_lcp(P, s, j, ri, bad);
+      if (!is_index(P)) P.shared[(uint64_t)s + j] = (uint16_t)m.sh;
+      rec = item_record_len(P, m, j % ri == 0);
+    }
+    const uint64_t incl = wave_incl_scan_u64(rec);
+    if (lh >= c && lh < c + kWave) last_head = carry + wave_bcast_u64(incl - rec, lh - c);
+    carry += wave_bcast_u64(incl, 63);
+  }
+  bad = __ballot(bad) != 0;
+  if (lane != 0) return;
+  const uint32_t bin_len = n ? (n + ri - 1) / ri : 0;
+  const uint32_t step = last_head <= 0xFFFF ? 2 : 4;
+  const uint32_t buckets = is_index(P) ? 0 : bucket_count(n, P.ratio);
+  const uint32_t hash_w = (buckets > 0 && bin_len <= kHashMaxPointers) ? buckets : 0;
+  const uint64_t total = kHdrLen + carry + 1 + (uint64_t)bin_len * step + hash_w + kTrailerLen;
+  if (carry > 0xFFFFFFF0ULL || total > 0xFFFFFF00ULL) bad = true;
+  uint32_t flags = 0;
+  if (bad) {
+    flags = kPlanBad;
+    P.status[b] = ST_BAD_ARG;
+  } else {
+    const uint64_t need = e2_need(total, hash_w);
+    if (need > kImgSmall || n > kWave) {
+      const uint32_t l = need <= kImgMedium ? kListMedium : need <= kImgBig ? kListBig : kListHuge;
+      flags = l == kListMedium ? kPlanMedium : l == kListBig ? kPlanBig : kPlanHuge;
+      P.lists[(size_t)l * P.n_blocks + atomicAdd(&P.list_count[l], 1u)] = b;
+    }
+  }
+  P.plans[b] = BlockPlan{(uint32_t)carry, bin_len, hash_w, step | (flags << 8)};
+  P.sizes[b] = bad ? 0 : total;
+}
+
+// ------------------------------------------------- E2: small blocks in LDS
+// kSmallWaves waves per workgroup, one block (<= 64 items, image <= kImgSmall)
+// per wave, lane = item: all of a lane's loads (item fields, key and value
+// windows) are in flight together, then the record is stored into the image.
+#ifndef LSM_ENC_WPE
+#define LSM_ENC_WPE 5
+#endif
+__global__ __launch_bounds__(kSmallWaves * kWave) __attribute__((amdgpu_waves_per_eu(LSM_ENC_WPE))) void encode_write_kernel(EncodeParams P) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
+  const int lane = threadIdx.x & 63;
   const uint32_t b = blockIdx.x * kSmallWaves + wave;
   if (b >= P.n_blocks) return;
-  if ((P.plans[b].step_flags >> 8) != 0) return;  // listed (medium / big / huge) or rejected
-  write_block_lds(P, b, smem + wave * kImgSmall);
+  const BlockPlan pl = P.plans[b];
+  if ((pl.step_flags >> 8) != 0) return;  // listed (medium / big / huge) or rejected
+  const uint32_t s = P.starts[b], n = P.starts[b + 1] - s;
+  const uint64_t off = P.block_off[b], end = P.block_off[b + 1];
+  if (end > P.out_cap) {
+    if (lane == 0) P.status[b] = ST_OVERFLOW;
+    return;
+  }
+  const uint32_t ri = is_index(P) ? 1 : P.ri;
+  const uint32_t step = pl.step_flags & 0xFF;
+  const uint32_t total = (uint32_t)(end - off);
+  const uint64_t dabs = (uint64_t)(uintptr_t)P.out + off;
+  const uint32_t pad = (uint32_t)(dabs & 15);
+  const uint32_t p0 = pad + kHdrLen;
+  const bool head = lane % ri == 0;
+  ItemMeta m;
+  RecordCopy rc;
+  uint32_t rec = 0;
+  if ((uint32_t)lane < n) {
+    bool bad = false;
+    m = load_item(P, (uint64_t)s + lane, bad);
+    if (!is_index(P)) m.sh = P.shared[(uint64_t)s + lane];
+    rec = (uint32_t)item_record_len(P, m, head);
+  }
+  const uint32_t roff = wave_incl_scan_u32(rec) - rec;
+  if ((uint32_t)lane < n) rc.issue(P, m, head, p0 + roff);
+  uint8_t* img = smem + wave * kImgSmall;
+  uint32_t* hlo = reinterpret_cast<uint32_t*>(img + ((pad + total + 15) & ~15u) + 32);
+  uint32_t* hhi = hlo + ((pl.hash_w + 3) & ~3u);
+  for (uint32_t k = lane; k < pl.hash_w; k += kWave) {
+    hlo[k] = 0xFFFFFFFFu;
+    hhi[k] = 0;
+  }
+  wave_lds_sync();
+  if ((uint32_t)lane < n) {
+    rc.store(P, m, head, img);
+    if (head) store_le(img, p0 + pl.recs + 1 + (lane / ri) * step, roff, step);
+    if (pl.hash_w) {
+      const uint32_t bk = key_bucket(P, m.ko, m.klen, pl.hash_w);
+      atomicMin(&hlo[bk], lane / ri);
+      atomicMax(&hhi[bk], lane / ri);
+    }
+  }
+  wave_lds_sync();
+  finish_block_lds(P, b, pl, n, ri, img, hlo, hhi, pad, total, reinterpret_cast<uint8_t*>(dabs & ~15ULL));
 }
 
 // Listed medium / big blocks: one wave per workgroup, grid-stride over the list.
@@ -553,16 +638,21 @@ __global__ __launch_bounds__(64) void encode_large_kernel(EncodeParams P) {
     for (uint32_t c = 0; c < n; c += kWave) {
       const uint32_t j = c + lane;
       const uint64_t i = (uint64_t)s + j;
+      const bool head = j % ri == 0;
       ItemMeta m;
+      RecordCopy rc;
       uint32_t rec = 0;
       if (j < n) {
-        m = load_item(P, i);
-        rec = item_record_len(P, m, j % ri == 0);
+        bool bad = false;
+        m = load_item(P, i, bad);
+        if (!is_index(P)) m.sh = P.shared[i];
+        rec = (uint32_t)item_record_len(P, m, head);
       }
       const uint32_t incl = wave_incl_scan_u32(rec);
       const uint32_t roff = carry + incl - rec;
       if (j < n) {
-        write_record(P, m, j % ri == 0, img, p0 + roff);
+        rc.issue(P, m, head, p0 + roff);
+        rc.store(P, m, head, img);
         if (j % ri == 0) store_le(img, p0 + bin_off + (j / ri) * step, roff, step);
       }
       carry += wave_bcast_u32(incl, 63);
@@ -642,8 +732,7 @@ hipError_t launch_encode(const lsm_items& items, const uint32_t* starts, uint32_
   hipError_t e = hipMemsetAsync(P.list_count, 0, 16, st);
   if (e != hipSuccess) return e;
   hipLaunchKernelGGL(encode_sizes_kernel, dim3((n_blocks + 3) / 4), dim3(256), 0, st, P);
-  e = launch_excl_scan(P.sizes, n_blocks, tiles, BlockOffOut{block_off}, st);
-  if (e != hipSuccess) return e;
+  if ((e = launch_excl_scan(P.sizes, n_blocks, tiles, BlockOffOut{block_off}, st)) != hipSuccess) return e;
   static bool attrs = [] {
     return hipFuncSetAttribute((const void*)encode_write_list_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)kImgBig) == hipSuccess;

@@ -11,7 +11,8 @@ import os
 from pathlib import Path
 
 HERE = Path(__file__).resolve().parent
-LIB_PATH = HERE / "liblsmgpu.so"
+# LSMGPU_LIB: diagnostic override (tuning sweeps load variant builds of the same library)
+LIB_PATH = Path(os.environ.get("LSMGPU_LIB", HERE / "liblsmgpu.so"))
 
 LSM_HEADER_LEN = 33
 LSM_TRAILER_LEN = 31

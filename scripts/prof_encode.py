@@ -1,0 +1,46 @@
+#!/usr/bin/env python3
+"""Encode loop on the bench workload (for rocprofv3 --kernel-trace --stats)."""
+import argparse
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+for p in (ROOT, ROOT / "lsm-tree_amd", ROOT / "oracle", ROOT / "tests"):
+    sys.path.insert(0, str(p))
+
+import torch  # noqa: E402
+
+import bench  # noqa: E402
+import lsmgpu  # noqa: E402
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--blocks", type=int, default=1 << 20)
+    ap.add_argument("--reps", type=int, default=5)
+    ap.add_argument("--workload", default="counter", choices=["counter", "prefix16k"])
+    args = ap.parse_args()
+    torch.cuda.set_device(0)
+    nb = args.blocks
+    if args.workload == "counter":
+        items, starts, n_items = bench.make_workload(torch, lsmgpu, nb)
+    else:
+        items, starts, n_items = bench.make_workload(torch, lsmgpu, nb, items_per_block=56, key_len=40, val_len=256)
+    enc_ctx = lsmgpu.Encoder()
+    enc = enc_ctx.encode(items, starts, nb)
+    torch.cuda.synchronize()
+    total = int(enc["block_off"][nb].item())
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(args.reps):
+        enc_ctx.encode(items, starts, nb, out=enc)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / args.reps
+    assert int((enc["status"][:nb] != 0).sum()) == 0
+    print(f"encode {args.workload}: {nb} blocks {n_items} items {total} bytes  {ms:.3f} ms  "
+          f"{total / ms / 1e6:.1f} GB/s written", flush=True)
+
+
+if __name__ == "__main__":
+    main()
