@@ -124,6 +124,7 @@ typedef struct lsm_decode_tuning {
 } lsm_decode_tuning;
 #define LSM_DECODE_ITEM_START_VALID 1u
 #define LSM_DECODE_LEGACY 0x10000u
+#define LSM_DECODE_DOUBLE 0x40000u /* legacy kernel, two stage slots: the next group's LDS-DMA overlaps this group's parse */
 #define LSM_DECODE_RING 0x80000u
 
 int lsm_abi_version(void);

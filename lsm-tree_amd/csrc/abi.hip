@@ -101,7 +101,9 @@ int lsm_decode_blocks_tuned(const uint8_t* d_blocks, const uint64_t* d_block_off
   if (P.tile_items > 8192 || P.stage_bytes < 256 || P.stage_bytes > 65536 || P.blocks_per_wave > 63)
     return LSM_BAD_ARG;
   if (legacy) {
-    if (lsmgpu::decode_lds_bytes(P.stage_bytes, P.tile_items, P.blocks_per_wave) > 160 * 1024) return LSM_BAD_ARG;
+    if (lsmgpu::decode_lds_bytes(P.stage_bytes, P.tile_items, P.blocks_per_wave,
+                                 (P.flags & lsmgpu::kDecodeDouble) ? 2 : 1) > 160 * 1024)
+      return LSM_BAD_ARG;
   } else {
     if (P.ring_slots < 2 || P.ring_slots > 8 || P.tile_items > 4096 || P.ring_l < 1 || P.ring_l > 8 ||
         P.ring_l + P.ring_x + P.ring_h > lsmgpu::kRingWaves - 1)

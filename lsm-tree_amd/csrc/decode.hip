@@ -607,7 +607,9 @@ __global__ __launch_bounds__(kGroupWaves * kWave) __attribute__((amdgpu_waves_pe
     itr = gload(P.item_start, b_begin + lane);
   }
   // XXH3 long-path secret words in LDS (read per use by the lean row hash).
-  LongSecret* ls = reinterpret_cast<LongSecret*>(img + ((P.stage_bytes + 15) & ~15u) + kStagePad);
+  const bool dbl = (P.flags & kDecodeDouble) != 0;
+  const uint32_t slot_stride = ((P.stage_bytes + 15) & ~15u) + kStagePad;
+  LongSecret* ls = reinterpret_cast<LongSecret*>(img + (dbl ? 2 : 1) * slot_stride);
   if (tid < sizeof(LongSecret) / 8)
     reinterpret_cast<uint64_t*>(ls)[tid] = reinterpret_cast<const uint64_t*>(&kLongSecret)[tid];
   uint32_t iter = 0;
@@ -624,39 +626,67 @@ __global__ __launch_bounds__(kGroupWaves * kWave) __attribute__((amdgpu_waves_pe
     tm[slot] += t1 - t0;                                                                   \
     t0 = t1;                                                                               \
   }
-  for (uint32_t b = b_begin; b < b_end; ++iter) {
-    const Group G = form_group(P, b, b_begin, b_end, gmax, offr, itr);
-    LSM_TICK(kTmForm);
-    if (G.k == 0) {  // larger than the stage: general path
-      if (tid == 0) defer_block(P, b);
-      b += 1;
-      continue;
+  // Next stageable group at or after bb (larger blocks go to the general path).
+  auto next_group = [&](uint32_t bb) -> Group {
+    for (;;) {
+      if (bb >= b_end) {
+        Group z;
+        z.b = bb;
+        z.k = 0;
+        return z;
+      }
+      const Group g = form_group(P, bb, b_begin, b_end, gmax, offr, itr);
+      if (g.k) return g;
+      if (tid == 0) defer_block(P, bb);
+      bb += 1;
     }
-    const uint32_t k = G.k;
-    // ---- 1. stage the span HBM -> LDS (LDS-DMA), clear the record descriptors
-    {
-      const uint32_t chunks = (uint32_t)((G.span1 - G.span0) >> 4);
-      const uint8_t* src = P.blocks + G.span0 + 16 * lane;
+  };
+  // LDS-DMA of a group's span into a stage slot (wave w moves 1-KiB pieces
+  // w, w + 8, ...).  Inline asm (lds_dma.hpp): invisible to the compiler's
+  // waitcnt pass, so a prefetch stays in flight across the current group's
+  // LDS work; the loop head waits for it with vmcnt(0).
+  auto issue_dma = [&](const Group& g, uint8_t* dst) {
+    const uint32_t chunks = (uint32_t)((g.span1 - g.span0) >> 4);
+    const uint8_t* src = P.blocks + g.span0 + 16 * lane;
+    const uint32_t d0 = __builtin_amdgcn_readfirstlane((uint32_t)(uintptr_t)dst);
+    if (dbl) {
+      for (uint32_t i = wave; i * kWave < chunks; i += kGroupWaves) {
+        if (i * kWave + lane < chunks) dma16<false>(src + 1024 * i, d0 + 1024 * i);
+      }
+    } else {  // nothing to overlap: the compiler-visible builtin
       for (uint32_t i = wave; i * kWave < chunks; i += kGroupWaves) {
         if (i * kWave + lane < chunks)
-          __builtin_amdgcn_global_load_lds((gbl_void_t*)(src + 1024 * i), (lds_void_t*)(img + 1024 * i), 16, 0, 0);
+          __builtin_amdgcn_global_load_lds((gbl_void_t*)(src + 1024 * i), (lds_void_t*)(dst + 1024 * i), 16, 0, 0);
       }
-      for (uint32_t i = tid; i < G.n_items; i += kGroupWaves * kWave) rec[i] = 0;
-      __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0): this wave's DMA has landed
-      lds_barrier();
     }
+  };
+  Group G = next_group(b_begin);
+  uint32_t cur = 0;
+  if (G.k) issue_dma(G, img);
+  for (; G.k; ++iter) {
+    const uint32_t b = G.b;
+    const uint32_t k = G.k;
+    uint8_t* const stage = img + cur * slot_stride;
+    // ---- 1. this group's span has landed (issued one group ahead when
+    //         double-buffered); clear the record descriptors; prefetch the next
+    for (uint32_t i = tid; i < G.n_items; i += kGroupWaves * kWave) rec[i] = 0;
+    vm_wait<0>();
+    lds_barrier();
     LSM_TICK(kTmDma);
+    const Group Gn = next_group(b + k);
+    if (dbl && Gn.k) issue_dma(Gn, img + (cur ^ 1) * slot_stride);
+    LSM_TICK(kTmForm);
     // ---- 2. wave 0: headers, trailers, restart-interval numbering; owner[c] = block of interval c
     if (wave == 0) {
       uint32_t chains = 0;
       BlockMeta m;
       if ((uint32_t)lane < k) {
-        meta_header_fields(img, (uint32_t)(G.off_j - G.span0), G.end_j - G.off_j, m);
+        meta_header_fields(stage, (uint32_t)(G.off_j - G.span0), G.end_j - G.off_j, m);
         m.item0 = G.it0_j - G.g_item0;
         m.hdr_st = m.st;
         m.ck_bad = 0;
         m.hck_bad = 0;
-        meta_trailer(img, P.expect_type, G.it1_j - G.it0_j, m);
+        meta_trailer(stage, P.expect_type, G.it1_j - G.it0_j, m);
         if (m.st == ST_OK && m.type == 1) m.st = ST_DEFER;  // index blocks: general path
         chains = m.st == ST_OK ? m.bin_len : 0;
       }
@@ -679,7 +709,7 @@ __global__ __launch_bounds__(kGroupWaves * kWave) __attribute__((amdgpu_waves_pe
         // the serial walk is the group's critical path: let it win issue
         // arbitration against the other workgroup's waves on this SIMD
         if (P.flags & kPrioA) __builtin_amdgcn_s_setprio(3);
-        phase_a(img, meta, owner, rec, role * kWave, nA * kWave, total, P.tile_items);
+        phase_a(stage, meta, owner, rec, role * kWave, nA * kWave, total, P.tile_items);
         if (P.flags & kPrioA) __builtin_amdgcn_s_setprio(0);
         LSM_TICK(kTmA);
       } else if (!(P.flags & kDiagSkipHash)) {
@@ -689,9 +719,9 @@ __global__ __launch_bounds__(kGroupWaves * kWave) __attribute__((amdgpu_waves_pe
           const uint32_t hb = meta[jb].hb, len = meta[jb].len;
           uint64_t lo, hi;
           const uint32_t plen = len - kHdrLen;
-          if (plen > 240) xxh3_128_row_long_lean(img, hb + kHdrLen, plen, ls, lo, hi);
-          else xxh3_128_short(plen, BaseReader8{img, hb + kHdrLen}, BaseReader64{img, hb + kHdrLen}, lo, hi);
-          const bool hck = header_cksum_ok(img, hb);
+          if (plen > 240) xxh3_128_row_long_lean(stage, hb + kHdrLen, plen, ls, lo, hi);
+          else xxh3_128_short(plen, BaseReader8{stage, hb + kHdrLen}, BaseReader64{stage, hb + kHdrLen}, lo, hi);
+          const bool hck = header_cksum_ok(stage, hb);
           if ((lane & 15) == 0) {
             meta[jb].ck_bad = lo != meta[jb].ck_lo || hi != meta[jb].ck_hi;
             meta[jb].hck_bad = !hck;
@@ -703,7 +733,7 @@ __global__ __launch_bounds__(kGroupWaves * kWave) __attribute__((amdgpu_waves_pe
     lds_barrier();
     LSM_TICK(kTmSplit);
     // ---- 4. phase B: thread = record; full parse + validation; coalesced stores
-    if (!(P.flags & (kDiagSkipParse | kDiagSkipPhaseB))) phase_b<kAllFields>(P, img, meta, rec, G.n_items, G.g_item0, threadIdx.x, blockDim.x);
+    if (!(P.flags & (kDiagSkipParse | kDiagSkipPhaseB))) phase_b<kAllFields>(P, stage, meta, rec, G.n_items, G.g_item0, threadIdx.x, blockDim.x);
     LSM_TICK(kTmB);
     lds_barrier();
     if (wave == 0 && (uint32_t)lane < k) {
@@ -715,7 +745,9 @@ __global__ __launch_bounds__(kGroupWaves * kWave) __attribute__((amdgpu_waves_pe
       if (st == ST_DEFER) defer_block(P, b + lane);
       else gstore(P.status, b + lane, st);
     }
-    b += k;
+    if (!dbl && Gn.k) issue_dma(Gn, img);  // single stage: refill after phase B
+    G = Gn;
+    if (dbl) cur ^= 1;
     if constexpr (timed) tm[kTmGroups] += 1;
     LSM_TICK(kTmTail);
   }
@@ -1468,10 +1500,10 @@ size_t decode_workspace_size(uint32_t n_blocks) {
   return counts_bytes(n_blocks) + tiles_bytes(n_blocks) + defer_bytes(n_blocks);
 }
 
-uint32_t decode_lds_bytes(uint32_t stage_bytes, uint32_t tile_items, uint32_t blocks_per_wave) {
+uint32_t decode_lds_bytes(uint32_t stage_bytes, uint32_t tile_items, uint32_t blocks_per_wave, uint32_t slots) {
   const uint32_t g = blocks_per_wave < kMaxGroup ? blocks_per_wave : kMaxGroup;
   return g * (uint32_t)sizeof(BlockMeta) + ((8 * (tile_items + 1) + 15) & ~15u) + ((tile_items + 15) & ~15u) +
-         ((stage_bytes + 15) & ~15u) + kStagePad + (uint32_t)sizeof(LongSecret);
+         slots * (((stage_bytes + 15) & ~15u) + kStagePad) + (uint32_t)sizeof(LongSecret);
 }
 
 static hipError_t launch_ring(const DecodeParams& P, hipStream_t st);
@@ -1507,7 +1539,7 @@ hipError_t launch_decode(const DecodeParams& P0, void* ws, hipStream_t st) {
 }
 
 static hipError_t launch_legacy(const DecodeParams& P, hipStream_t st) {
-  const uint32_t lds = decode_lds_bytes(P.stage_bytes, P.tile_items, P.blocks_per_wave);
+  const uint32_t lds = decode_lds_bytes(P.stage_bytes, P.tile_items, P.blocks_per_wave, (P.flags & kDecodeDouble) ? 2 : 1);
   const bool timed = (P.flags & kDiagTimers) != 0, all = all_fields(P.out);
   const void* fn = timed ? (all ? (const void*)decode_blocks_kernel<true, true> : (const void*)decode_blocks_kernel<true, false>)
                          : (all ? (const void*)decode_blocks_kernel<false, true> : (const void*)decode_blocks_kernel<false, false>);

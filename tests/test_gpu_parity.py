@@ -89,6 +89,7 @@ def test_decode_golden_blocks(gpu, golden_blocks):
 
 LEG = 0x10000  # LSM_DECODE_LEGACY
 RING = 0x80000  # LSM_DECODE_RING
+DBL = 0x40000  # LSM_DECODE_DOUBLE
 # (blocks_per_wave, slot/stage bytes, tile items, flags, ring slots, planners, hashers, loaders)
 TUNINGS = [None,                                 # library default kernel
            (0, 0, 0, RING),                      # ring defaults
@@ -99,7 +100,8 @@ TUNINGS = [None,                                 # library default kernel
            (0, 32768, 512, RING, 3, 3, 3, 1),    # a single loader wave
            (0, 32768, 512, RING | 0x20000, 3),   # nt DMA, 3 slots
            (0, 16384, 256, RING, 2, 1, 1),       # 2-slot ring
-           (48, 65536, 1024, LEG), (1, 256, 64, LEG), (63, 65536, 2048, LEG)]
+           (48, 65536, 1024, LEG), (1, 256, 64, LEG), (63, 65536, 2048, LEG),
+           (48, 32768, 512, LEG | DBL), (48, 65536, 1024, LEG | DBL), (1, 256, 64, LEG | DBL), (5, 4096, 64, LEG | DBL)]
 
 
 @pytest.mark.parametrize("tuning", TUNINGS)
