@@ -22,6 +22,7 @@
  *                         IndexBlock::iter         src/table/index_block/mod.rs:91-95
  *   lsm_cut_blocks     <- Writer::write chunking   src/table/writer/mod.rs:243-296
  *   lsm_xxh3_128_batch <- hash128                  src/hash.rs:7-9 (checksum of arbitrary byte ranges)
+ *   lsm_point_read_blocks <- DataBlock::point_read src/table/data_block/mod.rs:412-472
  */
 #ifndef LSMGPU_H
 #define LSMGPU_H
@@ -127,6 +128,19 @@ typedef struct lsm_decode_tuning {
 #define LSM_DECODE_DOUBLE 0x40000u /* legacy kernel, two stage slots: the next group's LDS-DMA overlaps this group's parse */
 #define LSM_DECODE_RING 0x80000u
 
+/* Point-read results (DataBlock::point_read -> Option<InternalValue>,
+ * data_block/mod.rs:412-472), one row per query; NULL fields other than item
+ * are not written.  item = index of the hit in its block's item order (the
+ * row lsm_decode_blocks gives it), -1 = None.  For a hit the key equals the
+ * needle; the value is payload[val_off .. val_off + val_len). */
+typedef struct lsm_point_result {
+    int32_t* item;
+    uint64_t* seqno;
+    uint32_t* val_off;
+    uint32_t* val_len;
+    uint8_t* vtype;
+} lsm_point_result;
+
 int lsm_abi_version(void);
 const char* lsm_status_name(int status);
 /* Last HIP error string of this thread (after LSM_HIP_ERROR). */
@@ -181,6 +195,21 @@ uint64_t lsm_cut_blocks(const uint64_t* key_off, const uint64_t* val_off, uint64
  * d_data[d_off[i] .. d_off[i+1]) into d_out (2 u64 per range: low, high). */
 int lsm_xxh3_128_batch(const uint8_t* d_data, const uint64_t* d_off, uint32_t n, uint64_t* d_out,
                        void* stream);
+
+/* ---- point read -----------------------------------------------------------
+ * Batched DataBlock::point_read(needle, snapshot_seqno) (data_block/mod.rs:412-472),
+ * the per-block step of Table::point_read (src/table/mod.rs:325-327): query q
+ * looks up needle q (d_needles[d_needle_off[q] .. d_needle_off[q+1]), arena
+ * readable LSM_INPUT_PADDING bytes past its end) in block d_query_block[q] of
+ * the batch (same layout as lsm_decode_blocks; blocks of type Data or Meta, as
+ * loaded and checksum-verified by Block::from_file).  Hash-index probe, else
+ * restart binary search, then the MVCC linear scan (newest version with
+ * seqno < snapshot).  d_status[q]: LSM_OK (hit or miss), or the structural
+ * error of the block (LSM_PARSE, LSM_TRUNCATED, LSM_TYPE_MISMATCH, ...). */
+int lsm_point_read_blocks(const uint8_t* d_blocks, const uint64_t* d_block_off, uint32_t n_blocks,
+                          const uint32_t* d_query_block, const uint8_t* d_needles,
+                          const uint64_t* d_needle_off, const uint64_t* d_snapshot, uint32_t n_queries,
+                          const lsm_point_result* d_out, int32_t* d_status, void* stream);
 
 #ifdef __cplusplus
 }

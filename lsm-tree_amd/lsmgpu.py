@@ -40,6 +40,11 @@ class LsmBlockParams(C.Structure):
                 ("reserved", C.c_uint8), ("hash_ratio", C.c_float)]
 
 
+class LsmPointResult(C.Structure):
+    _fields_ = [("item", C.c_void_p), ("seqno", C.c_void_p), ("val_off", C.c_void_p), ("val_len", C.c_void_p),
+                ("vtype", C.c_void_p)]
+
+
 class LsmDecodeTuning(C.Structure):
     _fields_ = [("blocks_per_wave", C.c_uint32), ("stage_bytes", C.c_uint32), ("tile_items", C.c_uint32),
                 ("flags", C.c_uint32), ("ring_slots", C.c_uint32), ("ring_walkers", C.c_uint32),
@@ -97,13 +102,18 @@ def lib():
         L.lsm_cut_blocks.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p, C.c_uint64]
         L.lsm_xxh3_128_batch.restype = C.c_int
         L.lsm_xxh3_128_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p]
+        L.lsm_point_read_blocks.restype = C.c_int
+        L.lsm_point_read_blocks.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p,
+                                            C.c_void_p, C.c_uint32, C.POINTER(LsmPointResult), C.c_void_p,
+                                            C.c_void_p]
         _lib = L
     return _lib
 
 
 EXPORTED_SYMBOLS = ["lsm_abi_version", "lsm_status_name", "lsm_last_error", "lsm_device_count", "lsm_set_device",
                     "lsm_decode_workspace_size", "lsm_decode_blocks", "lsm_decode_blocks_tuned", "lsm_encode_bound",
-                    "lsm_encode_workspace_size", "lsm_encode_blocks", "lsm_cut_blocks", "lsm_xxh3_128_batch"]
+                    "lsm_encode_workspace_size", "lsm_encode_blocks", "lsm_cut_blocks", "lsm_xxh3_128_batch",
+                    "lsm_point_read_blocks"]
 
 
 def _check(rc, what):
@@ -249,6 +259,27 @@ def xxh3_128_batch(data, off, n):
     torch = _torch()
     out = torch.empty(2 * max(n, 1), dtype=torch.int64, device=data.device)
     _check(lib().lsm_xxh3_128_batch(_ptr(data), _ptr(off), n, _ptr(out), _stream(None)), "lsm_xxh3_128_batch")
+    return out
+
+
+def point_read(blocks, block_off, n_blocks, query_block, needles, needle_off, snapshot, stream=None):
+    """Batched DataBlock::point_read (data_block/mod.rs:412-472).  All inputs cuda
+    tensors: blocks uint8 (padded), block_off int64 [n_blocks+1], query_block
+    int32 [n], needles uint8 (padded arena), needle_off int64 [n+1], snapshot
+    int64 [n].  Returns dict item/seqno/val_off/val_len/vtype/status (item -1 = None)."""
+    torch = _torch()
+    n = int(query_block.numel())
+    dev = blocks.device
+    out = {"item": torch.empty(max(n, 1), dtype=torch.int32, device=dev),
+           "seqno": torch.zeros(max(n, 1), dtype=torch.int64, device=dev),
+           "val_off": torch.zeros(max(n, 1), dtype=torch.int32, device=dev),
+           "val_len": torch.zeros(max(n, 1), dtype=torch.int32, device=dev),
+           "vtype": torch.zeros(max(n, 1), dtype=torch.uint8, device=dev),
+           "status": torch.empty(max(n, 1), dtype=torch.int32, device=dev)}
+    res = LsmPointResult(*(_ptr(out[f]) for f in ("item", "seqno", "val_off", "val_len", "vtype")))
+    _check(lib().lsm_point_read_blocks(_ptr(blocks), _ptr(block_off), n_blocks, _ptr(query_block), _ptr(needles),
+                                       _ptr(needle_off), _ptr(snapshot), n, C.byref(res), _ptr(out["status"]),
+                                       _stream(stream)), "lsm_point_read_blocks")
     return out
 
 
