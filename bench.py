@@ -39,7 +39,12 @@ def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
-def make_workload(torch, lsmgpu, n_blocks, items_per_block=52, key_len=16, val_len=64, seed=0x5EED0002):
+def make_workload(torch, lsmgpu, n_blocks, items_per_block=52, key_len=16, val_len=64, seed=0x5EED0002,
+                  kind="counter"):
+    """Synthetic items on the GPU, cut every items_per_block items (= the writer
+    rule for these fixed sizes, check_cut_rule).  kind: "counter" = big-endian
+    counter keys (G1); "prefix" = fixed random (key_len - 8)-byte prefix || 8-byte
+    BE counter (config 4); "random" = random 16-byte keys, sorted (G2)."""
     dev = "cuda"
     n = n_blocks * items_per_block
     g = torch.Generator(device=dev)
@@ -47,7 +52,16 @@ def make_workload(torch, lsmgpu, n_blocks, items_per_block=52, key_len=16, val_l
     ctr = torch.arange(n, dtype=torch.int64, device=dev)
     keys = torch.zeros(n * key_len + lsmgpu.LSM_INPUT_PADDING, dtype=torch.uint8, device=dev)
     kv = keys[:n * key_len].view(n, key_len)
-    kv[:, key_len - 8:] = ctr.view(torch.uint8).view(n, 8).flip(1)
+    if kind == "random":
+        assert key_len == 16
+        hi = torch.randint(0, 1 << 62, (n,), dtype=torch.int64, device=dev, generator=g).sort().values
+        lo = torch.randint(0, 1 << 62, (n,), dtype=torch.int64, device=dev, generator=g)
+        kv[:, :8] = hi.view(torch.uint8).view(n, 8).flip(1)
+        kv[:, 8:] = lo.view(torch.uint8).view(n, 8).flip(1)
+    else:
+        if kind == "prefix":
+            kv[:, :key_len - 8] = torch.randint(0, 256, (key_len - 8,), dtype=torch.uint8, device=dev, generator=g)
+        kv[:, key_len - 8:] = ctr.view(torch.uint8).view(n, 8).flip(1)
     vals = torch.randint(0, 256, (n * val_len + lsmgpu.LSM_INPUT_PADDING,), dtype=torch.uint8, device=dev,
                          generator=g)
     items = {
@@ -62,13 +76,13 @@ def make_workload(torch, lsmgpu, n_blocks, items_per_block=52, key_len=16, val_l
     return items, starts, n
 
 
-def check_cut_rule(lsmgpu, items_per_block, key_len, val_len):
-    """The fixed 52-item cut equals the reference writer rule (writer/mod.rs:284-290)."""
+def check_cut_rule(lsmgpu, items_per_block, key_len, val_len, block_size=4096):
+    """The fixed-count cut equals the reference writer rule (writer/mod.rs:284-290)."""
     import numpy as np
     m = items_per_block * 4
     ko = np.arange(m + 1, dtype=np.uint64) * key_len
     vo = np.arange(m + 1, dtype=np.uint64) * val_len
-    starts = lsmgpu.cut_blocks(ko, vo, 4096)
+    starts = lsmgpu.cut_blocks(ko, vo, block_size)
     assert list(starts) == list(range(0, m + 1, items_per_block)), starts
 
 
@@ -194,16 +208,200 @@ def host_inclusive(torch, lsmgpu, enc, item_start, nb, chunk_blocks=131072, reps
             "note": "pinned host blocks -> H2D -> decode -> D2H parsed SoA (25 B/item), 3 streams, double-buffered"}
 
 
-def load_traffic():
-    """HBM bytes per decode launch from the committed rocprofv3 PMC summary
-    (profiles/traffic_*.json), FETCH_SIZE doubled per the gfx950 guide."""
-    best = None
+def check_blocks_vs_oracle(torch, items, starts, enc, picks, restart_interval=16):
+    """Encoded bytes of the picked blocks == oracle encode of the same items."""
+    import numpy as np
+    import pyoracle
+    off = enc["block_off"]
+    for b in picks:
+        s0, s1 = int(starts[b].item()), int(starts[b + 1].item())
+        ko = items["key_off"][s0:s1 + 1].cpu().numpy().astype(np.uint64)
+        vo = items["val_off"][s0:s1 + 1].cpu().numpy().astype(np.uint64)
+        it = pyoracle.Items(items["keys"][int(ko[0]):int(ko[-1])].cpu().numpy(), ko - ko[0],
+                            items["vals"][int(vo[0]):int(vo[-1])].cpu().numpy(), vo - vo[0],
+                            items["seqno"][s0:s1].cpu().numpy().view(np.uint64), items["vtype"][s0:s1].cpu().numpy())
+        ref = pyoracle.block_write(pyoracle.data_block_encode(it, 0, s1 - s0, restart_interval=restart_interval))
+        got = enc["buf"][int(off[b].item()):int(off[b + 1].item())].cpu().numpy().tobytes()
+        assert got == ref, f"block {b} bytes differ from oracle"
+    return len(picks)
+
+
+def time_decode(torch, lsmgpu, blocks, boff, nb, n_items, steps):
+    """Device-resident lsm_decode_blocks over a batch (count + scan + verify +
+    parse), HIP events on the launch stream; checks every status and the count."""
+    dec = lsmgpu.Decoder(blocks.device)
+    out = dec.alloc_outputs(n_items, nb, fields=DATA_FIELDS + ["handle_off"])
+    dec.decode(blocks, boff, nb, out, n_items)
+    torch.cuda.synchronize()
+    assert int((out["status"][:nb] != 0).sum().item()) == 0, "decode status"
+    assert int(out["item_start"][nb].item()) == n_items, "item count"
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(steps):
+        dec.decode(blocks, boff, nb, out, n_items)
+    e1.record()
+    torch.cuda.synchronize()
+    return e0.elapsed_time(e1) / steps, out
+
+
+def bench_config4(torch, lsmgpu, steps, rank):
+    """configs[3]: prefix-heavy keys (32 B shared prefix + 8 B suffix), 256 B
+    values, 16 KiB blocks (56 items, 14953 B on disk), 262144 blocks."""
+    nb = 262144
+    check_cut_rule(lsmgpu, 56, 40, 256, 16384)
+    items, starts, n = make_workload(torch, lsmgpu, nb, items_per_block=56, key_len=40, val_len=256,
+                                     seed=0x5EED0004 + rank, kind="prefix")
+    enc_ctx = lsmgpu.Encoder()
+    enc = enc_ctx.encode(items, starts, nb)
+    torch.cuda.synchronize()
+    assert int((enc["status"][:nb] != 0).sum().item()) == 0
+    total = int(enc["block_off"][nb].item())
+    assert int(enc["block_off"][1].item()) == 14953  # SURVEY 8 table (first block; later ones vary by a byte)
+    checked = check_blocks_vs_oracle(torch, items, starts, enc, [0, 1, nb // 2, nb - 1])
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(3):
+        enc_ctx.encode(items, starts, nb, out=enc)
+    e1.record()
+    torch.cuda.synchronize()
+    enc_ms = e0.elapsed_time(e1) / 3
+    dec_ms, out = time_decode(torch, lsmgpu, enc["buf"], enc["block_off"], nb, n, steps)
+    assert bool((out["prefix_len"][:n].view(torch.int16)[1::56] >= 32).all().item())  # shared 32 B prefix
+    res = {"workload": "BASELINE configs[3]: 16 KiB blocks, 32 B shared prefix + 8 B suffix keys, 256 B values",
+           "blocks": nb, "bytes": total, "decode_ms": round(dec_ms, 4),
+           "decode_GiB_per_s": round(total / (dec_ms * 1e-3) / 2 ** 30, 3),
+           "encode_ms": round(enc_ms, 4), "encode_GiB_per_s": round(total / (enc_ms * 1e-3) / 2 ** 30, 3),
+           "oracle_checked_blocks": checked}
+    del items, enc, out
+    torch.cuda.empty_cache()
+    return res
+
+
+# configs[4] mix: equal bytes of 4/16/64 KiB data blocks with counter (G1)
+# and random sorted (G2) 16 B keys / 64 B values, plus one full index block
+# (RI 1) per 64 MiB "table" (flush target, src/tree/mod.rs:374-377).
+C5_SEGMENTS = [(4096, 52, "counter", 3769), (4096, 52, "random", 4466), (16384, 205, "counter", 14636),
+               (16384, 205, "random", 17300), (65536, 820, "counter", 58309), (65536, 820, "random", 69219)]
+C5_TABLE = 64 << 20
+
+
+def build_config5_shard(torch, lsmgpu, shard_bytes, rank):
+    """This rank's byte share of the configs[4] batch, GPU-encoded: data blocks
+    of the six segments, each followed by its index blocks (one per table)."""
+    segs, n_items, n_data_blocks, n_index_blocks = [], 0, 0, 0
+    picks_checked = 0
+    for si, (bs, ipb, kind, est) in enumerate(C5_SEGMENTS):
+        nb = max(1, int(shard_bytes / len(C5_SEGMENTS) / est))
+        check_cut_rule(lsmgpu, ipb, 16, 64, bs)
+        items, starts, n = make_workload(torch, lsmgpu, nb, items_per_block=ipb, seed=0x5EED0005 + 97 * rank + si,
+                                         kind=kind)
+        enc = lsmgpu.Encoder().encode(items, starts, nb)
+        torch.cuda.synchronize()
+        assert int((enc["status"][:nb] != 0).sum().item()) == 0
+        picks_checked += check_blocks_vs_oracle(torch, items, starts, enc, [0, nb - 1])
+        boff = enc["block_off"][:nb + 1]
+        dev = boff.device
+        # index entries: end key, seqno of each block's last item, handle (offset in its table, size)
+        last = starts[1:].to(torch.int64) - 1
+        end_keys = items["keys"][:n * 16].view(n, 16)[last].reshape(-1)
+        table = torch.div(boff[:-1], C5_TABLE, rounding_mode="floor")
+        tfirst = torch.ones(nb, dtype=torch.bool, device=dev)
+        tfirst[1:] = table[1:] != table[:-1]
+        first = torch.nonzero(tfirst).flatten()
+        tid = torch.cumsum(tfirst.to(torch.int64), 0) - 1
+        ix = {"keys": torch.cat([end_keys, torch.zeros(lsmgpu.LSM_INPUT_PADDING, dtype=torch.uint8, device=dev)]),
+              "key_off": torch.arange(nb + 1, dtype=torch.int64, device=dev) * 16,
+              "seqno": items["seqno"][last].contiguous(),
+              "handle_off": (boff[:-1] - boff[first][tid]).contiguous(),
+              "handle_size": (boff[1:] - boff[:-1]).to(torch.int32).contiguous()}
+        istarts = torch.cat([first, torch.tensor([nb], device=dev)]).to(torch.int32)
+        nt = int(first.numel())
+        ienc = lsmgpu.Encoder().encode(ix, istarts, nt, restart_interval=1, block_type=lsmgpu.BLOCK_INDEX)
+        torch.cuda.synchronize()
+        assert int((ienc["status"][:nt] != 0).sum().item()) == 0
+        dbytes, ibytes = int(boff[nb].item()), int(ienc["block_off"][nt].item())
+        segs.append((enc["buf"][:dbytes], boff[:-1].clone(), ienc["buf"][:ibytes], ienc["block_off"][:nt] + dbytes,
+                     dbytes + ibytes))
+        n_items += n + nb
+        n_data_blocks += nb
+        n_index_blocks += nt
+        del items, enc, ienc, ix
+    base, pieces, offl = 0, [], []
+    for dbuf, doff, ibuf, ioff, seg_bytes in segs:
+        pieces += [dbuf, ibuf]
+        offl += [doff + base, ioff + base]
+        base += seg_bytes
+    pieces.append(torch.zeros(lsmgpu.LSM_INPUT_PADDING, dtype=torch.uint8, device=pieces[0].device))
+    blocks = torch.cat(pieces)
+    block_off = torch.cat(offl + [torch.tensor([base], dtype=torch.int64, device=blocks.device)])
+    del segs, pieces
+    torch.cuda.empty_cache()
+    return blocks, block_off, n_data_blocks + n_index_blocks, n_items, base, n_index_blocks, picks_checked
+
+
+def bench_config5(torch, lsmgpu, steps, rank, world, dist, dev, total_bytes=8 << 30):
+    """configs[4]: 8 GiB of mixed data + index blocks, byte-split across the
+    ranks (strong scaling: the batch is fixed, each rank decodes its share)."""
+    blocks, boff, nb, n_items, nbytes, n_idx, checked = build_config5_shard(torch, lsmgpu, total_bytes / world, rank)
+    ms, out = time_decode(torch, lsmgpu, blocks, boff, nb, n_items, steps)
+    t = torch.tensor([ms, float(nbytes)], dtype=torch.float64, device=dev)
+    if dist is not None:
+        mx = t.clone()
+        dist.all_reduce(mx, op=dist.ReduceOp.MAX)
+        sm = t.clone()
+        dist.all_reduce(sm, op=dist.ReduceOp.SUM)
+        ms_all, bytes_all = float(mx[0].item()), float(sm[1].item())
+    else:
+        ms_all, bytes_all = ms, float(nbytes)
+    del blocks, boff, out
+    torch.cuda.empty_cache()
+    return {"workload": "BASELINE configs[4]: 8 GiB mixed 4/16/64 KiB data (G1+G2 keys) + index blocks, "
+                        "byte-split across ranks (strong scaling)",
+            "total_bytes": int(bytes_all), "blocks_per_rank": nb, "index_blocks_per_rank": n_idx,
+            "decode_ms_max_rank": round(ms_all, 4), "GiB_per_s": round(bytes_all / (ms_all * 1e-3) / 2 ** 30, 3),
+            "oracle_checked_blocks": checked}
+
+
+def bench_point_read(torch, lsmgpu, items, starts, enc, nb, n_items, n_queries=1 << 20, reps=5):
+    """Batched DataBlock::point_read: random existing keys of the config 2 batch,
+    snapshot = max; every query must hit its own item."""
+    g = torch.Generator(device="cuda")
+    g.manual_seed(0x5EED0006)
+    qi = torch.randint(0, n_items, (n_queries,), dtype=torch.int64, device="cuda", generator=g)
+    qb = torch.div(qi, 52, rounding_mode="floor").to(torch.int32)
+    needles = torch.cat([items["keys"][:n_items * 16].view(n_items, 16)[qi].reshape(-1),
+                         torch.zeros(lsmgpu.LSM_INPUT_PADDING, dtype=torch.uint8, device="cuda")])
+    noff = torch.arange(n_queries + 1, dtype=torch.int64, device="cuda") * 16
+    snap = torch.full((n_queries,), (1 << 63) - 1, dtype=torch.int64, device="cuda")
+    out = lsmgpu.point_read(enc["buf"], enc["block_off"], nb, qb, needles, noff, snap)
+    torch.cuda.synchronize()
+    assert int((out["status"] != 0).sum().item()) == 0
+    assert bool((out["item"].to(torch.int64) == qi - qb.to(torch.int64) * 52).all().item()), "point_read hits"
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        lsmgpu.point_read(enc["buf"], enc["block_off"], nb, qb, needles, noff, snap)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    return {"queries": n_queries, "ms": round(ms, 4), "Mqueries_per_s": round(n_queries / ms / 1e3, 1),
+            "note": "lane per query straight from HBM (hash index off: restart binary search + MVCC scan)"}
+
+
+def load_traffic(n_blocks):
+    """HBM bytes of one decode_blocks_kernel launch over n_blocks, from the
+    newest committed rocprofv3 PMC summary (profiles/traffic_*.json: FETCH_SIZE
+    x2 per the gfx950 guide + WRITE_SIZE), scaled per block when the profiled
+    launch had a different block count."""
+    best, src = None, None
     for p in sorted((ROOT / "profiles").glob("traffic_*.json")):
         try:
-            best = json.loads(p.read_text())
+            best, src = json.loads(p.read_text()), p.name
         except Exception:
             pass
-    return best
+    if not best:
+        return None, None
+    return int(round(best["bytes_per_launch"] * n_blocks / best["blocks"])), f"{src} ({best['blocks']} blocks)"
 
 
 def main():
@@ -217,6 +415,7 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=10.0)
     ap.add_argument("--tuning", type=str, default="", help="bpw,stage_bytes,tile_items")
     ap.add_argument("--skip-verify", action="store_true")
+    ap.add_argument("--no-extra", action="store_true", help="skip the configs[3]/[4] and point-read legs")
     args = ap.parse_args()
 
     import torch
@@ -302,7 +501,7 @@ def main():
     kernel_ms = k0.elapsed_time(k1) / args.steps
     alg_bytes = total_bytes + n_items * PARSED_BYTES_PER_ITEM + nb * PER_BLOCK_OUT
     achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
-    traffic = load_traffic()
+    traffic, traffic_src = load_traffic(nb)
 
     # encode (config 3 round trip) throughput on the same batch
     torch.cuda.synchronize()
@@ -314,6 +513,14 @@ def main():
     c1.record()
     torch.cuda.synchronize()
     enc_ms = c0.elapsed_time(c1) / esteps
+
+    dec_ms = kernel_ms  # the decode kernel alone (item_start precomputed), for the round trip
+    extra = {}
+    if not args.no_extra:
+        extra["point_read"] = bench_point_read(torch, lsmgpu, items, starts, enc, nb, n_items)
+        if world == 1:
+            extra["config4"] = bench_config4(torch, lsmgpu, max(3, args.steps // 4), rank)
+        extra["config5"] = bench_config5(torch, lsmgpu, max(3, args.steps // 4), rank, world, dist, dev)
 
     hostinc = None
     if rank == 0 and world == 1 and not args.no_host:
@@ -345,13 +552,18 @@ def main():
                        "tuning": list(tuning) if tuning else "default"},
             "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
                          "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                         "traffic": traffic.get("bytes_per_launch") if traffic else None,
+                         "traffic": traffic, "traffic_source": traffic_src,
                          "kernel": "decode_blocks_kernel", "kernel_ms": round(kernel_ms, 4),
                          "alg_bytes_per_launch": alg_bytes,
                          "read_only_frac": round(total_bytes / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)},
             "cpu_baseline": cpu,
             "encode": {"GiB_per_s_written": round(total_bytes / (enc_ms * 1e-3) / 2 ** 30, 3),
                        "ms": round(enc_ms, 4)},
+            "config3_roundtrip": {"workload": "BASELINE configs[2]: encode + checksum + decode of the same batch, "
+                                              "bit-exact block bytes vs the oracle (sampled)",
+                                  "encode_ms": round(enc_ms, 4), "decode_ms": round(dec_ms, 4),
+                                  "GiB_per_s": round(total_bytes / ((enc_ms + dec_ms) * 1e-3) / 2 ** 30, 3)},
+            **extra,
             "host_inclusive_decode": hostinc,
             "gpu_event_ms_per_step": round(gpu_ms / args.steps, 4),
         }
