@@ -567,6 +567,78 @@ __global__ __launch_bounds__(kWave) void decode_deferred_kernel(DecodeParams P) 
   for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) decode_block_direct(P, gload(P.defer_list, i), meta);
 }
 
+// Deferred blocks up to kBigStage bytes (the 16..64 KiB data blocks larger
+// than a group stage, and blocks with rare record shapes): one 4-wave
+// workgroup per block, the block staged in LDS by LDS-DMA, then wave 0
+// verifies the payload checksum while waves 1..3 walk the restart intervals
+// (lane = interval) from LDS and store every record; statuses merge in
+// oracle order (header, checksum, trailer / parse).  Larger blocks (full
+// index blocks) take the HBM path on wave 0.
+constexpr uint32_t kBigWaves = 4;
+constexpr uint32_t kBigStage = 80 * 1024;
+
+__global__ __launch_bounds__(kBigWaves * kWave) void decode_deferred_staged_kernel(DecodeParams P) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  BlockMeta* meta = reinterpret_cast<BlockMeta*>(smem);  // [0] header view, [1] trailer view
+  uint32_t* cks_bad = reinterpret_cast<uint32_t*>(smem + 2 * sizeof(BlockMeta));
+  uint8_t* stage = smem + 256;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid / kWave);
+  const int lane = tid & (kWave - 1);
+  const uint32_t n = gload(P.defer_count, 0);
+  for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
+    const uint32_t b = gload(P.defer_list, i);
+    const uint64_t off = gload(P.block_off, b), end = gload(P.block_off, b + 1);
+    const uint64_t span0 = off & ~15ULL, span1 = (max(end, off) + 15) & ~15ULL;
+    if (span1 - span0 > kBigStage) {  // HBM path
+      if (wave == 0) decode_block_direct(P, b, meta);
+      lds_barrier();
+      continue;
+    }
+    const uint32_t chunks = (uint32_t)((span1 - span0) >> 4);
+    const uint8_t* src = P.blocks + span0 + 16 * lane;
+    for (uint32_t c = wave; c * kWave < chunks; c += kBigWaves) {
+      if (c * kWave + lane < chunks)
+        __builtin_amdgcn_global_load_lds((gbl_void_t*)(src + 1024 * c), (lds_void_t*)(stage + 1024 * c), 16, 0, 0);
+    }
+    const uint64_t item_base = gload(P.item_start, b);
+    const uint32_t cap = gload(P.item_start, b + 1) - (uint32_t)item_base;
+    __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0): this wave's DMA has landed
+    lds_barrier();
+    const uint32_t hb = (uint32_t)(off & 15);
+    if (tid == 0) {
+      meta_header(stage, hb, end >= off ? end - off : 0, meta[0]);
+      meta[1] = meta[0];
+      meta_trailer(stage, P.expect_type, cap, meta[1]);
+      *cks_bad = 0;
+    }
+    lds_barrier();
+    if (wave == 0) {
+      if (meta[0].st == ST_OK) {
+        uint64_t lo, hi;
+        xxh3_128_wave(stage, hb + kHdrLen, meta[0].len - kHdrLen, &kLongSecret, lo, hi);
+        if (lane == 0) *cks_bad = lo != meta[0].ck_lo || hi != meta[0].ck_hi;
+      }
+    } else {
+      const BlockMeta m = meta[1];
+      if (m.st == ST_OK) {
+        bool ok = true;
+        for (uint32_t r = tid - kWave; r < m.bin_len; r += (kBigWaves - 1) * kWave) {
+          ok &= walk_interval(stage, hb + kHdrLen, m, r,
+                              [&](uint32_t j, const ItemFields& f) { emit_global(P.out, item_base + j, f); });
+        }
+        if (!ok) atomicCAS(&meta[1].st, ST_OK, ST_PARSE);
+      }
+    }
+    lds_barrier();
+    if (tid == 0) {
+      const int32_t st = meta[0].st != ST_OK ? meta[0].st : *cks_bad ? (int32_t)ST_CKSUM : meta[1].st;
+      gstore(P.status, b, st);
+    }
+    lds_barrier();
+  }
+}
+
 // Workgroup = kGroupWaves waves sharing one LDS stage of up to 64 KiB (16
 // 4-KiB blocks, ~64 restart intervals).  Per group:
 //   all waves   LDS-DMA of the span (wave w moves 1-KiB pieces w, w+4, ...)
@@ -1533,8 +1605,15 @@ hipError_t launch_decode(const DecodeParams& P0, void* ws, hipStream_t st) {
     hipError_t e = launch_legacy(P, st);
     if (e != hipSuccess) return e;
   }
-  const uint32_t dgrid = P.n_blocks < 4096 ? P.n_blocks : 4096;
-  if (dgrid) hipLaunchKernelGGL(decode_deferred_kernel, dim3(dgrid), dim3(kWave), 0, st, P);
+  const uint32_t dgrid = P.n_blocks < 1024 ? P.n_blocks : 1024;
+  if (dgrid) {
+    static const bool attr = hipFuncSetAttribute((const void*)decode_deferred_staged_kernel,
+                                                 hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                 (int)(kBigStage + 256 + kStagePad)) == hipSuccess;
+    (void)attr;
+    hipLaunchKernelGGL(decode_deferred_staged_kernel, dim3(dgrid), dim3(kBigWaves * kWave), kBigStage + 256 + kStagePad,
+                       st, P);
+  }
   return hipGetLastError();
 }
 
