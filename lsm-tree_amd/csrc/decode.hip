@@ -32,7 +32,7 @@ namespace lsmgpu {
 // Diagnostic-only flags (lsm_decode_tuning.flags high bits): drop one phase to
 // price it in a profile.  Outputs are NOT valid with any of them set.
 constexpr uint32_t kDiagSkipHash = 0x100, kDiagSkipParse = 0x200, kDiagSkipStore = 0x400,
-                   kDiagSkipPhaseB = 0x800, kPrioA = 0x4000, kRingNt = 0x20000;
+                   kDiagSkipPhaseB = 0x800, kDiagHalfWalk = 0x1000, kPrioA = 0x4000, kRingNt = 0x20000;
 
 constexpr uint32_t kMaxGroup = 32;  // blocks per staged group
 // Internal status: the block needs the general path (index block, a record
@@ -285,7 +285,7 @@ struct WalkSlots {
 };
 
 __device__ __forceinline__ void phase_a2(const WalkSlots& W, uint32_t c_first, uint32_t c_step, uint32_t total,
-                                         uint32_t dummy) {
+                                         uint32_t dummy, uint32_t diag_half = 0) {
   const int lane = threadIdx.x & (kWave - 1);
   for (uint32_t c0 = c_first; c0 < total; c0 += c_step) {
     const uint32_t cg = c0 + lane;
@@ -311,7 +311,8 @@ __device__ __forceinline__ void phase_a2(const WalkSlots& W, uint32_t c_first, u
     const uint64_t tag = ((uint64_t)j << kRecBlockShift) | kRecValid;
     const uint32_t stop = p0 + e_rel;
     uint32_t a = p0 + (ok ? s_rel : 0), key = a;
-    const uint32_t max_count = __builtin_amdgcn_readfirstlane(wave_max_u32(count));
+    uint32_t max_count = __builtin_amdgcn_readfirstlane(wave_max_u32(count));
+    if (diag_half) max_count = (max_count + 1) / 2;  // diagnostic: price the walk's serial chain
     if (!max_count) continue;
     Shape sp;
     bool defer = false;  // a record shape the straight path does not take: whole block to the general path
@@ -364,15 +365,129 @@ __device__ __forceinline__ void phase_a2(const WalkSlots& W, uint32_t c_first, u
   }
 }
 
+// Phase A with two lanes per restart interval (adjacent lanes h = 0, 1): the
+// dependent chain of the walk is the latency the group waits for, so lane
+// h = 1 walks the second half of the interval from a PREDICTED start while
+// h = 0 walks the first half.  h = 1 parses the head and record 1 like h = 0,
+// then jumps to record ms at start(1) + (ms - 1) * len(1) (uniform records);
+// the prediction holds iff h = 0 ends exactly there (lane-pair exchange).  If
+// it does not, h = 0 walks the second half itself and overwrites h = 1's
+// descriptors.  A verified split is a true parse, so phase B's checks are
+// unchanged.  Work items: 2 per interval, item = c_first + lane + k c_step.
+__device__ __forceinline__ void phase_a_split(const uint8_t* img, BlockMeta* meta, const uint8_t* owner,
+                                              uint64_t* rec, uint32_t c_first, uint32_t c_step, uint32_t total,
+                                              uint32_t dummy) {
+  const int lane = threadIdx.x & (kWave - 1);
+  for (uint32_t c0 = c_first; c0 < 2 * total; c0 += c_step) {
+    const uint32_t item = c0 + lane;
+    const uint32_t c = item >> 1;
+    const bool h1 = (item & 1) != 0;
+    const bool live = c < total;
+    const uint32_t j = live ? owner[c] : 0;
+    const BlockMeta& m = meta[j];
+    const TrailerInfo t = trailer_of(m);
+    const uint32_t p0 = m.p0, rec_end = m.rec_end;
+    const uint32_t r = live ? c - m.chain0 : 0;
+    const bool last_iv = r + 1 == t.bin_len;
+    const uint32_t s_rel = bin_get(img, p0, t, r);
+    const uint32_t e_rel = last_iv ? t.rec_end : bin_get(img, p0, t, r + 1);
+    bool ok = s_rel < t.rec_end && e_rel <= t.rec_end && (r != 0 || s_rel == 0);
+    const uint32_t count = (live && ok) ? (last_iv ? t.item_count - r * t.ri : t.ri) : 0;
+    if (live && !ok && !h1) atomicCAS(&meta[j].st, ST_OK, ST_PARSE);
+    const uint32_t ib0 = m.item0 + r * t.ri;
+    const uint64_t tag = ((uint64_t)j << kRecBlockShift) | kRecValid;
+    const uint32_t stop = p0 + e_rel;
+    // split point: h0 takes records [0, ms), h1 records 1 and [ms, count)
+    const uint32_t ms = count >= 4 ? (count + 3) >> 1 : count;
+    const uint32_t steps = h1 ? (ms < count ? count - ms + 2 : 0) : ms;  // loop bound jj < steps
+    uint32_t a = p0 + (ok ? s_rel : 0), key = a;
+    const uint32_t max_steps = __builtin_amdgcn_readfirstlane(wave_max_u32(max(steps, min(count, 1u))));
+    if (!max_steps) continue;
+    Shape sp;
+    bool defer = false;
+    {  // restart head (both lanes parse it; h0 writes its descriptor)
+      const Win16 w = read_win16(img, a);
+      const RecHead hd = rec_head(w.lo, true);
+      const uint32_t nxt = a + rec_len(hd.vt, hd.q, read_u16_unaligned(img, a + hd.q));
+      key = a + hd.hdr;
+      sp = make_shape(min(hd.e1 >> 3, 5u), 1);
+      defer = count > 1 && !(hd.ok && valid_vtype(hd.vt));
+      const bool act = count > 0 && !defer;
+      if (count > 1 && act) ok = nxt < rec_end;
+      const uint64_t rbits = (count > 1) ? ((uint64_t)(hd.e1 >> 3) << kRecN1Shift) : 0;
+      rec[(act && !h1) ? ib0 : dummy] = rec_desc(a, count == 1 ? stop : nxt, key, tag | kRecRestart | rbits);
+      a = (act && ok) ? nxt : a;
+    }
+    uint32_t qp = 0, pred = 0;
+    uint32_t hi = (uint32_t)((((uint64_t)key << kRecKeyShift) | tag | sp.bits) >> 32);
+    const uint32_t dmy = dummy;
+    for (uint32_t jj = 1; jj < max_steps; ++jj) {
+      const uint64_t h = read_u64_unaligned(img, a);
+      uint32_t z = read_u16_unaligned(img, a + qp);
+      const uint32_t klen = (uint32_t)(h >> sp.kshift) & 0x7F;
+      uint32_t q = sp.hdr + klen;
+      uint32_t vt = (uint32_t)h & 0xFF;
+      if (((~h & sp.msk) != sp.pat) | (q != qp)) {  // rare: header shape or key length changed
+        const RecHead hd = rec_head(h, false);
+        if (hd.ok) sp = make_shape(hd.e1 >> 3, (hd.e2 - hd.e1) >> 3);
+        const uint32_t idx_d = (h1 && jj > 1) ? jj + ms - 2 : jj;
+        defer = defer || (jj < steps && idx_d < count && !hd.ok);
+        q = hd.q;
+        z = read_u16_unaligned(img, a + q);
+        qp = q;
+        hi = (uint32_t)((((uint64_t)key << kRecKeyShift) | tag | sp.bits) >> 32);
+      }
+      const uint32_t nxt = min(a + rec_len(vt, q, z), rec_end);
+      const uint32_t idx = (h1 && jj > 1) ? jj + ms - 2 : jj;
+      const bool act = jj < steps && idx < count && !defer;
+      const uint32_t end = idx + 1 == count ? stop : nxt;
+      rec[act ? ib0 + idx : dmy] = ((uint64_t)hi << 32) | (uint64_t)(a | (end << kRecEndShift));
+      uint32_t an = act ? nxt : a;
+      if (h1 && jj == 1 && act) {  // jump to record ms assuming records 1 .. ms-1 all have record 1's length
+        an = min(nxt + (ms - 2) * (nxt - a), rec_end);
+        pred = an;
+      }
+      a = an;
+    }
+    // h0 now sits at the start of record ms (if it walked that far)
+    const uint32_t a0 = (uint32_t)__shfl_xor((int)a, 1);
+    const bool split = ms < count;
+    const bool hit = !split || pred == a0;  // (read on h1 lanes)
+    const bool redo = (uint32_t)__shfl_xor((int)(hit ? 1 : 0), 1) == 0;  // on h0 lanes: h1 mispredicted
+    const bool my_redo = !h1 && split && redo && !defer;
+    // fallback: h0 walks records [ms, count) itself
+    const uint32_t need = my_redo ? count - ms : 0;
+    const uint32_t max_redo = __builtin_amdgcn_readfirstlane(wave_max_u32(need));
+    for (uint32_t k = 0; k < max_redo; ++k) {
+      const uint64_t h = read_u64_unaligned(img, a);
+      const RecHead hd = rec_head(h, false);
+      const uint32_t z = read_u16_unaligned(img, a + hd.q);
+      if (hd.ok) sp = make_shape(hd.e1 >> 3, (hd.e2 - hd.e1) >> 3);
+      const bool act = k < need && !defer;
+      defer = defer || (k < need && !hd.ok);
+      const uint32_t idx = ms + k;
+      const uint32_t nxt = min(a + rec_len(hd.vt, hd.q, z), rec_end);
+      const uint32_t end = idx + 1 == count ? stop : nxt;
+      const uint32_t hb = (uint32_t)((((uint64_t)key << kRecKeyShift) | tag | sp.bits) >> 32);
+      rec[(act && !defer) ? ib0 + idx : dmy] = ((uint64_t)hb << 32) | (uint64_t)(a | (end << kRecEndShift));
+      a = act ? nxt : a;
+    }
+    const bool keep = !h1 || (split && hit);  // a mispredicted h1 lane's flags are void
+    if (keep && defer) meta[j].st = ST_DEFER;                             // wins over PARSE
+    else if (keep && count && !ok) atomicCAS(&meta[j].st, ST_OK, ST_PARSE);
+  }
+}
+
 __device__ __forceinline__ void phase_a(const uint8_t* img, BlockMeta* meta, const uint8_t* owner, uint64_t* rec,
-                                        uint32_t c_first, uint32_t c_step, uint32_t total, uint32_t dummy) {
+                                        uint32_t c_first, uint32_t c_step, uint32_t total, uint32_t dummy,
+                                        uint32_t diag_half = 0) {
   WalkSlots W;
   W.img[0] = W.img[1] = img;
   W.meta[0] = W.meta[1] = meta;
   W.owner[0] = W.owner[1] = owner;
   W.rec[0] = W.rec[1] = rec;
   W.tot_a = total;
-  phase_a2(W, c_first, c_step, total, dummy);
+  phase_a2(W, c_first, c_step, total, dummy, diag_half);
 }
 
 // parse_data_fast for a record whose header shape (n1 seqno bytes, n2 shared
@@ -575,13 +690,17 @@ __global__ __launch_bounds__(kWave) void decode_deferred_kernel(DecodeParams P) 
 // oracle order (header, checksum, trailer / parse).  Larger blocks (full
 // index blocks) take the HBM path on wave 0.
 constexpr uint32_t kBigWaves = 4;
-constexpr uint32_t kBigStage = 80 * 1024;
+constexpr uint32_t kBigStage = 72 * 1024;
+
+constexpr uint32_t kBigContrib = 256;                        // LDS: contributions, 64 B per KiB
+constexpr uint32_t kBigStageOff = kBigContrib + (kBigStage / 1024 + 1) * 64;
 
 __global__ __launch_bounds__(kBigWaves * kWave) void decode_deferred_staged_kernel(DecodeParams P) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   BlockMeta* meta = reinterpret_cast<BlockMeta*>(smem);  // [0] header view, [1] trailer view
   uint32_t* cks_bad = reinterpret_cast<uint32_t*>(smem + 2 * sizeof(BlockMeta));
-  uint8_t* stage = smem + 256;
+  uint64_t* contrib = reinterpret_cast<uint64_t*>(smem + kBigContrib);
+  uint8_t* stage = smem + kBigStageOff;
   const uint32_t tid = threadIdx.x;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(tid / kWave);
   const int lane = tid & (kWave - 1);
@@ -613,10 +732,16 @@ __global__ __launch_bounds__(kBigWaves * kWave) void decode_deferred_staged_kern
       *cks_bad = 0;
     }
     lds_barrier();
+    // payload checksum: per-KiB contributions on all waves, then the chain on wave 0
+    const bool hdr_ok = meta[0].st == ST_OK;
+    const uint32_t plen = meta[0].len - kHdrLen;
+    if (hdr_ok && plen > 240) xxh3_kib_contribs(stage, hb + kHdrLen, plen, &kLongSecret, contrib, wave, kBigWaves);
+    lds_barrier();
     if (wave == 0) {
-      if (meta[0].st == ST_OK) {
+      if (hdr_ok) {
         uint64_t lo, hi;
-        xxh3_128_wave(stage, hb + kHdrLen, meta[0].len - kHdrLen, &kLongSecret, lo, hi);
+        if (plen > 240) xxh3_128_wave_finish(stage, hb + kHdrLen, plen, &kLongSecret, contrib, lo, hi);
+        else xxh3_128_wave(stage, hb + kHdrLen, plen, &kLongSecret, lo, hi);
         if (lane == 0) *cks_bad = lo != meta[0].ck_lo || hi != meta[0].ck_hi;
       }
     } else {
@@ -708,7 +833,9 @@ __global__ __launch_bounds__(kGroupWaves * kWave) __attribute__((amdgpu_waves_pe
         return z;
       }
       const Group g = form_group(P, bb, b_begin, b_end, gmax, offr, itr);
-      if (g.k) return g;
+      // a lone block filling most of the stage would be hashed by one 16-lane
+      // row: the staged general path hashes it with four waves instead
+      if (g.k > 1 || (g.k == 1 && g.span1 - g.span0 <= P.stage_bytes / 2)) return g;
       if (tid == 0) defer_block(P, bb);
       bb += 1;
     }
@@ -775,13 +902,15 @@ __global__ __launch_bounds__(kGroupWaves * kWave) __attribute__((amdgpu_waves_pe
     {
       const uint32_t total = (P.flags & kDiagSkipParse) ? 0
                              : meta[k - 1].chain0 + (meta[k - 1].st == ST_OK ? meta[k - 1].bin_len : 0);
-      const uint32_t nA = min((total + kWave - 1) / kWave, kGroupWaves - 1);
+      const bool split = (P.flags & kDecodeSplitWalk) != 0;
+      const uint32_t nA = min(((split ? 2 : 1) * total + kWave - 1) / kWave, kGroupWaves - 1);
       const uint32_t role = (wave + kGroupWaves - iter % kGroupWaves) % kGroupWaves;  // rotates per group
       if (role < nA) {
         // the serial walk is the group's critical path: let it win issue
         // arbitration against the other workgroup's waves on this SIMD
         if (P.flags & kPrioA) __builtin_amdgcn_s_setprio(3);
-        phase_a(stage, meta, owner, rec, role * kWave, nA * kWave, total, P.tile_items);
+        if (split) phase_a_split(stage, meta, owner, rec, role * kWave, nA * kWave, total, P.tile_items);
+        else phase_a(stage, meta, owner, rec, role * kWave, nA * kWave, total, P.tile_items, P.flags & kDiagHalfWalk);
         if (P.flags & kPrioA) __builtin_amdgcn_s_setprio(0);
         LSM_TICK(kTmA);
       } else if (!(P.flags & kDiagSkipHash)) {
@@ -1609,10 +1738,10 @@ hipError_t launch_decode(const DecodeParams& P0, void* ws, hipStream_t st) {
   if (dgrid) {
     static const bool attr = hipFuncSetAttribute((const void*)decode_deferred_staged_kernel,
                                                  hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                 (int)(kBigStage + 256 + kStagePad)) == hipSuccess;
+                                                 (int)(kBigStageOff + kBigStage + kStagePad)) == hipSuccess;
     (void)attr;
-    hipLaunchKernelGGL(decode_deferred_staged_kernel, dim3(dgrid), dim3(kBigWaves * kWave), kBigStage + 256 + kStagePad,
-                       st, P);
+    hipLaunchKernelGGL(decode_deferred_staged_kernel, dim3(dgrid), dim3(kBigWaves * kWave),
+                       kBigStageOff + kBigStage + kStagePad, st, P);
   }
   return hipGetLastError();
 }

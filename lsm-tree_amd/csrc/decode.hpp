@@ -33,6 +33,7 @@ uint32_t decode_lds_bytes(uint32_t stage_bytes, uint32_t tile_items, uint32_t bl
 uint32_t decode_ring_lds_bytes(uint32_t slots, uint32_t slot_bytes, uint32_t tile_items);
 constexpr uint32_t kDecodeLegacy = 0x10000;  // tuning flag: the single-stage kernel (decode_blocks_kernel)
 constexpr uint32_t kDecodeDouble = 0x40000;  // tuning flag: legacy kernel with two stage slots (prefetch one group ahead)
+constexpr uint32_t kDecodeSplitWalk = 0x100000;  // tuning flag: two lanes per restart interval in phase A
 constexpr uint32_t kDecodeRing = 0x80000;    // tuning flag: the LDS-ring kernel (decode_ring_kernel)
 constexpr bool kDecodeDefaultRing = false;   // kernel when neither flag is given
 constexpr uint32_t kRingWaves = 16;

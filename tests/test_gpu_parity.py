@@ -90,6 +90,7 @@ def test_decode_golden_blocks(gpu, golden_blocks):
 LEG = 0x10000  # LSM_DECODE_LEGACY
 RING = 0x80000  # LSM_DECODE_RING
 DBL = 0x40000  # LSM_DECODE_DOUBLE
+SPLIT = 0x100000  # LSM_DECODE_SPLIT_WALK
 # (blocks_per_wave, slot/stage bytes, tile items, flags, ring slots, planners, hashers, loaders)
 TUNINGS = [None,                                 # library default kernel
            (0, 0, 0, RING),                      # ring defaults
@@ -101,7 +102,8 @@ TUNINGS = [None,                                 # library default kernel
            (0, 32768, 512, RING | 0x20000, 3),   # nt DMA, 3 slots
            (0, 16384, 256, RING, 2, 1, 1),       # 2-slot ring
            (48, 65536, 1024, LEG), (1, 256, 64, LEG), (63, 65536, 2048, LEG),
-           (48, 32768, 512, LEG | DBL), (48, 65536, 1024, LEG | DBL), (1, 256, 64, LEG | DBL), (5, 4096, 64, LEG | DBL)]
+           (48, 32768, 512, LEG | DBL), (48, 65536, 1024, LEG | DBL), (1, 256, 64, LEG | DBL), (5, 4096, 64, LEG | DBL),
+           (48, 65536, 1024, LEG | SPLIT), (3, 8192, 128, LEG | SPLIT), (48, 32768, 512, LEG | DBL | SPLIT)]
 
 
 @pytest.mark.parametrize("tuning", TUNINGS)
@@ -297,7 +299,7 @@ def test_structurally_broken_payloads_with_valid_checksums(gpu):
             payload = payload[:rng.randint(0, 40)]
         blocks.append(pyoracle.block_write(bytes(payload)))
     buf, off = pack(blocks)
-    for tuning in (None, (1, 256, 64)):
+    for tuning in (None, (1, 256, 64), (48, 65536, 1024, LEG | SPLIT)):
         g = gpu_decode(gpu, buf, off, tuning=tuning)
         parsed, item_start, status = pyoracle.decode_blocks(buf, off)
         compare_decode(g, parsed, item_start, status)
@@ -392,6 +394,6 @@ def test_resealed_mutation_fuzz(gpu):
     blocks = off[1:]
     parsed, item_start, status = pyoracle.decode_blocks(buf, off)
     assert (status == 0).sum() > len(blocks) // 4 and (status == 5).sum() > len(blocks) // 10
-    for tuning in (None, (1, 256, 64), (8, 8192, 256)):
+    for tuning in (None, (1, 256, 64), (8, 8192, 256), (8, 8192, 256, LEG | SPLIT), (48, 65536, 1024, LEG | SPLIT)):
         g = gpu_decode(gpu, buf, off, tuning=tuning)
         compare_decode(g, parsed, item_start, status)
