@@ -127,6 +127,7 @@ typedef struct lsm_decode_tuning {
 #define LSM_DECODE_LEGACY 0x10000u
 #define LSM_DECODE_DOUBLE 0x40000u /* legacy kernel, two stage slots: the next group's LDS-DMA overlaps this group's parse */
 #define LSM_DECODE_RING 0x80000u
+#define LSM_DECODE_SPLIT_WALK 0x100000u /* legacy kernel: two lanes per restart interval in the boundary walk */
 
 /* Point-read results (DataBlock::point_read -> Option<InternalValue>,
  * data_block/mod.rs:412-472), one row per query; NULL fields other than item
