@@ -40,7 +40,7 @@ constexpr uint32_t kImgMedium = 20 * 1024;
 constexpr uint32_t kImgBig = 96 * 1024;
 constexpr uint32_t kSmallWaves = 4;
 constexpr uint32_t kE3HashChunk = 4096;    // buckets per LDS pass in E3
-enum : uint32_t { kListMedium = 0, kListBig = 1, kListHuge = 2, kLists = 3 };
+constexpr uint64_t kListedOne = 1ULL << 40, kOffMask = kListedOne - 1;
 
 struct alignas(16) BlockPlan {
   uint32_t recs;      // bytes of all records
@@ -69,15 +69,30 @@ __device__ __forceinline__ Win16 read_win16_at(const uint8_t* base, uint64_t off
   return read_win16(base + (off & ~3ULL), (uint32_t)(off & 3));
 }
 
-// longest_shared_prefix_length, src/table/util.rs:125-130
+// longest_shared_prefix_length, src/table/util.rs:125-130.  Up to 48 bytes
+// per step with all six windows in flight together (one HBM round trip for
+// the keys of every BASELINE shape).
 __device__ __forceinline__ uint32_t lcp_global(const uint8_t* keys, uint64_t a, uint64_t b, uint32_t n) {
   uint32_t k = 0;
   while (k < n) {
-    const Win16 wa = read_win16_at(keys, a + k), wb = read_win16_at(keys, b + k);
-    const uint64_t x0 = wa.lo ^ wb.lo, x1 = wa.hi ^ wb.hi;
-    if (x0) return min(n, k + (uint32_t)(__builtin_ctzll(x0) >> 3));
-    if (x1) return min(n, k + 8 + (uint32_t)(__builtin_ctzll(x1) >> 3));
-    k += 16;
+    Win16 wa[3], wb[3];
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      wa[i] = wb[i] = Win16{0, 0};
+      if (i == 0 || k + 16 * i < n) {
+        wa[i] = read_win16_at(keys, a + k + 16 * i);
+        wb[i] = read_win16_at(keys, b + k + 16 * i);
+      }
+    }
+#pragma unroll
+    for (int i = 0; i < 3; ++i) {
+      const uint32_t kk = k + 16 * i;
+      if (kk >= n) return n;
+      const uint64_t x0 = wa[i].lo ^ wb[i].lo, x1 = wa[i].hi ^ wb[i].hi;
+      if (x0) return min(n, kk + (uint32_t)(__builtin_ctzll(x0) >> 3));
+      if (x1) return min(n, kk + 8 + (uint32_t)(__builtin_ctzll(x1) >> 3));
+    }
+    k += 48;
   }
   return n;
 }
@@ -96,8 +111,8 @@ struct EncodeParams {
   uint16_t* shared;     // [n_items]
   uint64_t* sizes;      // [n_blocks] block bytes (E1) -> exclusive scan -> block_off
   BlockPlan* plans;     // [n_blocks]
-  uint32_t* lists;      // [kLists][n_blocks]: medium, big, huge blocks
-  uint32_t* list_count; // [kLists]
+  uint32_t* lists;      // [n_blocks]: the listed blocks in block order (from the size scan)
+  uint32_t* list_count; // [1]
 };
 
 __device__ __forceinline__ bool is_index(const EncodeParams& P) { return P.type == 1; }
@@ -532,14 +547,13 @@ __global__ __launch_bounds__(256) void encode_sizes_kernel(EncodeParams P) {
     P.status[b] = ST_BAD_ARG;
   } else {
     const uint64_t need = e2_need(total, hash_w);
-    if (need > kImgSmall || n > kWave) {
-      const uint32_t l = need <= kImgMedium ? kListMedium : need <= kImgBig ? kListBig : kListHuge;
-      flags = l == kListMedium ? kPlanMedium : l == kListBig ? kPlanBig : kPlanHuge;
-      P.lists[(size_t)l * P.n_blocks + atomicAdd(&P.list_count[l], 1u)] = b;
-    }
+    if (need > kImgSmall || n > kWave)
+      flags = need <= kImgMedium ? kPlanMedium : need <= kImgBig ? kPlanBig : kPlanHuge;
   }
   P.plans[b] = BlockPlan{(uint32_t)carry, bin_len, hash_w, step | (flags << 8)};
-  P.sizes[b] = bad ? 0 : total;
+  // bits 40.. count the listed (not small) blocks: the size scan numbers them
+  // (no global atomics: one counter serialised a batch of uniformly large blocks)
+  P.sizes[b] = (bad ? 0 : total) | ((flags & (kPlanMedium | kPlanBig | kPlanHuge)) ? kListedOne : 0);
 }
 
 // ------------------------------------------------- E2: small blocks in LDS
@@ -603,22 +617,24 @@ __global__ __launch_bounds__(kSmallWaves * kWave) __attribute__((amdgpu_waves_pe
 }
 
 // Listed medium / big blocks: one wave per workgroup, grid-stride over the list.
-__global__ __launch_bounds__(kWave) void encode_write_list_kernel(EncodeParams P, uint32_t list) {
+__global__ __launch_bounds__(kWave) void encode_write_list_kernel(EncodeParams P, uint32_t plan_flag) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  const uint32_t count = P.list_count[list];
-  const uint32_t* L = P.lists + (size_t)list * P.n_blocks;
-  for (uint32_t li = blockIdx.x; li < count; li += gridDim.x) write_block_lds(P, L[li], smem);
+  const uint32_t count = P.list_count[0];
+  for (uint32_t li = blockIdx.x; li < count; li += gridDim.x) {
+    const uint32_t b = P.lists[li];
+    if ((P.plans[b].step_flags >> 8) == plan_flag) write_block_lds(P, b, smem);
+  }
 }
 
 // ----------------------------------------------------- E3: HBM write pass
 __global__ __launch_bounds__(64) void encode_large_kernel(EncodeParams P) {
   __shared__ uint32_t hlo[kE3HashChunk], hhi[kE3HashChunk];
   const int lane = threadIdx.x;
-  const uint32_t count = P.list_count[kListHuge];
-  const uint32_t* L = P.lists + (size_t)kListHuge * P.n_blocks;
+  const uint32_t count = P.list_count[0];
   for (uint32_t li = blockIdx.x; li < count; li += gridDim.x) {
-    const uint32_t b = L[li];
+    const uint32_t b = P.lists[li];
     const BlockPlan pl = P.plans[b];
+    if ((pl.step_flags >> 8) != kPlanHuge) continue;
     const uint32_t step = pl.step_flags & 0xFF;
     const uint64_t dst_off = P.block_off[b], dst_end = P.block_off[b + 1];
     if (dst_end > P.out_cap) {
@@ -687,16 +703,26 @@ __global__ __launch_bounds__(64) void encode_large_kernel(EncodeParams P) {
   }
 }
 
-struct BlockOffOut {
+// Scan output: block offsets (low 40 bits of the prefix) and the list of the
+// listed blocks (high bits = their running count).
+struct EncodeOffOut {
   uint64_t* off;
-  __device__ void operator()(uint64_t i, uint64_t prefix) const { off[i] = prefix; }
+  const uint64_t* sizes;
+  uint32_t* list;
+  uint32_t* count;
+  uint64_t n;
+  __device__ void operator()(uint64_t i, uint64_t prefix) const {
+    off[i] = prefix & kOffMask;
+    if (i < n && (sizes[i] & ~kOffMask)) list[prefix >> 40] = (uint32_t)i;
+    if (i == n) *count = (uint32_t)(prefix >> 40);
+  }
 };
 
 static size_t al256(size_t x) { return (x + 255) / 256 * 256; }
 
 size_t encode_workspace_size(uint64_t n_items, uint32_t n_blocks) {
   return al256(n_items * 2) + al256((size_t)n_blocks * 8) + al256((size_t)n_blocks * sizeof(BlockPlan)) +
-         al256((size_t)n_blocks * 4 * kLists) + 256 + al256(scan_tiles(n_blocks) * 8);
+         al256((size_t)n_blocks * 4) + 256 + al256(scan_tiles(n_blocks) * 8);
 }
 
 uint64_t encode_bound(uint64_t n_items, uint32_t n_blocks, uint64_t key_bytes, uint64_t val_bytes,
@@ -726,13 +752,14 @@ hipError_t launch_encode(const lsm_items& items, const uint32_t* starts, uint32_
   P.shared = (uint16_t*)w; w += al256(items.n_items * 2);
   P.sizes = (uint64_t*)w; w += al256((size_t)n_blocks * 8);
   P.plans = (BlockPlan*)w; w += al256((size_t)n_blocks * sizeof(BlockPlan));
-  P.lists = (uint32_t*)w; w += al256((size_t)n_blocks * 4 * kLists);
+  P.lists = (uint32_t*)w; w += al256((size_t)n_blocks * 4);
   P.list_count = (uint32_t*)w; w += 256;
   uint64_t* tiles = (uint64_t*)w;
-  hipError_t e = hipMemsetAsync(P.list_count, 0, 16, st);
-  if (e != hipSuccess) return e;
+  hipError_t e;
   hipLaunchKernelGGL(encode_sizes_kernel, dim3((n_blocks + 3) / 4), dim3(256), 0, st, P);
-  if ((e = launch_excl_scan(P.sizes, n_blocks, tiles, BlockOffOut{block_off}, st)) != hipSuccess) return e;
+  if ((e = launch_excl_scan(P.sizes, n_blocks, tiles,
+                            EncodeOffOut{block_off, P.sizes, P.lists, P.list_count, n_blocks}, st)) != hipSuccess)
+    return e;
   static bool attrs = [] {
     return hipFuncSetAttribute((const void*)encode_write_list_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
                                (int)kImgBig) == hipSuccess;
@@ -740,8 +767,8 @@ hipError_t launch_encode(const lsm_items& items, const uint32_t* starts, uint32_
   (void)attrs;
   hipLaunchKernelGGL(encode_write_kernel, dim3((n_blocks + kSmallWaves - 1) / kSmallWaves), dim3(kSmallWaves * kWave),
                      kSmallWaves * kImgSmall, st, P);
-  hipLaunchKernelGGL(encode_write_list_kernel, dim3(2048), dim3(kWave), kImgMedium, st, P, (uint32_t)kListMedium);
-  hipLaunchKernelGGL(encode_write_list_kernel, dim3(512), dim3(kWave), kImgBig, st, P, (uint32_t)kListBig);
+  hipLaunchKernelGGL(encode_write_list_kernel, dim3(2048), dim3(kWave), kImgMedium, st, P, kPlanMedium);
+  hipLaunchKernelGGL(encode_write_list_kernel, dim3(512), dim3(kWave), kImgBig, st, P, kPlanBig);
   hipLaunchKernelGGL(encode_large_kernel, dim3(1024), dim3(64), 0, st, P);
   return hipGetLastError();
 }

@@ -109,3 +109,17 @@ def test_product_path_has_no_cpu_fallback(L):
         pytest.skip("GPU present")
     with pytest.raises(L.LsmError):
         L.decode_blocks(torch.zeros(128, dtype=torch.uint8), torch.zeros(2, dtype=torch.int64))
+
+
+def test_bench_workload_cut_rules(L):
+    """The fixed item counts bench.py cuts its synthetic batches at equal the
+    reference writer rule (writer/mod.rs:284-290) for every BASELINE shape
+    (52 @ 4 KiB 16/64, 56 @ 16 KiB 40/256, 205 @ 16 KiB,
+    820 @ 64 KiB)."""
+    import sys
+    sys.path.insert(0, str(ROOT))
+    import bench
+    for ipb, kl, vl, bs in ((52, 16, 64, 4096), (56, 40, 256, 16384), (205, 16, 64, 16384), (820, 16, 64, 65536)):
+        bench.check_cut_rule(L, ipb, kl, vl, bs)
+    for bs, ipb, kind, est in bench.C5_SEGMENTS:
+        bench.check_cut_rule(L, ipb, 16, 64, bs)
