@@ -660,7 +660,10 @@ __device__ __forceinline__ Group form_group(const DecodeParams& P, uint32_t b, u
   const uint64_t off_b = wave_readlane_u64(G.off_j, 0);
   G.g_item0 = wave_readlane_u32(G.it0_j, 0);
   G.span0 = off_b & ~15ULL;
-  const bool fits = in_run && G.end_j >= G.off_j && G.off_j >= off_b &&
+  // lone blocks (lone_block) never join a group: they are listed for the general path up front
+  const bool lone = ((G.end_j + 15) & ~15ULL) - (G.off_j & ~15ULL) > P.stage_bytes / 2 ||
+                    G.it1_j - G.it0_j > P.tile_items;
+  const bool fits = in_run && !lone && G.end_j >= G.off_j && G.off_j >= off_b &&
                     ((G.end_j + 15) & ~15ULL) - G.span0 <= P.stage_bytes && G.it1_j - G.g_item0 <= P.tile_items;
   G.k = (uint32_t)__builtin_ctzll(~__ballot(fits));  // lanes >= gmax never fit
   G.span1 = G.k ? (wave_readlane_u64(G.end_j, G.k - 1) + 15) & ~15ULL : G.span0;
@@ -672,6 +675,17 @@ __device__ __forceinline__ Group form_group(const DecodeParams& P, uint32_t b, u
 __device__ __forceinline__ void defer_block(const DecodeParams& P, uint32_t b) {
   const uint32_t slot = atomicAdd(P.defer_count, 1u);
   gstore(P.defer_list, slot, b);
+}
+// Wave-level: lanes with `pred` list block b (one atomic per wave, not per block).
+__device__ __forceinline__ void defer_blocks_wave(const DecodeParams& P, bool pred, uint32_t b) {
+  const uint64_t m = __ballot(pred);
+  if (!m) return;
+  const int lane = threadIdx.x & (kWave - 1);
+  uint32_t base = 0;
+  if (lane == (int)__builtin_ctzll(m)) base = atomicAdd(P.defer_count, (uint32_t)__builtin_popcountll(m));
+  base = (uint32_t)__shfl((int)base, (int)__builtin_ctzll(m));
+  const uint32_t rank = (uint32_t)__builtin_popcountll(m & ((1ULL << lane) - 1));
+  if (pred) gstore(P.defer_list, base + rank, b);
 }
 
 // General path for the deferred blocks: one wave per block, straight from
@@ -833,11 +847,8 @@ __global__ __launch_bounds__(kGroupWaves * kWave) __attribute__((amdgpu_waves_pe
         return z;
       }
       const Group g = form_group(P, bb, b_begin, b_end, gmax, offr, itr);
-      // a lone block filling most of the stage would be hashed by one 16-lane
-      // row: the staged general path hashes it with four waves instead
-      if (g.k > 1 || (g.k == 1 && g.span1 - g.span0 <= P.stage_bytes / 2)) return g;
-      if (tid == 0) defer_block(P, bb);
-      bb += 1;
+      if (g.k) return g;
+      bb += 1;  // a lone block: listed for the general path before the loop
     }
   };
   // LDS-DMA of a group's span into a stage slot (wave w moves 1-KiB pieces
@@ -859,6 +870,17 @@ __global__ __launch_bounds__(kGroupWaves * kWave) __attribute__((amdgpu_waves_pe
       }
     }
   };
+  // Lone blocks (larger than half the stage, or more items than a tile) go to
+  // the general path, decode_deferred_staged_kernel, which hashes a large
+  // block with four waves rather than one 16-lane row: listed here, one
+  // atomic per workgroup.
+  if (wave == 0) {
+    const uint64_t nx = wave_shfl_u64(offr, min(lane + 1, kWave - 1));
+    const uint32_t ix = (uint32_t)__shfl((int)itr, min(lane + 1, kWave - 1));
+    const bool in = b_begin + lane < b_end;
+    const bool lone = in && (((nx + 15) & ~15ULL) - (offr & ~15ULL) > P.stage_bytes / 2 || ix - itr > P.tile_items);
+    defer_blocks_wave(P, lone, b_begin + lane);
+  }
   Group G = next_group(b_begin);
   uint32_t cur = 0;
   if (G.k) issue_dma(G, img);
@@ -937,14 +959,17 @@ __global__ __launch_bounds__(kGroupWaves * kWave) __attribute__((amdgpu_waves_pe
     if (!(P.flags & (kDiagSkipParse | kDiagSkipPhaseB))) phase_b<kAllFields>(P, stage, meta, rec, G.n_items, G.g_item0, threadIdx.x, blockDim.x);
     LSM_TICK(kTmB);
     lds_barrier();
-    if (wave == 0 && (uint32_t)lane < k) {
-      const BlockMeta& m = meta[lane];
-      const int32_t st = m.hdr_st != ST_OK ? m.hdr_st
-                         : m.hck_bad ? (int32_t)ST_HDR_CKSUM
-                         : m.ck_bad  ? (int32_t)ST_CKSUM
-                                     : m.st;
-      if (st == ST_DEFER) defer_block(P, b + lane);
-      else gstore(P.status, b + lane, st);
+    if (wave == 0) {
+      int32_t st = ST_OK;
+      if ((uint32_t)lane < k) {
+        const BlockMeta& m = meta[lane];
+        st = m.hdr_st != ST_OK ? m.hdr_st
+             : m.hck_bad ? (int32_t)ST_HDR_CKSUM
+             : m.ck_bad  ? (int32_t)ST_CKSUM
+                         : m.st;
+        if (st != ST_DEFER) gstore(P.status, b + lane, st);
+      }
+      defer_blocks_wave(P, (uint32_t)lane < k && st == ST_DEFER, b + lane);
     }
     if (!dbl && Gn.k) issue_dma(Gn, img);  // single stage: refill after phase B
     G = Gn;
