@@ -104,6 +104,7 @@ struct EncodeParams {
   uint32_t ri;
   float ratio;
   uint32_t type;
+  uint32_t diag;  // lsm_block_params.reserved: diagnostic ablations (0 in normal use)
   uint8_t* out;
   uint64_t out_cap;
   uint64_t* block_off;
@@ -432,15 +433,18 @@ __device__ __forceinline__ void finish_block_lds(const EncodeParams& P, uint32_t
   for (uint32_t k = lane; k < pl.hash_w; k += kWave) img[p0 + hash_off + k] = (uint8_t)bucket_byte(hlo[k], hhi[k]);
   write_trailer_bytes(img, p0 + plen - kTrailerLen, ri, step, pl.bin_len, bin_off, pl.hash_w, hash_off, n);
   wave_lds_sync();
-  uint64_t ck_lo, ck_hi;
-  xxh3_128_wave(img, p0, plen, &kLongSecret, ck_lo, ck_hi);
-  write_header_bytes(img, pad, P.type, ck_lo, ck_hi, plen);
+  if (!(P.diag & 2)) {
+    uint64_t ck_lo, ck_hi;
+    xxh3_128_wave(img, p0, plen, &kLongSecret, ck_lo, ck_hi);
+    write_header_bytes(img, pad, P.type, ck_lo, ck_hi, plen);
+  }
   wave_lds_sync();
-  const uint32_t chunks = (pad + total + 15) >> 4;
+  const uint32_t chunks = (P.diag & 4) ? 0 : (pad + total + 15) >> 4;
   for (uint32_t c = lane; c < chunks; c += kWave) {
     const uint32_t lo = c * 16, hi = lo + 16;
     if (lo >= pad && hi <= pad + total) {
-      reinterpret_cast<u32x4*>(gdst)[c] = reinterpret_cast<const u32x4*>(img)[c];
+      // streaming output: non-temporal (measured 2 % faster than a plain store)
+      __builtin_nontemporal_store(reinterpret_cast<const u32x4*>(img)[c], reinterpret_cast<u32x4*>(gdst) + c);
     } else {
       for (uint32_t k = max(lo, pad); k < min(hi, pad + total); ++k) gdst[k] = img[k];
     }
@@ -603,7 +607,7 @@ __global__ __launch_bounds__(kSmallWaves * kWave) __attribute__((amdgpu_waves_pe
     hhi[k] = 0;
   }
   wave_lds_sync();
-  if ((uint32_t)lane < n) {
+  if ((uint32_t)lane < n && !(P.diag & 1)) {
     rc.store(P, m, head, img);
     if (head) store_le(img, p0 + pl.recs + 1 + (lane / ri) * step, roff, step);
     if (pl.hash_w) {
@@ -744,6 +748,7 @@ hipError_t launch_encode(const lsm_items& items, const uint32_t* starts, uint32_
   P.ri = params.block_type == 1 ? 1 : params.restart_interval;
   P.ratio = params.block_type == 1 ? 0.0f : params.hash_ratio;
   P.type = params.block_type;
+  P.diag = params.reserved;
   P.out = out;
   P.out_cap = out_cap;
   P.block_off = block_off;

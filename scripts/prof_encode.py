@@ -19,6 +19,7 @@ def main():
     ap.add_argument("--blocks", type=int, default=1 << 20)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--workload", default="counter", choices=["counter", "prefix16k"])
+    ap.add_argument("--ablate", action="store_true", help="diagnostic ablations (lsm_block_params.reserved bits)")
     args = ap.parse_args()
     torch.cuda.set_device(0)
     nb = args.blocks
@@ -38,6 +39,25 @@ def main():
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / args.reps
     assert int((enc["status"][:nb] != 0).sum()) == 0
+    if args.ablate:
+        import ctypes as C
+        L = lsmgpu.lib()
+        for bits, name in ((1, "no record stores"), (2, "no hash/header"), (4, "no copy-out"), (7, "none of them")):
+            orig = lsmgpu.LsmBlockParams
+            class P2(C.Structure):  # noqa: E306
+                _fields_ = orig._fields_
+            def mk(ri, bt, c, r, hr, bits=bits):
+                return orig(ri, bt, c, bits, hr)
+            lsmgpu.LsmBlockParams = mk
+            enc_ctx.encode(items, starts, nb, out=enc)
+            torch.cuda.synchronize()
+            e0.record()
+            for _ in range(args.reps):
+                enc_ctx.encode(items, starts, nb, out=enc)
+            e1.record()
+            torch.cuda.synchronize()
+            lsmgpu.LsmBlockParams = orig
+            print(f"  ablate {name:20s} {e0.elapsed_time(e1) / args.reps:.3f} ms", flush=True)
     print(f"encode {args.workload}: {nb} blocks {n_items} items {total} bytes  {ms:.3f} ms  "
           f"{total / ms / 1e6:.1f} GB/s written", flush=True)
 
