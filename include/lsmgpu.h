@@ -104,7 +104,8 @@ typedef struct lsm_block_params {
     uint8_t restart_interval; /* data_block_restart_interval (config default 16); forced 1 for index */
     uint8_t block_type;       /* LSM_BLOCK_DATA / LSM_BLOCK_INDEX / LSM_BLOCK_META */
     uint8_t compression;      /* 0 = CompressionType::None (the only supported value) */
-    uint8_t reserved;
+    uint8_t reserved;         /* must be 0 (non-zero bits are diagnostic ablations that skip
+                                 parts of the encode and leave the output invalid) */
     float hash_ratio;         /* data_block_hash_ratio (default 0.0) */
 } lsm_block_params;
 
