@@ -20,8 +20,8 @@ int set_hip_error(hipError_t e, const char* where) {
 
 // legacy single-stage kernel (LSM_DECODE_LEGACY)
 constexpr uint32_t kDefaultBlocksPerWave = 48;  // per workgroup
-constexpr uint32_t kDefaultStageBytes = 65536;
-constexpr uint32_t kDefaultTileItems = 1024;
+constexpr uint32_t kDefaultStageBytes = 32768;  // four 4-wave workgroups per CU (LDS ~40 KiB each)
+constexpr uint32_t kDefaultTileItems = 448;
 // ring kernel (default)
 constexpr uint32_t kRingSlotBytes = 32768, kRingTileItems = 512, kRingSlots = 4, kRingWalkers = 3,
                    kRingHashers = 4, kRingLoaders = 4;

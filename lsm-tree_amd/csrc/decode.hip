@@ -661,7 +661,7 @@ __device__ __forceinline__ Group form_group(const DecodeParams& P, uint32_t b, u
   G.g_item0 = wave_readlane_u32(G.it0_j, 0);
   G.span0 = off_b & ~15ULL;
   // lone blocks (lone_block) never join a group: they are listed for the general path up front
-  const bool lone = ((G.end_j + 15) & ~15ULL) - (G.off_j & ~15ULL) > P.stage_bytes / 2 ||
+  const bool lone = ((G.end_j + 15) & ~15ULL) - (G.off_j & ~15ULL) > P.stage_bytes ||
                     G.it1_j - G.it0_j > P.tile_items;
   const bool fits = in_run && !lone && G.end_j >= G.off_j && G.off_j >= off_b &&
                     ((G.end_j + 15) & ~15ULL) - G.span0 <= P.stage_bytes && G.it1_j - G.g_item0 <= P.tile_items;
@@ -788,7 +788,13 @@ __global__ __launch_bounds__(kBigWaves * kWave) void decode_deferred_staged_kern
 // pa rotates with the group index so the serial walk lands on each SIMD in
 // turn.  Phase A needs only the trailer, not the checksum, so it runs
 // concurrently with the hash; statuses merge in oracle order at the end.
-constexpr uint32_t kGroupWaves = 8;
+#ifndef LSM_DEC_WAVES
+#define LSM_DEC_WAVES 4
+#endif
+#ifndef LSM_DEC_WPE
+#define LSM_DEC_WPE 3
+#endif
+constexpr uint32_t kGroupWaves = LSM_DEC_WAVES;
 
 // Diagnostic phase timers (flag kDiagTimers): per workgroup clock64() deltas,
 // summed over the grid; read back with lsm_diag_decode_timers (abi.hip).
@@ -797,7 +803,7 @@ enum : int { kTmForm, kTmDma, kTmHdr, kTmA, kTmHash, kTmSplit, kTmB, kTmTail, kT
 __device__ unsigned long long g_decode_timers[kTmN];
 
 template <bool kTimed, bool kAllFields>
-__global__ __launch_bounds__(kGroupWaves * kWave) __attribute__((amdgpu_waves_per_eu(4))) void decode_blocks_kernel(DecodeParams P) {
+__global__ __launch_bounds__(kGroupWaves * kWave) __attribute__((amdgpu_waves_per_eu(LSM_DEC_WPE))) void decode_blocks_kernel(DecodeParams P) {
   // LDS: [meta: G x 80 B][rec: u64 per item + 1 scratch][owner: u8 per item][staged bytes + pad]
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint32_t gmax = min(kMaxGroup, P.blocks_per_wave);
@@ -870,15 +876,14 @@ __global__ __launch_bounds__(kGroupWaves * kWave) __attribute__((amdgpu_waves_pe
       }
     }
   };
-  // Lone blocks (larger than half the stage, or more items than a tile) go to
-  // the general path, decode_deferred_staged_kernel, which hashes a large
-  // block with four waves rather than one 16-lane row: listed here, one
-  // atomic per workgroup.
+  // Lone blocks (larger than the stage, or more items than a tile) go to the
+  // general path, decode_deferred_staged_kernel (a 72 KiB stage, the block
+  // hashed by four waves): listed here, one atomic per workgroup.
   if (wave == 0) {
     const uint64_t nx = wave_shfl_u64(offr, min(lane + 1, kWave - 1));
     const uint32_t ix = (uint32_t)__shfl((int)itr, min(lane + 1, kWave - 1));
     const bool in = b_begin + lane < b_end;
-    const bool lone = in && (((nx + 15) & ~15ULL) - (offr & ~15ULL) > P.stage_bytes / 2 || ix - itr > P.tile_items);
+    const bool lone = in && (((nx + 15) & ~15ULL) - (offr & ~15ULL) > P.stage_bytes || ix - itr > P.tile_items);
     defer_blocks_wave(P, lone, b_begin + lane);
   }
   Group G = next_group(b_begin);
@@ -935,6 +940,20 @@ __global__ __launch_bounds__(kGroupWaves * kWave) __attribute__((amdgpu_waves_pe
         else phase_a(stage, meta, owner, rec, role * kWave, nA * kWave, total, P.tile_items, P.flags & kDiagHalfWalk);
         if (P.flags & kPrioA) __builtin_amdgcn_s_setprio(0);
         LSM_TICK(kTmA);
+      } else if (!(P.flags & kDiagSkipHash) && k <= kGroupWaves - nA) {
+        // few (large) blocks: one wave per block, the 64-lane XXH3 (1 KiB per step)
+        const uint32_t jb = role - nA;
+        if (jb < k && meta[jb].hdr_st == ST_OK) {
+          const uint32_t hb = meta[jb].hb, plen = meta[jb].len - kHdrLen;
+          uint64_t lo, hi;
+          xxh3_128_wave(stage, hb + kHdrLen, plen, ls, lo, hi);
+          const bool hck = header_cksum_ok(stage, hb);
+          if (lane == 0) {
+            meta[jb].ck_bad = lo != meta[jb].ck_lo || hi != meta[jb].ck_hi;
+            meta[jb].hck_bad = !hck;
+          }
+        }
+        LSM_TICK(kTmHash);
       } else if (!(P.flags & kDiagSkipHash)) {
         const uint32_t rows = (kGroupWaves - nA) * 4;
         for (uint32_t jb = (role - nA) * 4 + (lane >> 4); jb < k; jb += rows) {
