@@ -388,6 +388,20 @@ def bench_point_read(torch, lsmgpu, items, starts, enc, nb, n_items, n_queries=1
             "note": "lane per query straight from HBM (hash index off: restart binary search + MVCC scan)"}
 
 
+def bench_file_checksum(torch, lsmgpu, enc, total_bytes, reps=5):
+    """Whole-file xxh3_128 (ChecksummedWriter digest, src/checksum.rs:59-96) over
+    the encoded configs[1] batch taken as one file."""
+    lsmgpu.xxh3_128_file(enc["buf"], total_bytes)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        lsmgpu.xxh3_128_file(enc["buf"], total_bytes)  # (returns the digest: synchronises)
+    ms = (time.perf_counter() - t0) * 1e3 / reps
+    return {"bytes": total_bytes, "ms": round(ms, 4), "GiB_per_s": round(total_bytes / (ms * 1e-3) / 2 ** 30, 1),
+            "note": "per-KiB XXH3 contributions across the GPU, then one wave's scramble chain; "
+                    "host-timed incl. the 16-B digest copy"}
+
+
 def load_traffic(n_blocks):
     """HBM bytes of one decode_blocks_kernel launch over n_blocks, from the
     newest committed rocprofv3 PMC summary (profiles/traffic_*.json: FETCH_SIZE
@@ -518,6 +532,7 @@ def main():
     extra = {}
     if not args.no_extra:
         extra["point_read"] = bench_point_read(torch, lsmgpu, items, starts, enc, nb, n_items)
+        extra["file_checksum"] = bench_file_checksum(torch, lsmgpu, enc, total_bytes)
         if world == 1:
             extra["config4"] = bench_config4(torch, lsmgpu, max(3, args.steps // 4), rank)
         extra["config5"] = bench_config5(torch, lsmgpu, max(3, args.steps // 4), rank, world, dist, dev)

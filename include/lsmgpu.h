@@ -23,6 +23,7 @@
  *   lsm_cut_blocks     <- Writer::write chunking   src/table/writer/mod.rs:243-296
  *   lsm_xxh3_128_batch <- hash128                  src/hash.rs:7-9 (checksum of arbitrary byte ranges)
  *   lsm_point_read_blocks <- DataBlock::point_read src/table/data_block/mod.rs:412-472
+ *   lsm_xxh3_128_file  <- ChecksummedWriter         src/checksum.rs:59-96 (whole-file checksum)
  */
 #ifndef LSMGPU_H
 #define LSMGPU_H
@@ -197,6 +198,15 @@ uint64_t lsm_cut_blocks(const uint64_t* key_off, const uint64_t* val_off, uint64
  * d_data[d_off[i] .. d_off[i+1]) into d_out (2 u64 per range: low, high). */
 int lsm_xxh3_128_batch(const uint8_t* d_data, const uint64_t* d_off, uint32_t n, uint64_t* d_out,
                        void* stream);
+/* Whole-file checksum: xxh3_128 of d_data[0 .. len) into d_out[0] (low), d_out[1]
+ * (high), spread over the whole GPU (per-KiB contributions in parallel, then
+ * one wave runs the scramble chain).  Replaces ChecksummedWriter's streaming
+ * digest over an SST file (src/checksum.rs:59-96; equal to the one-shot
+ * xxh3_128, tests/table_full_file_checksum.rs:26-31).  d_data readable up to
+ * 16 bytes past len; workspace: lsm_xxh3_128_file_workspace_size(len) bytes. */
+size_t lsm_xxh3_128_file_workspace_size(uint64_t len);
+int lsm_xxh3_128_file(const uint8_t* d_data, uint64_t len, uint64_t* d_out, void* d_workspace,
+                      size_t workspace_bytes, void* stream);
 
 /* ---- point read -----------------------------------------------------------
  * Batched DataBlock::point_read(needle, snapshot_seqno) (data_block/mod.rs:412-472),

@@ -102,6 +102,10 @@ def lib():
         L.lsm_cut_blocks.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p, C.c_uint64]
         L.lsm_xxh3_128_batch.restype = C.c_int
         L.lsm_xxh3_128_batch.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p]
+        L.lsm_xxh3_128_file_workspace_size.restype = C.c_size_t
+        L.lsm_xxh3_128_file_workspace_size.argtypes = [C.c_uint64]
+        L.lsm_xxh3_128_file.restype = C.c_int
+        L.lsm_xxh3_128_file.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]
         L.lsm_point_read_blocks.restype = C.c_int
         L.lsm_point_read_blocks.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p,
                                             C.c_void_p, C.c_uint32, C.POINTER(LsmPointResult), C.c_void_p,
@@ -113,7 +117,7 @@ def lib():
 EXPORTED_SYMBOLS = ["lsm_abi_version", "lsm_status_name", "lsm_last_error", "lsm_device_count", "lsm_set_device",
                     "lsm_decode_workspace_size", "lsm_decode_blocks", "lsm_decode_blocks_tuned", "lsm_encode_bound",
                     "lsm_encode_workspace_size", "lsm_encode_blocks", "lsm_cut_blocks", "lsm_xxh3_128_batch",
-                    "lsm_point_read_blocks"]
+                    "lsm_point_read_blocks", "lsm_xxh3_128_file_workspace_size", "lsm_xxh3_128_file"]
 
 
 def _check(rc, what):
@@ -281,6 +285,19 @@ def point_read(blocks, block_off, n_blocks, query_block, needles, needle_off, sn
                                        _ptr(needle_off), _ptr(snapshot), n, C.byref(res), _ptr(out["status"]),
                                        _stream(stream)), "lsm_point_read_blocks")
     return out
+
+
+def xxh3_128_file(data, length=None, offset=0, stream=None):
+    """Whole-file xxh3_128 (ChecksummedWriter digest) of data[offset .. offset+length)
+    (uint8 cuda tensor, readable 16 B past the end) -> (low, high) as Python ints."""
+    torch = _torch()
+    length = data.numel() - offset if length is None else length
+    ws = torch.empty(max(lib().lsm_xxh3_128_file_workspace_size(length), 256), dtype=torch.uint8, device=data.device)
+    out = torch.zeros(2, dtype=torch.int64, device=data.device)
+    _check(lib().lsm_xxh3_128_file(C.c_void_p(data.data_ptr() + offset), length, _ptr(out), _ptr(ws), ws.numel(),
+                                   _stream(stream)), "lsm_xxh3_128_file")
+    lo, hi = (int(x) & (2 ** 64 - 1) for x in out.cpu().tolist())
+    return lo, hi
 
 
 def cut_blocks(key_off, val_off, block_size):
