@@ -15,6 +15,12 @@ checked bit-exactly against the oracle before timing.
 
 N > 1: one process per GPU (torch.distributed, RCCL), each rank decodes its own
 1 M-block shard (weak scaling, no data-path collective).
+
+Side legs in the same JSON line (not `value`): encode and the configs[2] round
+trip, configs[3] (prefix-heavy 16 KiB blocks, N = 1), configs[4] (8 GiB of
+mixed 4/16/64 KiB data + index blocks byte-split across the ranks: strong
+scaling), batched point reads, the whole-file checksum, the host-inclusive
+(PCIe) decode rate and the CPU baseline (oracle port on the host cores).
 """
 from __future__ import annotations
 
