@@ -84,6 +84,38 @@ __global__ __launch_bounds__(64) void xxh3_file_finish_kernel(const uint8_t* __r
   const uint64_t scr0 = ls->acc[16 + 2 * q], scr1 = ls->acc[16 + 2 * q + 1];
   const uint64_t nb = (len - 1) / 1024;
   uint64_t n = 0;
+  // The chain is one wave's dependent VALU work; feeding it straight from HBM
+  // stalls on load latency every few steps.  Instead the whole wave streams
+  // the contributions of kChunk KiB blocks (16 KiB) into registers one chunk
+  // ahead, parks them in LDS, and the chain reads LDS only.
+  constexpr uint32_t kChunk = 256;
+  __shared__ u32x4 stage[kChunk * 4];  // 64 B of contributions per KiB block
+  const uint64_t nchunks = nb / kChunk;
+  const u32x4* src = reinterpret_cast<const u32x4*>(contrib);
+  u32x4 r[16];
+  if (nchunks) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) r[i] = __builtin_nontemporal_load(&src[i * 64 + lane]);
+  }
+  for (uint64_t c = 0; c < nchunks; ++c) {
+#pragma unroll
+    for (int i = 0; i < 16; ++i) stage[i * 64 + lane] = r[i];
+    __syncthreads();
+    if (c + 1 < nchunks) {
+      const u32x4* nx = src + (c + 1) * kChunk * 4;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) r[i] = __builtin_nontemporal_load(&nx[i * 64 + lane]);
+    }
+    const uint64_t* st = reinterpret_cast<const uint64_t*>(stage);
+#pragma unroll 8
+    for (uint32_t u = 0; u < kChunk; ++u) {
+      const uint64_t c0 = st[8 * u + 2 * q], c1 = st[8 * u + 2 * q + 1];
+      a0 += c0; a0 ^= a0 >> 47; a0 ^= scr0; a0 *= P32_1;
+      a1 += c1; a1 ^= a1 >> 47; a1 ^= scr1; a1 *= P32_1;
+    }
+    __syncthreads();
+  }
+  n = nchunks * kChunk;
   for (; n + 4 <= nb; n += 4) {  // contributions of four KiB blocks in flight per step
     uint64_t c[8];
 #pragma unroll

@@ -12,7 +12,7 @@ import pyoracle
 pytestmark = pytest.mark.gpu
 
 SIZES = [0, 1, 3, 4, 8, 9, 16, 17, 128, 129, 240, 241, 1023, 1024, 1025, 1088, 2048, 4103, 65599,
-         1 << 20, (1 << 20) + 1, (3 << 20) + 333]
+         (256 << 10) + 1, (512 << 10) + 1, 1 << 20, (1 << 20) + 1, (3 << 20) + 333]
 
 
 def test_file_checksum_sizes(gpu):
