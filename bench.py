@@ -408,6 +408,40 @@ def bench_file_checksum(torch, lsmgpu, enc, total_bytes, reps=5):
                     "host-timed incl. the 16-B digest copy"}
 
 
+def bench_bloom(torch, lsmgpu, items, n_items, reps=5):
+    """Standard Bloom filter over the configs[1] batch's keys (FullFilterWriter,
+    src/table/writer/filter/full.rs:47-92, BitsPerKey(10) default): hash64 of every
+    key, filter build (k scattered atomicOr per key), then one probe per key.
+    Two sizes: one table's worth of keys (1 M, filter 1.25 MB, L2-resident) and
+    the whole batch as one filter (HBM-resident)."""
+    out = {}
+    for name, n in (("table_1M", min(1 << 20, n_items)), ("batch", n_items)):
+        ko = items["key_off"][:n + 1]
+        m, k = lsmgpu.bloom_shape(n, bpk=10.0)
+        h = lsmgpu.hash64_keys(items["keys"], ko)
+        filt = lsmgpu.bloom_build(h, m, k)
+        hit = lsmgpu.bloom_contains(filt, h)
+        torch.cuda.synchronize()
+        assert int((hit != 1).sum().item()) == 0, "bloom: false negative"
+        ev = [torch.cuda.Event(enable_timing=True) for _ in range(4)]
+        ev[0].record()
+        for _ in range(reps):
+            h = lsmgpu.hash64_keys(items["keys"], ko)
+        ev[1].record()
+        for _ in range(reps):
+            filt = lsmgpu.bloom_build(h, m, k)
+        ev[2].record()
+        for _ in range(reps):
+            hit = lsmgpu.bloom_contains(filt, h)
+        ev[3].record()
+        torch.cuda.synchronize()
+        t = [ev[i].elapsed_time(ev[i + 1]) / reps for i in range(3)]
+        out[name] = {"keys": n, "m_bits": m, "k": k, "hash64_ms": round(t[0], 4), "build_ms": round(t[1], 4),
+                     "probe_ms": round(t[2], 4), "Mkeys_per_s_build": round(n / (t[0] + t[1]) / 1e3, 1),
+                     "Mprobes_per_s": round(n / t[2] / 1e3, 1)}
+    return out
+
+
 def load_traffic(n_blocks):
     """HBM bytes of one decode_blocks_kernel launch over n_blocks, from the
     newest committed rocprofv3 PMC summary (profiles/traffic_*.json: FETCH_SIZE
@@ -539,6 +573,7 @@ def main():
     if not args.no_extra:
         extra["point_read"] = bench_point_read(torch, lsmgpu, items, starts, enc, nb, n_items)
         extra["file_checksum"] = bench_file_checksum(torch, lsmgpu, enc, total_bytes)
+        extra["bloom"] = bench_bloom(torch, lsmgpu, items, n_items)
         if world == 1:
             extra["config4"] = bench_config4(torch, lsmgpu, max(3, args.steps // 4), rank)
         extra["config5"] = bench_config5(torch, lsmgpu, max(3, args.steps // 4), rank, world, dist, dev)

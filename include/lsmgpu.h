@@ -24,6 +24,10 @@
  *   lsm_xxh3_128_batch <- hash128                  src/hash.rs:7-9 (checksum of arbitrary byte ranges)
  *   lsm_point_read_blocks <- DataBlock::point_read src/table/data_block/mod.rs:412-472
  *   lsm_xxh3_128_file  <- ChecksummedWriter         src/checksum.rs:59-96 (whole-file checksum)
+ *   lsm_bloom_shape    <- BloomConstructionPolicy::init  src/table/filter/mod.rs:25-34
+ *   lsm_hash64_keys    <- FullFilterWriter::register_key src/table/writer/filter/full.rs:47-50
+ *   lsm_bloom_build    <- standard_bloom Builder set_with_hash + build  builder.rs:33-53,154-170
+ *   lsm_bloom_contains <- StandardBloomFilterReader::contains_hash  standard_bloom/mod.rs:100-120
  */
 #ifndef LSMGPU_H
 #define LSMGPU_H
@@ -222,6 +226,39 @@ int lsm_point_read_blocks(const uint8_t* d_blocks, const uint64_t* d_block_off, 
                           const uint32_t* d_query_block, const uint8_t* d_needles,
                           const uint64_t* d_needle_off, const uint64_t* d_snapshot, uint32_t n_queries,
                           const lsm_point_result* d_out, int32_t* d_status, void* stream);
+
+/* ---- standard Bloom filter (src/table/filter/standard_bloom/) ---------------
+ * The filter is the exact byte image of Builder::build (builder.rs:33-53):
+ * "LSM\x03", filter type 0 (StandardBloom), hash type 0, m u64 LE, k u64 LE,
+ * then m/8 bit bytes (bit i = byte i/8, mask 0x80 >> i%8,
+ * bit_array/builder.rs:8-11).  Double hashing: h2 = (h1 >> 32) * 0x517cc1b727220a95,
+ * position i = h1 % m, h1 += h2, h2 *= i for i = 1..k (builder.rs:10-13,154-170). */
+enum { LSM_BLOOM_BITS_PER_KEY = 0, LSM_BLOOM_FP_RATE = 1 }; /* BloomConstructionPolicy */
+#define LSM_BLOOM_HEADER 22
+#define LSM_BLOOM_MAX_K 65536         /* larger k is rejected (bounded device loops) */
+#define LSM_BLOOM_BAD_FILTER 0xFF     /* lsm_bloom_contains output: InvalidHeader("BloomFilter") */
+/* Builder::calculate_m (builder.rs:128-151), f32 arithmetic as in the reference. */
+uint64_t lsm_bloom_calculate_m(uint64_t n, float fpr);
+/* (m, k) of BloomConstructionPolicy::{BitsPerKey(value), FalsePositiveRate(value)}.init(n)
+ * (filter/mod.rs:25-34; with_bpk builder.rs:91-126, with_fp_rate :58-85).
+ * LSM_BAD_ARG where the reference asserts (n == 0, bpk <= 0). */
+int lsm_bloom_shape(uint64_t n, int policy, float value, uint64_t* m, uint64_t* k);
+/* Byte length of the filter image: LSM_BLOOM_HEADER + m/8. */
+uint64_t lsm_bloom_filter_size(uint64_t m);
+/* hash64 = xxh3_64 (src/hash.rs:2-4) of n keys d_keys[d_key_off[i] .. d_key_off[i+1])
+ * into d_out[i] (the FullFilterWriter hash buffer, writer/filter/full.rs:47-50).
+ * d_keys 16-byte aligned and readable LSM_INPUT_PADDING bytes past its end. */
+int lsm_hash64_keys(const uint8_t* d_keys, const uint64_t* d_key_off, uint64_t n, uint64_t* d_out, void* stream);
+/* Builds the filter image of n hashes into d_filter (4-byte aligned, filter_cap >=
+ * lsm_bloom_filter_size(m) rounded up to 4; the bytes past the image are zeroed).
+ * m must be a positive multiple of 8 (both policies produce a multiple of 8; BitsPerKey < 1
+ * gives m = 0, where the reference panics in h1 % m), 1 <= k <= LSM_BLOOM_MAX_K. */
+int lsm_bloom_build(const uint64_t* d_hashes, uint64_t n, uint64_t m, uint64_t k, uint8_t* d_filter,
+                    uint64_t filter_cap, void* stream);
+/* d_out[i] = 1 if hash i may be contained, 0 if not (no false negatives),
+ * LSM_BLOOM_BAD_FILTER if the image's header is malformed or truncated. */
+int lsm_bloom_contains(const uint8_t* d_filter, uint64_t filter_len, const uint64_t* d_hashes, uint64_t n,
+                       uint8_t* d_out, void* stream);
 
 #ifdef __cplusplus
 }

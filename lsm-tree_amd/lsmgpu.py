@@ -110,6 +110,19 @@ def lib():
         L.lsm_point_read_blocks.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p,
                                             C.c_void_p, C.c_uint32, C.POINTER(LsmPointResult), C.c_void_p,
                                             C.c_void_p]
+        L.lsm_bloom_calculate_m.restype = C.c_uint64
+        L.lsm_bloom_calculate_m.argtypes = [C.c_uint64, C.c_float]
+        L.lsm_bloom_shape.restype = C.c_int
+        L.lsm_bloom_shape.argtypes = [C.c_uint64, C.c_int, C.c_float, C.POINTER(C.c_uint64), C.POINTER(C.c_uint64)]
+        L.lsm_bloom_filter_size.restype = C.c_uint64
+        L.lsm_bloom_filter_size.argtypes = [C.c_uint64]
+        L.lsm_hash64_keys.restype = C.c_int
+        L.lsm_hash64_keys.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p]
+        L.lsm_bloom_build.restype = C.c_int
+        L.lsm_bloom_build.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint64, C.c_void_p, C.c_uint64,
+                                      C.c_void_p]
+        L.lsm_bloom_contains.restype = C.c_int
+        L.lsm_bloom_contains.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p]
         _lib = L
     return _lib
 
@@ -117,7 +130,9 @@ def lib():
 EXPORTED_SYMBOLS = ["lsm_abi_version", "lsm_status_name", "lsm_last_error", "lsm_device_count", "lsm_set_device",
                     "lsm_decode_workspace_size", "lsm_decode_blocks", "lsm_decode_blocks_tuned", "lsm_encode_bound",
                     "lsm_encode_workspace_size", "lsm_encode_blocks", "lsm_cut_blocks", "lsm_xxh3_128_batch",
-                    "lsm_point_read_blocks", "lsm_xxh3_128_file_workspace_size", "lsm_xxh3_128_file"]
+                    "lsm_point_read_blocks", "lsm_xxh3_128_file_workspace_size", "lsm_xxh3_128_file",
+                    "lsm_bloom_calculate_m", "lsm_bloom_shape", "lsm_bloom_filter_size", "lsm_hash64_keys",
+                    "lsm_bloom_build", "lsm_bloom_contains"]
 
 
 def _check(rc, what):
@@ -298,6 +313,48 @@ def xxh3_128_file(data, length=None, offset=0, stream=None):
                                    _stream(stream)), "lsm_xxh3_128_file")
     lo, hi = (int(x) & (2 ** 64 - 1) for x in out.cpu().tolist())
     return lo, hi
+
+
+BLOOM_BITS_PER_KEY, BLOOM_FP_RATE, BLOOM_BAD_FILTER = 0, 1, 0xFF
+
+
+def bloom_shape(n, bpk=None, fpr=None):
+    """BloomConstructionPolicy::{BitsPerKey, FalsePositiveRate}.init(n) -> (m, k)
+    (src/table/filter/mod.rs:25-34).  Host-only."""
+    m, k = C.c_uint64(), C.c_uint64()
+    policy, value = (BLOOM_BITS_PER_KEY, bpk) if bpk is not None else (BLOOM_FP_RATE, fpr)
+    _check(lib().lsm_bloom_shape(n, policy, value, C.byref(m), C.byref(k)), "lsm_bloom_shape")
+    return m.value, k.value
+
+
+def hash64_keys(keys, key_off, n=None, stream=None):
+    """xxh3_64 of each key (FullFilterWriter::register_key, writer/filter/full.rs:47-50):
+    keys = padded uint8 cuda tensor, key_off = int64 cuda tensor [n+1] -> int64 cuda [n]."""
+    torch = _torch()
+    n = key_off.numel() - 1 if n is None else n
+    out = torch.empty(max(n, 1), dtype=torch.int64, device=keys.device)
+    _check(lib().lsm_hash64_keys(_ptr(keys), _ptr(key_off), n, _ptr(out), _stream(stream)), "lsm_hash64_keys")
+    return out[:n]
+
+
+def bloom_build(hashes, m, k, stream=None):
+    """Standard Bloom filter image (Builder::set_with_hash + build, standard_bloom/builder.rs)
+    of int64 cuda hashes -> uint8 cuda tensor of lsm_bloom_filter_size(m) bytes."""
+    torch = _torch()
+    size = lib().lsm_bloom_filter_size(m)
+    buf = torch.empty((size + 3) // 4 * 4, dtype=torch.uint8, device=hashes.device)
+    _check(lib().lsm_bloom_build(_ptr(hashes), hashes.numel(), m, k, _ptr(buf), buf.numel(), _stream(stream)),
+           "lsm_bloom_build")
+    return buf[:size]
+
+
+def bloom_contains(filt, hashes, stream=None):
+    """contains_hash per hash (standard_bloom/mod.rs:100-120) -> uint8 cuda [n]: 1, 0 or BLOOM_BAD_FILTER."""
+    torch = _torch()
+    out = torch.empty(max(hashes.numel(), 1), dtype=torch.uint8, device=hashes.device)
+    _check(lib().lsm_bloom_contains(_ptr(filt), filt.numel(), _ptr(hashes), hashes.numel(), _ptr(out),
+                                    _stream(stream)), "lsm_bloom_contains")
+    return out[:hashes.numel()]
 
 
 def cut_blocks(key_off, val_off, block_size):

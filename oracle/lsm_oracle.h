@@ -148,6 +148,14 @@ int orc_decode_blocks(const uint8_t* blocks, const uint64_t* block_off, uint32_t
 uint64_t orc_decode_materialize_blocks(const uint8_t* blocks, const uint64_t* block_off,
                                        uint32_t n_blocks, int nthreads, uint64_t* fold);
 
+/* ---- standard Bloom filter (bloom.c; src/table/filter/standard_bloom/) ---- */
+#define ORC_BLOOM_HDR 22 /* magic 4 + filter type 1 + hash type 1 + m u64 + k u64 */
+uint64_t orc_bloom_calculate_m(uint64_t n, float fpr);
+int orc_bloom_shape_fpr(uint64_t n, float fpr, uint64_t* m, uint64_t* k);
+int orc_bloom_shape_bpk(uint64_t n, float bpk, uint64_t* m, uint64_t* k);
+void orc_bloom_build(const uint64_t* hashes, uint64_t n, uint64_t m, uint64_t k, uint8_t* out);
+int orc_bloom_contains(const uint8_t* filter, uint64_t len, uint64_t h1);
+
 #ifdef __cplusplus
 }
 #endif

@@ -87,6 +87,15 @@ def lib():
                                         C.c_uint64, C.c_void_p, C.c_void_p, C.c_int]
         L.orc_decode_materialize_blocks.restype = C.c_uint64
         L.orc_decode_materialize_blocks.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_int, u64p]
+        L.orc_bloom_calculate_m.restype = C.c_uint64
+        L.orc_bloom_calculate_m.argtypes = [C.c_uint64, C.c_float]
+        for f in (L.orc_bloom_shape_fpr, L.orc_bloom_shape_bpk):
+            f.restype = C.c_int
+            f.argtypes = [C.c_uint64, C.c_float, u64p, u64p]
+        L.orc_bloom_build.restype = None
+        L.orc_bloom_build.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint64, C.c_void_p]
+        L.orc_bloom_contains.restype = C.c_int
+        L.orc_bloom_contains.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64]
         _lib = L
     return _lib
 
@@ -107,6 +116,38 @@ def xxh3_128(b: bytes) -> int:
     lo, hi = C.c_uint64(), C.c_uint64()
     lib().orc_xxh3_128(_ptr(a), len(b), C.byref(lo), C.byref(hi))
     return (hi.value << 64) | lo.value
+
+
+BLOOM_HDR = 22
+
+
+def bloom_calculate_m(n: int, fpr: float) -> int:
+    """Builder::calculate_m (src/table/filter/standard_bloom/builder.rs:128-151)."""
+    return lib().orc_bloom_calculate_m(n, fpr)
+
+
+def bloom_shape(n: int, bpk: float | None = None, fpr: float | None = None):
+    """BloomConstructionPolicy::init (src/table/filter/mod.rs:25-34) -> (m, k)."""
+    m, k = C.c_uint64(), C.c_uint64()
+    f = lib().orc_bloom_shape_bpk if bpk is not None else lib().orc_bloom_shape_fpr
+    rc = f(n, bpk if bpk is not None else fpr, C.byref(m), C.byref(k))
+    if rc:
+        raise ValueError("bloom shape: n must be > 0 (and bpk > 0)")
+    return m.value, k.value
+
+
+def bloom_build(hashes: np.ndarray, m: int, k: int) -> bytes:
+    """set_with_hash for every hash, then Builder::build (builder.rs:33-53,154-170)."""
+    h = np.ascontiguousarray(hashes, dtype=np.uint64)
+    out = np.zeros(BLOOM_HDR + m // 8, np.uint8)
+    lib().orc_bloom_build(_ptr(h) if len(h) else None, len(h), m, k, _ptr(out))
+    return out.tobytes()
+
+
+def bloom_contains(filt: bytes, h: int) -> int:
+    """StandardBloomFilterReader::contains_hash (standard_bloom/mod.rs:100-120)."""
+    a = np.frombuffer(filt, np.uint8)
+    return lib().orc_bloom_contains(_ptr(a), len(filt), h)
 
 
 class Items:

@@ -123,3 +123,18 @@ def test_bench_workload_cut_rules(L):
         bench.check_cut_rule(L, ipb, kl, vl, bs)
     for bs, ipb, kind, est in bench.C5_SEGMENTS:
         bench.check_cut_rule(L, ipb, 16, 64, bs)
+
+
+@pytest.mark.parametrize("n,kw", [(1000, {"fpr": 0.01}), (1000, {"fpr": 0.1}), (1_000_000, {"fpr": 0.1}),
+                                  (10, {"fpr": 0.0001}), (10, {"fpr": 0.0}), (1_000_000, {"bpk": 10.0}),
+                                  (3, {"bpk": 5.0}), (7, {"bpk": 0.5}), (100_000, {"fpr": 0.5})])
+def test_bloom_shape_matches_oracle(L, oracle, n, kw):
+    assert L.bloom_shape(n, **kw) == oracle.bloom_shape(n, **kw)
+
+
+def test_bloom_calculate_m_kats(L):
+    lib = L.lib()  # standard_bloom/builder.rs:173-187
+    assert [lib.lsm_bloom_calculate_m(1000, 0.01), lib.lsm_bloom_calculate_m(1000, 0.1),
+            lib.lsm_bloom_calculate_m(1_000_000, 0.1)] == [9_592, 4_800, 4_792_536]
+    with pytest.raises(L.LsmError):
+        L.bloom_shape(0, bpk=10.0)
