@@ -24,6 +24,7 @@
  *   lsm_xxh3_128_batch <- hash128                  src/hash.rs:7-9 (checksum of arbitrary byte ranges)
  *   lsm_point_read_blocks <- DataBlock::point_read src/table/data_block/mod.rs:412-472
  *   lsm_xxh3_128_file  <- ChecksummedWriter         src/checksum.rs:59-96 (whole-file checksum)
+ *   lsm_lz4_decompress_blocks <- Block::from_reader/from_file, CompressionType::Lz4  block/mod.rs:87-182
  *   lsm_bloom_shape    <- BloomConstructionPolicy::init  src/table/filter/mod.rs:25-34
  *   lsm_hash64_keys    <- FullFilterWriter::register_key src/table/writer/filter/full.rs:47-50
  *   lsm_bloom_build    <- standard_bloom Builder set_with_hash + build  builder.rs:33-53,154-170
@@ -59,7 +60,8 @@ typedef enum lsm_status {
     LSM_TRUNCATED = 8,     /* handle shorter than header / data_length mismatch (Error::Io) */
     LSM_UNSUPPORTED = 9,   /* compression != None, filter block parse */
     LSM_BAD_ARG = 10,
-    LSM_HIP_ERROR = 11
+    LSM_HIP_ERROR = 11,
+    LSM_DECOMPRESS = 12    /* Error::Decompress(Lz4): malformed LZ4 block   block/mod.rs:113-114 */
 } lsm_status;
 
 /* BlockType codes, src/table/block/type.rs:13-22 */
@@ -259,6 +261,22 @@ int lsm_bloom_build(const uint64_t* d_hashes, uint64_t n, uint64_t m, uint64_t k
  * LSM_BLOOM_BAD_FILTER if the image's header is malformed or truncated. */
 int lsm_bloom_contains(const uint8_t* d_filter, uint64_t filter_len, const uint64_t* d_hashes, uint64_t n,
                        uint8_t* d_out, void* stream);
+
+/* ---- LZ4 block decompression ----------------------------------------------
+ * Block::from_reader / from_file with CompressionType::Lz4 (block/mod.rs:87-182),
+ * batched: on-disk blocks d_blocks[d_block_off[b] .. d_block_off[b+1]) (header +
+ * LZ4-compressed payload; same buffer rules as lsm_decode_blocks) are checked
+ * (magic, type, header checksum, data_length, xxh3_128 of the stored payload) and
+ * decompressed (lz4_flex::decompress_into, LZ4 block format) into
+ * d_out[d_out_off[b] .. d_out_off[b+1]), whose length must be the header's
+ * uncompressed_length (else LSM_OVERFLOW).  d_status[b]: LSM_OK, a header/checksum
+ * status as in lsm_decode_blocks, or LSM_DECOMPRESS (malformed LZ4 stream, or one
+ * that does not decode to exactly uncompressed_length bytes).
+ * Workspace: lsm_lz4_workspace_size(n_blocks) bytes. */
+size_t lsm_lz4_workspace_size(uint32_t n_blocks);
+int lsm_lz4_decompress_blocks(const uint8_t* d_blocks, const uint64_t* d_block_off, uint32_t n_blocks,
+                              uint8_t* d_out, const uint64_t* d_out_off, int32_t* d_status,
+                              void* d_workspace, size_t workspace_bytes, void* stream);
 
 #ifdef __cplusplus
 }

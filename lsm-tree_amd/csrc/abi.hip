@@ -46,6 +46,7 @@ const char* lsm_status_name(int s) {
     case LSM_UNSUPPORTED: return "UNSUPPORTED";
     case LSM_BAD_ARG: return "BAD_ARG";
     case LSM_HIP_ERROR: return "HIP_ERROR";
+    case LSM_DECOMPRESS: return "DECOMPRESS";
     default: return "UNKNOWN";
   }
 }

@@ -1,0 +1,243 @@
+// lz4.hip — Block::from_reader / from_file for CompressionType::Lz4
+// (src/table/block/mod.rs:87-128, :131-182): header checks, xxh3_128 verify of
+// the stored (compressed) payload, then lz4_flex::decompress_into of the LZ4
+// block format into header.uncompressed_length bytes (mod.rs:104-118).
+//
+// LZ4 decode is a serial chain of sequences, so the unit of parallelism is the
+// block: one wave per block.  The wave stages the compressed payload into its
+// own LDS slice (coalesced dword loads), every lane walks the token stream
+// redundantly from LDS (wave-uniform control flow, broadcast reads), and the
+// literal and match copies are spread over the 64 lanes inside an LDS output
+// slice (a match with offset < 64 is copied in offset-sized rounds, so every
+// source byte is already written).  The decoded block is then stored to HBM.
+//   lz4_small_kernel  4 waves/workgroup, 8 KiB in + 8 KiB out per wave (the
+//                     4 KiB data-block class; 8 waves per CU).
+//   lz4_large_kernel  1 wave/workgroup, 72 KiB in + 80 KiB out (16/64 KiB
+//                     blocks); anything larger is decoded by lane 0 straight
+//                     in HBM (rare: only oversize blocks).
+#include <hip/hip_runtime.h>
+
+#include "block_format.hpp"
+#include "device_common.hpp"
+#include "lsmgpu.h"
+
+namespace lsmgpu {
+
+constexpr int32_t kLz4Deferred = -1;  // small kernel -> large kernel hand-off
+
+// Wave-uniform LZ4 block decode from an LDS input slice into an LDS output
+// slice; returns the number of bytes written or -1 (Error::Decompress).
+__device__ __forceinline__ int64_t lz4_wave_decode(const uint8_t* in, uint32_t n, uint8_t* out, uint32_t cap, int lane) {
+  uint32_t ip = 0, op = 0;
+  if (n == 0) return -1;
+  for (;;) {
+    if (ip >= n) return -1;
+    const uint32_t token = in[ip++];
+    uint32_t lit = token >> 4;
+    if (lit == 15) {
+      uint32_t b;
+      do {
+        if (ip >= n) return -1;
+        b = in[ip++];
+        lit += b;
+      } while (b == 255);
+    }
+    if (lit > n - ip || lit > cap - op) return -1;
+    for (uint32_t j = lane; j < lit; j += 64) out[op + j] = in[ip + j];
+    ip += lit;
+    op += lit;
+    if (ip == n) return op;
+    if (n - ip < 2) return -1;
+    const uint32_t off = (uint32_t)in[ip] | ((uint32_t)in[ip + 1] << 8);
+    ip += 2;
+    if (off == 0 || off > op) return -1;
+    uint32_t ml = (token & 15u) + 4;
+    if ((token & 15u) == 15) {
+      uint32_t b;
+      do {
+        if (ip >= n) return -1;
+        b = in[ip++];
+        ml += b;
+      } while (b == 255);
+    }
+    if (ml > cap - op) return -1;
+    const uint32_t step = off < 64 ? off : 64;
+    for (uint32_t c = 0; c < ml; c += step) {
+      __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");  // previous round's bytes before this round's reads
+      const uint32_t j = c + lane;
+      if (lane < step && j < ml) out[op + j] = out[op + j - off];
+    }
+    __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+    op += ml;
+  }
+}
+
+// Serial fallback for blocks larger than the LDS stages: lane 0, in HBM.
+__device__ int64_t lz4_serial_decode(const uint8_t* in, uint64_t n, uint8_t* out, uint64_t cap) {
+  uint64_t ip = 0, op = 0;
+  if (n == 0) return -1;
+  for (;;) {
+    if (ip >= n) return -1;
+    const uint32_t token = in[ip++];
+    uint64_t lit = token >> 4;
+    if (lit == 15) {
+      uint32_t b;
+      do {
+        if (ip >= n) return -1;
+        b = in[ip++];
+        lit += b;
+      } while (b == 255);
+    }
+    if (lit > n - ip || lit > cap - op) return -1;
+    for (uint64_t j = 0; j < lit; ++j) out[op + j] = in[ip + j];
+    ip += lit;
+    op += lit;
+    if (ip == n) return (int64_t)op;
+    if (n - ip < 2) return -1;
+    const uint64_t off = (uint64_t)in[ip] | ((uint64_t)in[ip + 1] << 8);
+    ip += 2;
+    if (off == 0 || off > op) return -1;
+    uint64_t ml = (token & 15u) + 4;
+    if ((token & 15u) == 15) {
+      uint32_t b;
+      do {
+        if (ip >= n) return -1;
+        b = in[ip++];
+        ml += b;
+      } while (b == 255);
+    }
+    if (ml > cap - op) return -1;
+    for (uint64_t j = 0; j < ml; ++j) out[op + j] = out[op + j - off];
+    op += ml;
+  }
+}
+
+struct Lz4Block {
+  const uint8_t* base;  // 16-aligned
+  uint32_t hb;          // header position in base
+  uint32_t data_len;
+  uint32_t raw_len;
+  uint8_t* dst;
+};
+
+// Header + payload checksum (Block::from_reader, mod.rs:92-102); wave-uniform.
+__device__ __forceinline__ int32_t lz4_check_block(const uint8_t* blocks, const uint64_t* block_off, const uint64_t* out_off,
+                                   uint8_t* out, uint32_t i, Lz4Block& b) {
+  const uint64_t o = block_off[i], e = block_off[i + 1];
+  b.base = blocks + (o & ~15ULL);
+  b.hb = (uint32_t)(o & 15);
+  HeaderInfo h;
+  int32_t st = check_header(b.base, b.hb, e - o, h);
+  if (st != ST_OK) return st;
+  if ((uint64_t)h.data_length != e - o - kHdrLen) return ST_TRUNCATED;
+  b.data_len = h.data_length;
+  b.raw_len = read_u32_unaligned(b.base, b.hb + 25);  // uncompressed_length, header.rs:101
+  if ((uint64_t)b.raw_len != out_off[i + 1] - out_off[i]) return ST_OVERFLOW;
+  uint64_t lo, hi;
+  xxh3_128_wave(b.base, b.hb + kHdrLen, b.data_len, &kLongSecret, lo, hi);
+  if (lo != h.ck_lo || hi != h.ck_hi) return ST_CKSUM;
+  b.dst = out + out_off[i];
+  return ST_OK;
+}
+
+template <uint32_t kIn, uint32_t kOut>
+__device__ __forceinline__ int32_t lz4_stage_and_decode(const Lz4Block& b, uint32_t* lin, uint8_t* lout, int lane) {
+  // coalesced dword window [a0, a0 + 4*words) covering the payload
+  const uint32_t p0 = b.hb + kHdrLen, a0 = p0 & ~3u, sh = p0 - a0;
+  const uint32_t words = (sh + b.data_len + 3) / 4;
+  const uint32_t* src = reinterpret_cast<const uint32_t*>(b.base + a0);
+  for (uint32_t w = lane; w < words; w += 64) lin[w] = src[w];
+  __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+  const int64_t got = lz4_wave_decode(reinterpret_cast<const uint8_t*>(lin) + sh, b.data_len, lout, kOut, lane);
+  if (got != (int64_t)b.raw_len) return LSM_DECOMPRESS;
+  for (uint32_t j = lane; j < b.raw_len; j += 64) b.dst[j] = lout[j];
+  return ST_OK;
+}
+
+constexpr uint32_t kSmallIn = 8192, kSmallOut = 8192;
+constexpr uint32_t kLargeIn = 72 * 1024, kLargeOut = 80 * 1024;
+
+__global__ __launch_bounds__(256) void lz4_small_kernel(const uint8_t* __restrict__ blocks,
+                                                        const uint64_t* __restrict__ block_off, uint32_t n,
+                                                        uint8_t* __restrict__ out, const uint64_t* __restrict__ out_off,
+                                                        int32_t* __restrict__ status) {
+  __shared__ uint32_t s_in[4][kSmallIn / 4];
+  __shared__ uint8_t s_out[4][kSmallOut];
+  const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
+  const uint32_t i = blockIdx.x * 4 + wv;
+  if (i >= n) return;
+  Lz4Block b;
+  int32_t st = lz4_check_block(blocks, block_off, out_off, out, i, b);
+  if (st == ST_OK) {
+    const uint32_t sh = (b.hb + kHdrLen) & 3u;
+    if (b.data_len + sh + 4 > kSmallIn || b.raw_len > kSmallOut)
+      st = kLz4Deferred;
+    else
+      st = lz4_stage_and_decode<kSmallIn, kSmallOut>(b, s_in[wv], s_out[wv], lane);
+  }
+  if (lane == 0) status[i] = st;
+}
+
+__global__ __launch_bounds__(64) void lz4_large_kernel(const uint8_t* __restrict__ blocks,
+                                                       const uint64_t* __restrict__ block_off, uint32_t n,
+                                                       uint8_t* __restrict__ out, const uint64_t* __restrict__ out_off,
+                                                       int32_t* __restrict__ status, const uint32_t* __restrict__ list,
+                                                       const uint32_t* __restrict__ count) {
+  extern __shared__ uint32_t s_dyn[];
+  const int lane = threadIdx.x;
+  const uint32_t total = *count;
+  for (uint32_t li = blockIdx.x; li < total; li += gridDim.x) {
+    const uint32_t i = list[li];
+    Lz4Block b;
+    int32_t st = lz4_check_block(blocks, block_off, out_off, out, i, b);
+    if (st == ST_OK) {
+      const uint32_t sh = (b.hb + kHdrLen) & 3u;
+      if (b.data_len + sh + 4 <= kLargeIn && b.raw_len <= kLargeOut) {
+        st = lz4_stage_and_decode<kLargeIn, kLargeOut>(b, s_dyn, reinterpret_cast<uint8_t*>(s_dyn + kLargeIn / 4), lane);
+      } else {
+        int64_t got = 0;
+        if (lane == 0) got = lz4_serial_decode(b.base + b.hb + kHdrLen, b.data_len, b.dst, b.raw_len);
+        got = __shfl(got, 0);
+        st = got == (int64_t)b.raw_len ? ST_OK : LSM_DECOMPRESS;
+      }
+    }
+    if (lane == 0) status[i] = st;
+  }
+}
+
+__global__ __launch_bounds__(256) void lz4_collect_deferred(int32_t* __restrict__ status, uint32_t n,
+                                                            uint32_t* __restrict__ list, uint32_t* __restrict__ count) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i < n && status[i] == kLz4Deferred) list[atomicAdd(count, 1u)] = i;
+}
+
+}  // namespace lsmgpu
+
+using namespace lsmgpu;
+
+extern "C" size_t lsm_lz4_workspace_size(uint32_t n_blocks) { return 16 + (size_t)n_blocks * 4; }
+
+extern "C" int lsm_lz4_decompress_blocks(const uint8_t* d_blocks, const uint64_t* d_block_off, uint32_t n_blocks,
+                                         uint8_t* d_out, const uint64_t* d_out_off, int32_t* d_status,
+                                         void* d_workspace, size_t workspace_bytes, void* stream) {
+  if (n_blocks == 0) return LSM_OK;
+  if (!d_blocks || !d_block_off || !d_out || !d_out_off || !d_status || !d_workspace ||
+      ((uintptr_t)d_blocks & 15) || workspace_bytes < lsm_lz4_workspace_size(n_blocks))
+    return LSM_BAD_ARG;
+  const hipStream_t st = (hipStream_t)stream;
+  uint32_t* count = (uint32_t*)d_workspace;
+  uint32_t* list = count + 4;
+  if (hipMemsetAsync(count, 0, 4, st) != hipSuccess) return LSM_HIP_ERROR;
+  hipLaunchKernelGGL(lz4_small_kernel, dim3((n_blocks + 3) / 4), dim3(256), 0, st, d_blocks, d_block_off, n_blocks,
+                     d_out, d_out_off, d_status);
+  hipLaunchKernelGGL(lz4_collect_deferred, dim3((n_blocks + 255) / 256), dim3(256), 0, st, d_status, n_blocks, list,
+                     count);
+  static const hipError_t attr = hipFuncSetAttribute((const void*)lz4_large_kernel,
+                                                     hipFuncAttributeMaxDynamicSharedMemorySize,
+                                                     (int)(kLargeIn + kLargeOut));
+  if (attr != hipSuccess) return LSM_HIP_ERROR;
+  const uint32_t grid = n_blocks < 1024 ? n_blocks : 1024;
+  hipLaunchKernelGGL(lz4_large_kernel, dim3(grid), dim3(64), kLargeIn + kLargeOut, st, d_blocks, d_block_off,
+                     n_blocks, d_out, d_out_off, d_status, list, count);
+  return hipGetLastError() == hipSuccess ? LSM_OK : LSM_HIP_ERROR;
+}

@@ -19,7 +19,8 @@ LSM_TRAILER_LEN = 31
 LSM_INPUT_PADDING = 64
 
 STATUS = {0: "OK", 1: "BAD_MAGIC", 2: "BAD_TYPE", 3: "HDR_CKSUM", 4: "CKSUM", 5: "PARSE", 6: "OVERFLOW",
-          7: "TYPE_MISMATCH", 8: "TRUNCATED", 9: "UNSUPPORTED", 10: "BAD_ARG", 11: "HIP_ERROR"}
+          7: "TYPE_MISMATCH", 8: "TRUNCATED", 9: "UNSUPPORTED", 10: "BAD_ARG", 11: "HIP_ERROR",
+          12: "DECOMPRESS"}
 BLOCK_DATA, BLOCK_INDEX, BLOCK_FILTER, BLOCK_META = 0, 1, 2, 3
 
 
@@ -123,6 +124,11 @@ def lib():
                                       C.c_void_p]
         L.lsm_bloom_contains.restype = C.c_int
         L.lsm_bloom_contains.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p]
+        L.lsm_lz4_workspace_size.restype = C.c_size_t
+        L.lsm_lz4_workspace_size.argtypes = [C.c_uint32]
+        L.lsm_lz4_decompress_blocks.restype = C.c_int
+        L.lsm_lz4_decompress_blocks.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p,
+                                                C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]
         _lib = L
     return _lib
 
@@ -132,7 +138,7 @@ EXPORTED_SYMBOLS = ["lsm_abi_version", "lsm_status_name", "lsm_last_error", "lsm
                     "lsm_encode_workspace_size", "lsm_encode_blocks", "lsm_cut_blocks", "lsm_xxh3_128_batch",
                     "lsm_point_read_blocks", "lsm_xxh3_128_file_workspace_size", "lsm_xxh3_128_file",
                     "lsm_bloom_calculate_m", "lsm_bloom_shape", "lsm_bloom_filter_size", "lsm_hash64_keys",
-                    "lsm_bloom_build", "lsm_bloom_contains"]
+                    "lsm_bloom_build", "lsm_bloom_contains", "lsm_lz4_workspace_size", "lsm_lz4_decompress_blocks"]
 
 
 def _check(rc, what):
@@ -355,6 +361,29 @@ def bloom_contains(filt, hashes, stream=None):
     _check(lib().lsm_bloom_contains(_ptr(filt), filt.numel(), _ptr(hashes), hashes.numel(), _ptr(out),
                                     _stream(stream)), "lsm_bloom_contains")
     return out[:hashes.numel()]
+
+
+def lz4_decompress_blocks(blocks, block_off, n_blocks=None, stream=None):
+    """Block::from_reader with CompressionType::Lz4 over a batch (block/mod.rs:87-128):
+    blocks = padded uint8 cuda tensor of on-disk blocks, block_off = int64 cuda [n+1].
+    Output sizes come from each header's uncompressed_length (bytes 25..28).
+    Returns (out uint8 cuda, out_off int64 cuda [n+1], status int32 cuda [n])."""
+    torch = _torch()
+    n = block_off.numel() - 1 if n_blocks is None else n_blocks
+    dev = blocks.device
+    hdr = block_off[:n].unsqueeze(1) + torch.arange(25, 29, device=dev)
+    raw = blocks[hdr].to(torch.int64)
+    raw_len = raw[:, 0] | (raw[:, 1] << 8) | (raw[:, 2] << 16) | (raw[:, 3] << 24)
+    out_off = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    out_off[1:] = torch.cumsum(raw_len, 0)
+    total = int(out_off[-1].item()) if n else 0
+    out = torch.empty(max(total, 1), dtype=torch.uint8, device=dev)
+    status = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+    ws = torch.empty(lib().lsm_lz4_workspace_size(n), dtype=torch.uint8, device=dev)
+    _check(lib().lsm_lz4_decompress_blocks(_ptr(blocks), _ptr(block_off), n, _ptr(out), _ptr(out_off),
+                                           _ptr(status), _ptr(ws), ws.numel(), _stream(stream)),
+           "lsm_lz4_decompress_blocks")
+    return out, out_off, status[:n]
 
 
 def cut_blocks(key_off, val_off, block_size):

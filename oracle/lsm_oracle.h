@@ -156,6 +156,9 @@ int orc_bloom_shape_bpk(uint64_t n, float bpk, uint64_t* m, uint64_t* k);
 void orc_bloom_build(const uint64_t* hashes, uint64_t n, uint64_t m, uint64_t k, uint8_t* out);
 int orc_bloom_contains(const uint8_t* filter, uint64_t len, uint64_t h1);
 
+/* ---- LZ4 block format decoder (lz4.c; lz4_flex::decompress_into, block/mod.rs:104-118) ---- */
+int64_t orc_lz4_decompress(const uint8_t* src, uint64_t n, uint8_t* dst, uint64_t cap);
+
 #ifdef __cplusplus
 }
 #endif

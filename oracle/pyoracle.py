@@ -96,6 +96,8 @@ def lib():
         L.orc_bloom_build.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint64, C.c_void_p]
         L.orc_bloom_contains.restype = C.c_int
         L.orc_bloom_contains.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64]
+        L.orc_lz4_decompress.restype = C.c_int64
+        L.orc_lz4_decompress.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64]
         _lib = L
     return _lib
 
@@ -148,6 +150,23 @@ def bloom_contains(filt: bytes, h: int) -> int:
     """StandardBloomFilterReader::contains_hash (standard_bloom/mod.rs:100-120)."""
     a = np.frombuffer(filt, np.uint8)
     return lib().orc_bloom_contains(_ptr(a), len(filt), h)
+
+
+def lz4_decompress(src: bytes, cap: int):
+    """LZ4 block decode (lz4_flex::decompress_into, src/table/block/mod.rs:104-118) -> bytes or None."""
+    a = np.frombuffer(src, np.uint8) if len(src) else np.zeros(1, np.uint8)
+    out = np.zeros(max(cap, 1), np.uint8)
+    n = lib().orc_lz4_decompress(_ptr(a), len(src), _ptr(out), cap)
+    return None if n < 0 else out[:n].tobytes()
+
+
+def block_header(block_type: int, payload: bytes, uncompressed_length: int) -> bytes:
+    """Header::encode_into (src/table/block/header.rs:80-112) for a payload as stored
+    (compressed or not): checksum = xxh3_128(stored payload)."""
+    ck = xxh3_128(payload)
+    h = b"LSM\x03" + bytes([block_type]) + ck.to_bytes(16, "little") + len(payload).to_bytes(4, "little") + \
+        uncompressed_length.to_bytes(4, "little")
+    return h + (xxh3_128(h) & 0xFFFFFFFF).to_bytes(4, "little")
 
 
 class Items:
