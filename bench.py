@@ -442,6 +442,53 @@ def bench_bloom(torch, lsmgpu, items, n_items, reps=5):
     return out
 
 
+def bench_lz4(torch, lsmgpu, enc, n_blocks, reps=5, sample=131072):
+    """Block::from_reader with CompressionType::Lz4 (src/table/block/mod.rs:87-128)
+    over LZ4 copies of the first `sample` configs[1] blocks: the payloads are
+    compressed on the host by liblz4 (pyarrow "lz4_raw", the block format
+    lz4_flex writes) and re-framed (header checksums by python-xxhash); then the
+    batch is checked + decompressed on the device.  Random 64 B values make the
+    payloads barely compressible, so this is the literal-heavy worst case."""
+    import numpy as np
+    try:
+        import pyarrow as pa
+        import xxhash
+    except ImportError as e:
+        return {"skipped": str(e)}
+    nb = min(sample, n_blocks)
+    off = enc["block_off"][:nb + 1].cpu().numpy().astype(np.int64)
+    host = enc["buf"][:int(off[-1])].cpu().numpy().tobytes()
+    codec = pa.Codec("lz4_raw")
+    parts, raw_total = [], 0
+    for b in range(nb):
+        payload = host[off[b] + 33:off[b + 1]]
+        c = codec.compress(payload, asbytes=True)
+        ck = xxhash.xxh3_128_intdigest(c)
+        h = b"LSM\x03\x00" + ck.to_bytes(16, "little") + len(c).to_bytes(4, "little") + \
+            len(payload).to_bytes(4, "little")
+        parts.append(h + xxhash.xxh3_128_intdigest(h).to_bytes(16, "little")[:4] + c)
+        raw_total += len(payload)
+    loff = np.zeros(nb + 1, np.int64)
+    loff[1:] = np.cumsum([len(p) for p in parts])
+    dbuf = lsmgpu.to_device_bytes(np.frombuffer(b"".join(parts), np.uint8))
+    doff = torch.from_numpy(loff).cuda()
+    out, out_off, status = lsmgpu.lz4_decompress_blocks(dbuf, doff)
+    torch.cuda.synchronize()
+    assert int((status != 0).sum().item()) == 0, "lz4: block status"
+    o0 = int(off[0]) + 33
+    assert out[:int(off[1]) - o0].cpu().numpy().tobytes() == host[o0:int(off[1])], "lz4: block 0 bytes"
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(reps):
+        lsmgpu.lz4_decompress_blocks(dbuf, doff)
+    e1.record()
+    torch.cuda.synchronize()
+    ms = e0.elapsed_time(e1) / reps
+    return {"blocks": nb, "stored_bytes": int(loff[-1]), "raw_bytes": raw_total, "ms": round(ms, 4),
+            "GiB_per_s_raw": round(raw_total / (ms * 1e-3) / 2 ** 30, 1),
+            "note": "header + xxh3_128 verify + LZ4 decode, wave per block; host-side size scan included"}
+
+
 def load_traffic(n_blocks):
     """HBM bytes of one decode_blocks_kernel launch over n_blocks, from the
     newest committed rocprofv3 PMC summary (profiles/traffic_*.json: FETCH_SIZE
@@ -574,6 +621,8 @@ def main():
         extra["point_read"] = bench_point_read(torch, lsmgpu, items, starts, enc, nb, n_items)
         extra["file_checksum"] = bench_file_checksum(torch, lsmgpu, enc, total_bytes)
         extra["bloom"] = bench_bloom(torch, lsmgpu, items, n_items)
+        if rank == 0:
+            extra["lz4"] = bench_lz4(torch, lsmgpu, enc, nb)
         if world == 1:
             extra["config4"] = bench_config4(torch, lsmgpu, max(3, args.steps // 4), rank)
         extra["config5"] = bench_config5(torch, lsmgpu, max(3, args.steps // 4), rank, world, dist, dev)
