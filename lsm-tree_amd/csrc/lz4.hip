@@ -26,30 +26,44 @@ namespace lsmgpu {
 
 constexpr int32_t kLz4Deferred = -1;  // small kernel -> large kernel hand-off
 
-// Wave-uniform LZ4 block decode from an LDS input slice into an LDS output
-// slice; returns the number of bytes written or -1 (Error::Decompress).
-__device__ __forceinline__ int64_t lz4_wave_decode(const uint8_t* in, uint32_t n, uint8_t* out, uint32_t cap, int lane) {
+// Wave-uniform LZ4 block decode from an LDS input slice (dword-staged, payload
+// at byte `sh`, readable 8 bytes past its end) into an LDS output slice;
+// returns the number of bytes written or -1 (Error::Decompress).  The parse
+// chain is one 8-byte window read per sequence in the common case: the window
+// read at a sequence's offset field also holds the next token.
+__device__ __forceinline__ uint64_t lds_read8(const uint32_t* w, uint32_t p) {
+  const uint32_t a = p >> 2, s = p & 3u;
+  const uint32_t d0 = w[a], d1 = w[a + 1], d2 = w[a + 2];
+  return s ? ((uint64_t)alignbyte(d1, d0, s) | ((uint64_t)alignbyte(d2, d1, s) << 32))
+           : ((uint64_t)d0 | ((uint64_t)d1 << 32));
+}
+
+__device__ __forceinline__ int64_t lz4_wave_decode(const uint32_t* lin, uint32_t sh, uint32_t n, uint8_t* out,
+                                                   uint32_t cap, int lane) {
+  const uint8_t* in = reinterpret_cast<const uint8_t*>(lin) + sh;
   uint32_t ip = 0, op = 0;
   if (n == 0) return -1;
+  uint64_t win = lds_read8(lin, sh);  // bytes at ip
   for (;;) {
     if (ip >= n) return -1;
-    const uint32_t token = in[ip++];
-    uint32_t lit = token >> 4;
+    const uint32_t token = (uint32_t)win & 0xFFu;
+    uint32_t lit = token >> 4, hp = ip + 1;
     if (lit == 15) {
       uint32_t b;
       do {
-        if (ip >= n) return -1;
-        b = in[ip++];
+        if (hp >= n) return -1;
+        b = in[hp++];
         lit += b;
       } while (b == 255);
     }
-    if (lit > n - ip || lit > cap - op) return -1;
-    for (uint32_t j = lane; j < lit; j += 64) out[op + j] = in[ip + j];
-    ip += lit;
+    if (lit > n - hp || lit > cap - op) return -1;
+    for (uint32_t j = lane; j < lit; j += 64) out[op + j] = in[hp + j];
+    ip = hp + lit;
     op += lit;
     if (ip == n) return op;
     if (n - ip < 2) return -1;
-    const uint32_t off = (uint32_t)in[ip] | ((uint32_t)in[ip + 1] << 8);
+    const uint64_t w2 = lds_read8(lin, sh + ip);  // offset, then (usually) the next token
+    const uint32_t off = (uint32_t)w2 & 0xFFFFu;
     ip += 2;
     if (off == 0 || off > op) return -1;
     uint32_t ml = (token & 15u) + 4;
@@ -60,6 +74,9 @@ __device__ __forceinline__ int64_t lz4_wave_decode(const uint8_t* in, uint32_t n
         b = in[ip++];
         ml += b;
       } while (b == 255);
+      win = lds_read8(lin, sh + ip);
+    } else {
+      win = w2 >> 16;
     }
     if (ml > cap - op) return -1;
     const uint32_t step = off < 64 ? off : 64;
@@ -149,9 +166,30 @@ __device__ __forceinline__ int32_t lz4_stage_and_decode(const Lz4Block& b, uint3
   const uint32_t* src = reinterpret_cast<const uint32_t*>(b.base + a0);
   for (uint32_t w = lane; w < words; w += 64) lin[w] = src[w];
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-  const int64_t got = lz4_wave_decode(reinterpret_cast<const uint8_t*>(lin) + sh, b.data_len, lout, kOut, lane);
+#ifdef LSM_LZ4_DIAG_SKIP_DECODE  // ablation build only: checks + checksum + staging, no decode
+  if (lane == 0) b.dst[0] = (uint8_t)lin[0];
+  return ST_OK;
+#endif
+  const int64_t got = lz4_wave_decode(lin, sh, b.data_len, lout, kOut, lane);
   if (got != (int64_t)b.raw_len) return LSM_DECOMPRESS;
+#ifdef LSM_LZ4_BYTE_STORE
   for (uint32_t j = lane; j < b.raw_len; j += 64) b.dst[j] = lout[j];
+#else
+  // dword stores to HBM: head bytes up to the first aligned dword, then dwords
+  // built from two aligned LDS dwords (alignbyte), then the tail bytes
+  const uint32_t len = b.raw_len;
+  uint32_t head = (4u - (uint32_t)((uintptr_t)b.dst & 3)) & 3u;
+  if (head > len) head = len;
+  if ((uint32_t)lane < head) b.dst[lane] = lout[lane];
+  const uint32_t body = (len - head) >> 2, s = head & 3u;
+  const uint32_t* l32 = reinterpret_cast<const uint32_t*>(lout);
+  uint32_t* d32 = reinterpret_cast<uint32_t*>(b.dst + head);
+  for (uint32_t w = lane; w < body; w += 64) {
+    const uint32_t a = (head >> 2) + w;  // head < 4, so a = w; kept general
+    d32[w] = s ? alignbyte(l32[a + 1], l32[a], s) : l32[a];
+  }
+  for (uint32_t j = head + 4 * body + lane; j < len; j += 64) b.dst[j] = lout[j];
+#endif
   return ST_OK;
 }
 
@@ -171,7 +209,7 @@ __global__ __launch_bounds__(256) void lz4_small_kernel(const uint8_t* __restric
   int32_t st = lz4_check_block(blocks, block_off, out_off, out, i, b);
   if (st == ST_OK) {
     const uint32_t sh = (b.hb + kHdrLen) & 3u;
-    if (b.data_len + sh + 4 > kSmallIn || b.raw_len > kSmallOut)
+    if (b.data_len + sh + 12 > kSmallIn || b.raw_len > kSmallOut)  // +12: dword window + 8-byte reads
       st = kLz4Deferred;
     else
       st = lz4_stage_and_decode<kSmallIn, kSmallOut>(b, s_in[wv], s_out[wv], lane);
@@ -193,7 +231,7 @@ __global__ __launch_bounds__(64) void lz4_large_kernel(const uint8_t* __restrict
     int32_t st = lz4_check_block(blocks, block_off, out_off, out, i, b);
     if (st == ST_OK) {
       const uint32_t sh = (b.hb + kHdrLen) & 3u;
-      if (b.data_len + sh + 4 <= kLargeIn && b.raw_len <= kLargeOut) {
+      if (b.data_len + sh + 12 <= kLargeIn && b.raw_len <= kLargeOut) {
         st = lz4_stage_and_decode<kLargeIn, kLargeOut>(b, s_dyn, reinterpret_cast<uint8_t*>(s_dyn + kLargeIn / 4), lane);
       } else {
         int64_t got = 0;
