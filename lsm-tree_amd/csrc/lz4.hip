@@ -34,8 +34,14 @@ constexpr int32_t kLz4Deferred = -1;  // small kernel -> large kernel hand-off
 __device__ __forceinline__ uint64_t lds_read8(const uint32_t* w, uint32_t p) {
   const uint32_t a = p >> 2, s = p & 3u;
   const uint32_t d0 = w[a], d1 = w[a + 1], d2 = w[a + 2];
-  return s ? ((uint64_t)alignbyte(d1, d0, s) | ((uint64_t)alignbyte(d2, d1, s) << 32))
-           : ((uint64_t)d0 | ((uint64_t)d1 << 32));
+  const uint32_t lo = s ? alignbyte(d1, d0, s) : d0, hi = s ? alignbyte(d2, d1, s) : d1;
+  // wave-uniform by construction (every lane reads the same bytes): move it to
+  // SGPRs so the walk's bounds checks and loops are scalar branches
+  return (uint64_t)__builtin_amdgcn_readfirstlane(lo) | ((uint64_t)__builtin_amdgcn_readfirstlane(hi) << 32);
+}
+
+__device__ __forceinline__ uint32_t lds_read1(const uint8_t* in, uint32_t p) {
+  return __builtin_amdgcn_readfirstlane((uint32_t)in[p]);
 }
 
 __device__ __forceinline__ int64_t lz4_wave_decode(const uint32_t* lin, uint32_t sh, uint32_t n, uint8_t* out,
@@ -52,7 +58,7 @@ __device__ __forceinline__ int64_t lz4_wave_decode(const uint32_t* lin, uint32_t
       uint32_t b;
       do {
         if (hp >= n) return -1;
-        b = in[hp++];
+        b = lds_read1(in, hp++);
         lit += b;
       } while (b == 255);
     }
@@ -71,7 +77,7 @@ __device__ __forceinline__ int64_t lz4_wave_decode(const uint32_t* lin, uint32_t
       uint32_t b;
       do {
         if (ip >= n) return -1;
-        b = in[ip++];
+        b = lds_read1(in, ip++);
         ml += b;
       } while (b == 255);
       win = lds_read8(lin, sh + ip);
@@ -148,8 +154,8 @@ __device__ __forceinline__ int32_t lz4_check_block(const uint8_t* blocks, const 
   int32_t st = check_header(b.base, b.hb, e - o, h);
   if (st != ST_OK) return st;
   if ((uint64_t)h.data_length != e - o - kHdrLen) return ST_TRUNCATED;
-  b.data_len = h.data_length;
-  b.raw_len = read_u32_unaligned(b.base, b.hb + 25);  // uncompressed_length, header.rs:101
+  b.data_len = __builtin_amdgcn_readfirstlane(h.data_length);  // wave-uniform: keep the walk scalar
+  b.raw_len = __builtin_amdgcn_readfirstlane(read_u32_unaligned(b.base, b.hb + 25));  // uncompressed_length, header.rs:101
   if ((uint64_t)b.raw_len != out_off[i + 1] - out_off[i]) return ST_OVERFLOW;
   uint64_t lo, hi;
   xxh3_128_wave(b.base, b.hb + kHdrLen, b.data_len, &kLongSecret, lo, hi);
