@@ -25,6 +25,7 @@
  *   lsm_point_read_blocks <- DataBlock::point_read src/table/data_block/mod.rs:412-472
  *   lsm_xxh3_128_file  <- ChecksummedWriter         src/checksum.rs:59-96 (whole-file checksum)
  *   lsm_lz4_decompress_blocks <- Block::from_reader/from_file, CompressionType::Lz4  block/mod.rs:87-182
+ *   lsm_lz4_plan_output <- the builder_unzeroed(uncompressed_length) sizing of the same  block/mod.rs:104-112
  *   lsm_bloom_shape    <- BloomConstructionPolicy::init  src/table/filter/mod.rs:25-34
  *   lsm_hash64_keys    <- FullFilterWriter::register_key src/table/writer/filter/full.rs:47-50
  *   lsm_bloom_build    <- standard_bloom Builder set_with_hash + build  builder.rs:33-53,154-170
@@ -40,7 +41,7 @@
 extern "C" {
 #endif
 
-#define LSM_ABI_VERSION 1
+#define LSM_ABI_VERSION 2
 #define LSM_HEADER_LEN 33  /* Header::serialized_len(), header.rs:64-76 */
 #define LSM_TRAILER_LEN 31 /* TRAILER_SIZE, trailer.rs:14-23 */
 /* d_blocks must be 16-byte aligned and readable for LSM_INPUT_PADDING bytes
@@ -111,31 +112,20 @@ typedef struct lsm_block_params {
     uint8_t restart_interval; /* data_block_restart_interval (config default 16); forced 1 for index */
     uint8_t block_type;       /* LSM_BLOCK_DATA / LSM_BLOCK_INDEX / LSM_BLOCK_META */
     uint8_t compression;      /* 0 = CompressionType::None (the only supported value) */
-    uint8_t reserved;         /* must be 0 (non-zero bits are diagnostic ablations that skip
-                                 parts of the encode and leave the output invalid) */
+    uint8_t reserved;         /* must be 0 (else LSM_BAD_ARG) */
     float hash_ratio;         /* data_block_hash_ratio (default 0.0) */
 } lsm_block_params;
 
-/* Tuning knobs for the decode kernel (0 = library default). */
+/* Tuning knobs for the decode kernel (0 = library default).  Any flag bit
+ * other than LSM_DECODE_ITEM_START_VALID is rejected with LSM_BAD_ARG. */
 typedef struct lsm_decode_tuning {
-    uint32_t blocks_per_wave;  /* LSM_DECODE_LEGACY only: consecutive blocks one workgroup owns (1..63) */
-    uint32_t stage_bytes;      /* LDS bytes per ring slot (default 32768; legacy: per stage, 65536) */
-    uint32_t tile_items;       /* items one slot (legacy: one stage) may hold (default 512) */
+    uint32_t blocks_per_wave;  /* consecutive blocks one workgroup owns (1..63, default 48) */
+    uint32_t stage_bytes;      /* LDS stage bytes (256..65536, default 32768); larger blocks take the general path */
+    uint32_t tile_items;       /* items one stage may hold (default 448, at most 8192) */
     uint32_t flags;            /* LSM_DECODE_ITEM_START_VALID: d_item_start already holds the
-                                  prefix sum of this batch (skip the count + scan pass);
-                                  LSM_DECODE_LEGACY / LSM_DECODE_RING: force the single-stage
-                                  kernel or the LDS-ring kernel (default: the faster one) */
-    uint32_t ring_slots;       /* LDS ring depth, 2..8 (default 4) */
-    uint32_t ring_walkers;     /* waves walking record boundaries (default 3) */
-    uint32_t ring_hashers;     /* waves verifying payload checksums (default 4); the other
-                                  16 - loaders - walkers - hashers waves parse and store */
-    uint32_t ring_loaders;     /* waves issuing the LDS-DMA of every group, 1..8 (default 4) */
+                                  prefix sum of this batch (skip the count + scan pass) */
 } lsm_decode_tuning;
 #define LSM_DECODE_ITEM_START_VALID 1u
-#define LSM_DECODE_LEGACY 0x10000u
-#define LSM_DECODE_DOUBLE 0x40000u /* legacy kernel, two stage slots: the next group's LDS-DMA overlaps this group's parse */
-#define LSM_DECODE_RING 0x80000u
-#define LSM_DECODE_SPLIT_WALK 0x100000u /* legacy kernel: two lanes per restart interval in the boundary walk */
 
 /* Point-read results (DataBlock::point_read -> Option<InternalValue>,
  * data_block/mod.rs:412-472), one row per query; NULL fields other than item
@@ -274,6 +264,18 @@ int lsm_bloom_contains(const uint8_t* d_filter, uint64_t filter_len, const uint6
  * that does not decode to exactly uncompressed_length bytes).
  * Workspace: lsm_lz4_workspace_size(n_blocks) bytes. */
 size_t lsm_lz4_workspace_size(uint32_t n_blocks);
+/* Output plan for lsm_lz4_decompress_blocks: d_out_off (n_blocks+1 device u64)
+ * = exclusive prefix sum of each block's uncompressed_length, counted only for
+ * blocks whose header verifies (magic, type, header checksum, data_length ==
+ * handle size) and whose uncompressed_length <= max_block_bytes; other blocks
+ * get 0 bytes (their decompress status is then the header error, or
+ * LSM_OVERFLOW).  So a corrupt header cannot size the output, as
+ * Block::from_reader allocates only after Header::decode_from passed
+ * (block/mod.rs:91-112).  Workspace: lsm_lz4_plan_workspace_size(n_blocks). */
+size_t lsm_lz4_plan_workspace_size(uint32_t n_blocks);
+int lsm_lz4_plan_output(const uint8_t* d_blocks, const uint64_t* d_block_off, uint32_t n_blocks,
+                        uint64_t max_block_bytes, uint64_t* d_out_off, void* d_workspace, size_t workspace_bytes,
+                        void* stream);
 int lsm_lz4_decompress_blocks(const uint8_t* d_blocks, const uint64_t* d_block_off, uint32_t n_blocks,
                               uint8_t* d_out, const uint64_t* d_out_off, int32_t* d_status,
                               void* d_workspace, size_t workspace_bytes, void* stream);

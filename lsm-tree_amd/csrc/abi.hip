@@ -10,21 +10,22 @@
 #include "lsmgpu.h"
 
 namespace {
-
 thread_local char g_last_error[256] = "";
+}  // namespace
 
-int set_hip_error(hipError_t e, const char* where) {
+// Records the HIP error for lsm_last_error() (per calling thread).
+int lsmgpu::hip_status(hipError_t e, const char* where) {
+  if (e == hipSuccess) return LSM_OK;
   snprintf(g_last_error, sizeof g_last_error, "%s: %s", where, hipGetErrorString(e));
   return LSM_HIP_ERROR;
 }
 
-// legacy single-stage kernel (LSM_DECODE_LEGACY)
+namespace {
+int set_hip_error(hipError_t e, const char* where) { return lsmgpu::hip_status(e, where); }
+
 constexpr uint32_t kDefaultBlocksPerWave = 48;  // per workgroup
 constexpr uint32_t kDefaultStageBytes = 32768;  // four 4-wave workgroups per CU (LDS ~40 KiB each)
 constexpr uint32_t kDefaultTileItems = 448;
-// ring kernel (default)
-constexpr uint32_t kRingSlotBytes = 32768, kRingTileItems = 512, kRingSlots = 4, kRingWalkers = 3,
-                   kRingHashers = 4, kRingLoaders = 4;
 
 }  // namespace
 
@@ -87,30 +88,16 @@ int lsm_decode_blocks_tuned(const uint8_t* d_blocks, const uint64_t* d_block_off
   P.item_start_w = d_item_start;
   P.status = d_status;
   P.flags = tuning ? tuning->flags : 0;
-  if (!(P.flags & (lsmgpu::kDecodeLegacy | lsmgpu::kDecodeRing)))
-    P.flags |= lsmgpu::kDecodeDefaultRing ? lsmgpu::kDecodeRing : lsmgpu::kDecodeLegacy;
-  const bool legacy = (P.flags & lsmgpu::kDecodeLegacy) != 0;
+  const uint32_t allowed = LSM_DECODE_ITEM_START_VALID | (lsmgpu::kDiagBuild ? lsmgpu::kDecodeDiagMask : 0u);
+  if (P.flags & ~allowed) return LSM_BAD_ARG;
   auto pick = [&](uint32_t v, uint32_t dflt) { return v ? v : dflt; };
   P.blocks_per_wave = pick(tuning ? tuning->blocks_per_wave : 0, kDefaultBlocksPerWave);
-  P.stage_bytes = pick(tuning ? tuning->stage_bytes : 0, legacy ? kDefaultStageBytes : kRingSlotBytes);
-  P.tile_items = pick(tuning ? tuning->tile_items : 0, legacy ? kDefaultTileItems : kRingTileItems);
-  P.ring_slots = pick(tuning ? tuning->ring_slots : 0, kRingSlots);
-  P.ring_x = pick(tuning ? tuning->ring_walkers : 0, kRingWalkers);
-  P.ring_h = pick(tuning ? tuning->ring_hashers : 0, kRingHashers);
-  P.ring_l = pick(tuning ? tuning->ring_loaders : 0, kRingLoaders);
-  P.stage_bytes = (P.stage_bytes + 15) & ~15u;
+  P.stage_bytes = pick(tuning ? tuning->stage_bytes : 0, kDefaultStageBytes);
+  P.tile_items = pick(tuning ? tuning->tile_items : 0, kDefaultTileItems);
   if (P.tile_items > 8192 || P.stage_bytes < 256 || P.stage_bytes > 65536 || P.blocks_per_wave > 63)
     return LSM_BAD_ARG;
-  if (legacy) {
-    if (lsmgpu::decode_lds_bytes(P.stage_bytes, P.tile_items, P.blocks_per_wave,
-                                 (P.flags & lsmgpu::kDecodeDouble) ? 2 : 1) > 160 * 1024)
-      return LSM_BAD_ARG;
-  } else {
-    if (P.ring_slots < 2 || P.ring_slots > 8 || P.tile_items > 4096 || P.ring_l < 1 || P.ring_l > 8 ||
-        P.ring_l + P.ring_x + P.ring_h > lsmgpu::kRingWaves - 1)
-      return LSM_BAD_ARG;
-    if (lsmgpu::decode_ring_lds_bytes(P.ring_slots, P.stage_bytes, P.tile_items) > 160 * 1024) return LSM_BAD_ARG;
-  }
+  P.stage_bytes = (P.stage_bytes + 15) & ~15u;
+  if (lsmgpu::decode_lds_bytes(P.stage_bytes, P.tile_items, P.blocks_per_wave) > 160 * 1024) return LSM_BAD_ARG;
   hipError_t e = lsmgpu::launch_decode(P, d_workspace, (hipStream_t)stream);
   return e == hipSuccess ? LSM_OK : set_hip_error(e, "lsm_decode_blocks");
 }
@@ -138,6 +125,7 @@ int lsm_encode_blocks(const lsm_items* d_items, const uint32_t* d_block_item_sta
   if (n_blocks == 0) return LSM_OK;
   if (!d_items || !params || !d_block_item_start || !d_out || !d_block_off || !d_status) return LSM_BAD_ARG;
   if (params->compression != 0) return LSM_UNSUPPORTED;
+  if (params->reserved != 0 && !lsmgpu::kDiagBuild) return LSM_BAD_ARG;
   if (params->block_type != LSM_BLOCK_DATA && params->block_type != LSM_BLOCK_INDEX &&
       params->block_type != LSM_BLOCK_META)
     return LSM_BAD_ARG;
@@ -184,9 +172,3 @@ int lsm_xxh3_128_batch(const uint8_t* d_data, const uint64_t* d_off, uint32_t n,
 }
 
 }  // extern "C"
-
-/* Diagnostic (not part of the public header): phase timers of decode launches
- * run with tuning flag 0x2000, summed clock64() cycles per phase and wave. */
-extern "C" int lsm_diag_decode_timers(uint64_t* out, int n, int reset) {
-  return lsmgpu::read_decode_timers(out, n, reset != 0) == hipSuccess ? LSM_OK : LSM_HIP_ERROR;
-}

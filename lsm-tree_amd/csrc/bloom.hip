@@ -18,6 +18,7 @@
 // the probe latency bound; neither is an HBM-streaming kernel.
 #include <hip/hip_runtime.h>
 
+#include "decode.hpp"
 #include "device_common.hpp"
 #include "lsmgpu.h"
 
@@ -155,7 +156,7 @@ int lsm_hash64_keys(const uint8_t* d_keys, const uint64_t* d_key_off, uint64_t n
   if (!d_keys || !d_key_off || !d_out || ((uintptr_t)d_keys & 15)) return LSM_BAD_ARG;
   hipLaunchKernelGGL(hash64_keys_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, d_keys, d_key_off, n,
                      d_out);
-  return hipGetLastError() == hipSuccess ? LSM_OK : LSM_HIP_ERROR;
+  return lsmgpu::hip_status(hipGetLastError(), __func__);
 }
 
 int lsm_bloom_build(const uint64_t* d_hashes, uint64_t n, uint64_t m, uint64_t k, uint8_t* d_filter,
@@ -172,7 +173,7 @@ int lsm_bloom_build(const uint64_t* d_hashes, uint64_t n, uint64_t m, uint64_t k
   if (n)
     hipLaunchKernelGGL(bloom_set_kernel, dim3(grid_for(n)), dim3(256), 0, st, d_hashes, n, m, (uint32_t)k,
                        (uint32_t*)d_filter);
-  return hipGetLastError() == hipSuccess ? LSM_OK : LSM_HIP_ERROR;
+  return lsmgpu::hip_status(hipGetLastError(), __func__);
 }
 
 int lsm_bloom_contains(const uint8_t* d_filter, uint64_t filter_len, const uint64_t* d_hashes, uint64_t n,
@@ -181,7 +182,7 @@ int lsm_bloom_contains(const uint8_t* d_filter, uint64_t filter_len, const uint6
   if (!d_filter || !d_hashes || !d_out || filter_len < kBloomHdr) return LSM_BAD_ARG;
   hipLaunchKernelGGL(bloom_contains_kernel, dim3(grid_for(n)), dim3(256), 0, (hipStream_t)stream, d_filter,
                      filter_len, d_hashes, n, d_out);
-  return hipGetLastError() == hipSuccess ? LSM_OK : LSM_HIP_ERROR;
+  return lsmgpu::hip_status(hipGetLastError(), __func__);
 }
 
 }  // extern "C"

@@ -189,5 +189,5 @@ extern "C" int lsm_xxh3_128_file(const uint8_t* d_data, uint64_t len, uint64_t* 
   if (!d_out || (len && !d_data)) return LSM_BAD_ARG;
   if (len > 240 && (!d_workspace || workspace_bytes < lsmgpu::xxh3_file_workspace_size(len))) return LSM_BAD_ARG;
   const hipError_t e = lsmgpu::launch_xxh3_128_file(d_data, len, d_out, d_workspace, (hipStream_t)stream);
-  return e == hipSuccess ? LSM_OK : LSM_HIP_ERROR;
+  return lsmgpu::hip_status(e, "lsm_xxh3_128_file");
 }

@@ -24,21 +24,38 @@ struct DecodeParams {
   uint32_t flags;
   uint32_t* defer_count;  // workspace: blocks handed to the general path
   uint32_t* defer_list;
-  // ring kernel (decode_ring_kernel): LDS ring slots and wave roles
-  uint32_t ring_slots, ring_l, ring_x, ring_h;  // slots, loader / walker / hasher waves
 };
 
+// Diagnostic builds (-DLSM_DIAG, `make variant`) honour ablation bits in
+// lsm_decode_tuning.flags / lsm_block_params.reserved that skip parts of the
+// work (outputs invalid); the release library rejects them (LSM_BAD_ARG).
+#ifdef LSM_DIAG
+constexpr bool kDiagBuild = true;
+#else
+constexpr bool kDiagBuild = false;
+#endif
+constexpr uint32_t kDiagSkipHash = 0x100, kDiagSkipParse = 0x200, kDiagSkipStore = 0x400, kDiagSkipPhaseB = 0x800;
+constexpr uint32_t kDecodeDiagMask = kDiagSkipHash | kDiagSkipParse | kDiagSkipStore | kDiagSkipPhaseB;
+
+// The > 64 KiB dynamic-LDS attribute acts on the CURRENT device: set it once
+// per device (a process may drive several GPUs, one host thread per device).
+inline hipError_t set_lds_attr(const void* fn, uint32_t bytes, uint64_t* done_mask) {
+  int dev = 0;
+  hipError_t e = hipGetDevice(&dev);
+  if (e != hipSuccess) return e;
+  const uint64_t bit = dev < 64 ? 1ULL << dev : 0;
+  if (bit && (__atomic_load_n(done_mask, __ATOMIC_ACQUIRE) & bit)) return hipSuccess;
+  e = hipFuncSetAttribute(fn, hipFuncAttributeMaxDynamicSharedMemorySize, (int)bytes);
+  if (e == hipSuccess && bit) __atomic_fetch_or(done_mask, bit, __ATOMIC_RELEASE);
+  return e;
+}
+
+// hipSuccess -> LSM_OK; else LSM_HIP_ERROR with the message kept for lsm_last_error().
+int hip_status(hipError_t e, const char* where);
+
 size_t decode_workspace_size(uint32_t n_blocks);
-uint32_t decode_lds_bytes(uint32_t stage_bytes, uint32_t tile_items, uint32_t blocks_per_wave, uint32_t slots);
-uint32_t decode_ring_lds_bytes(uint32_t slots, uint32_t slot_bytes, uint32_t tile_items);
-constexpr uint32_t kDecodeLegacy = 0x10000;  // tuning flag: the single-stage kernel (decode_blocks_kernel)
-constexpr uint32_t kDecodeDouble = 0x40000;  // tuning flag: legacy kernel with two stage slots (prefetch one group ahead)
-constexpr uint32_t kDecodeSplitWalk = 0x100000;  // tuning flag: two lanes per restart interval in phase A
-constexpr uint32_t kDecodeRing = 0x80000;    // tuning flag: the LDS-ring kernel (decode_ring_kernel)
-constexpr bool kDecodeDefaultRing = false;   // kernel when neither flag is given
-constexpr uint32_t kRingWaves = 16;
+uint32_t decode_lds_bytes(uint32_t stage_bytes, uint32_t tile_items, uint32_t blocks_per_wave);
 hipError_t launch_decode(const DecodeParams& P, void* workspace, hipStream_t st);
-hipError_t read_decode_timers(uint64_t* host, int n, bool reset);  // diagnostic
 
 hipError_t launch_xxh3_128_batch(const uint8_t* data, const uint64_t* off, uint32_t n, uint64_t* out,
                                  hipStream_t st);

@@ -25,6 +25,7 @@
 #include <math.h>
 
 #include "block_format.hpp"
+#include "decode.hpp"
 #include "encode.hpp"
 #include "scan.hpp"
 
@@ -433,13 +434,13 @@ __device__ __forceinline__ void finish_block_lds(const EncodeParams& P, uint32_t
   for (uint32_t k = lane; k < pl.hash_w; k += kWave) img[p0 + hash_off + k] = (uint8_t)bucket_byte(hlo[k], hhi[k]);
   write_trailer_bytes(img, p0 + plen - kTrailerLen, ri, step, pl.bin_len, bin_off, pl.hash_w, hash_off, n);
   wave_lds_sync();
-  if (!(P.diag & 2)) {
+  if (!(kDiagBuild && (P.diag & 2))) {
     uint64_t ck_lo, ck_hi;
     xxh3_128_wave(img, p0, plen, &kLongSecret, ck_lo, ck_hi);
     write_header_bytes(img, pad, P.type, ck_lo, ck_hi, plen);
   }
   wave_lds_sync();
-  const uint32_t chunks = (P.diag & 4) ? 0 : (pad + total + 15) >> 4;
+  const uint32_t chunks = (kDiagBuild && (P.diag & 4)) ? 0 : (pad + total + 15) >> 4;
   for (uint32_t c = lane; c < chunks; c += kWave) {
     const uint32_t lo = c * 16, hi = lo + 16;
     if (lo >= pad && hi <= pad + total) {
@@ -607,7 +608,7 @@ __global__ __launch_bounds__(kSmallWaves * kWave) __attribute__((amdgpu_waves_pe
     hhi[k] = 0;
   }
   wave_lds_sync();
-  if ((uint32_t)lane < n && !(P.diag & 1)) {
+  if ((uint32_t)lane < n && !(kDiagBuild && (P.diag & 1))) {
     rc.store(P, m, head, img);
     if (head) store_le(img, p0 + pl.recs + 1 + (lane / ri) * step, roff, step);
     if (pl.hash_w) {
@@ -765,11 +766,8 @@ hipError_t launch_encode(const lsm_items& items, const uint32_t* starts, uint32_
   if ((e = launch_excl_scan(P.sizes, n_blocks, tiles,
                             EncodeOffOut{block_off, P.sizes, P.lists, P.list_count, n_blocks}, st)) != hipSuccess)
     return e;
-  static bool attrs = [] {
-    return hipFuncSetAttribute((const void*)encode_write_list_kernel, hipFuncAttributeMaxDynamicSharedMemorySize,
-                               (int)kImgBig) == hipSuccess;
-  }();
-  (void)attrs;
+  static uint64_t attr_done = 0;
+  if ((e = set_lds_attr((const void*)encode_write_list_kernel, kImgBig, &attr_done)) != hipSuccess) return e;
   hipLaunchKernelGGL(encode_write_kernel, dim3((n_blocks + kSmallWaves - 1) / kSmallWaves), dim3(kSmallWaves * kWave),
                      kSmallWaves * kImgSmall, st, P);
   hipLaunchKernelGGL(encode_write_list_kernel, dim3(2048), dim3(kWave), kImgMedium, st, P, kPlanMedium);

@@ -19,8 +19,10 @@
 #include <hip/hip_runtime.h>
 
 #include "block_format.hpp"
+#include "decode.hpp"
 #include "device_common.hpp"
 #include "lsmgpu.h"
+#include "scan.hpp"
 
 namespace lsmgpu {
 
@@ -256,9 +258,56 @@ __global__ __launch_bounds__(256) void lz4_collect_deferred(int32_t* __restrict_
   if (i < n && status[i] == kLz4Deferred) list[atomicAdd(count, 1u)] = i;
 }
 
+// Output plan (lane per block): the uncompressed_length of every block whose
+// header verifies (magic, type, header checksum, data_length == handle), as
+// Block::from_reader only sizes its buffer after Header::decode_from has
+// passed (block/mod.rs:91-112); 0 for a failing header or a length above the
+// caller's cap (that block then reports its header status, or OVERFLOW).
+__global__ __launch_bounds__(256) void lz4_plan_kernel(const uint8_t* __restrict__ blocks,
+                                                       const uint64_t* __restrict__ block_off, uint32_t n,
+                                                       uint64_t max_raw, uint64_t* __restrict__ raw) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t o = block_off[i], e = block_off[i + 1];
+  const uint8_t* base = blocks + (o & ~15ULL);
+  const uint32_t hb = (uint32_t)(o & 15);
+  HeaderInfo h;
+  uint64_t len = 0;
+  if (e >= o && check_header(base, hb, e - o, h) == ST_OK && (uint64_t)h.data_length == e - o - kHdrLen) {
+    len = read_u32_unaligned(base, hb + 25);  // uncompressed_length, header.rs:101
+    if (len > max_raw) len = 0;
+  }
+  raw[i] = len;
+}
+
+struct Lz4OffOut {
+  uint64_t* off;
+  __device__ void operator()(uint64_t i, uint64_t prefix) const { off[i] = prefix; }
+};
+
 }  // namespace lsmgpu
 
 using namespace lsmgpu;
+
+extern "C" size_t lsm_lz4_plan_workspace_size(uint32_t n_blocks) {
+  return ((size_t)n_blocks * 8 + 255) / 256 * 256 + (scan_tiles(n_blocks ? n_blocks : 1) * 8 + 255) / 256 * 256;
+}
+
+extern "C" int lsm_lz4_plan_output(const uint8_t* d_blocks, const uint64_t* d_block_off, uint32_t n_blocks,
+                                   uint64_t max_block_bytes, uint64_t* d_out_off, void* d_workspace,
+                                   size_t workspace_bytes, void* stream) {
+  if (n_blocks == 0) return LSM_OK;
+  if (!d_blocks || !d_block_off || !d_out_off || !d_workspace || ((uintptr_t)d_blocks & 15) ||
+      workspace_bytes < lsm_lz4_plan_workspace_size(n_blocks))
+    return LSM_BAD_ARG;
+  const hipStream_t st = (hipStream_t)stream;
+  uint64_t* raw = (uint64_t*)d_workspace;
+  uint64_t* tiles = (uint64_t*)((uint8_t*)d_workspace + ((size_t)n_blocks * 8 + 255) / 256 * 256);
+  hipLaunchKernelGGL(lz4_plan_kernel, dim3((n_blocks + 255) / 256), dim3(256), 0, st, d_blocks, d_block_off, n_blocks,
+                     max_block_bytes, raw);
+  hipError_t e = launch_excl_scan(raw, n_blocks, tiles, Lz4OffOut{d_out_off}, st);
+  return hip_status(e != hipSuccess ? e : hipGetLastError(), "lsm_lz4_plan_output");
+}
 
 extern "C" size_t lsm_lz4_workspace_size(uint32_t n_blocks) { return 16 + (size_t)n_blocks * 4; }
 
@@ -272,17 +321,17 @@ extern "C" int lsm_lz4_decompress_blocks(const uint8_t* d_blocks, const uint64_t
   const hipStream_t st = (hipStream_t)stream;
   uint32_t* count = (uint32_t*)d_workspace;
   uint32_t* list = count + 4;
-  if (hipMemsetAsync(count, 0, 4, st) != hipSuccess) return LSM_HIP_ERROR;
+  hipError_t e = hipMemsetAsync(count, 0, 4, st);
+  if (e != hipSuccess) return hip_status(e, "lsm_lz4_decompress_blocks");
   hipLaunchKernelGGL(lz4_small_kernel, dim3((n_blocks + 3) / 4), dim3(256), 0, st, d_blocks, d_block_off, n_blocks,
                      d_out, d_out_off, d_status);
   hipLaunchKernelGGL(lz4_collect_deferred, dim3((n_blocks + 255) / 256), dim3(256), 0, st, d_status, n_blocks, list,
                      count);
-  static const hipError_t attr = hipFuncSetAttribute((const void*)lz4_large_kernel,
-                                                     hipFuncAttributeMaxDynamicSharedMemorySize,
-                                                     (int)(kLargeIn + kLargeOut));
-  if (attr != hipSuccess) return LSM_HIP_ERROR;
+  static uint64_t attr_done = 0;
+  if ((e = set_lds_attr((const void*)lz4_large_kernel, kLargeIn + kLargeOut, &attr_done)) != hipSuccess)
+    return hip_status(e, "lsm_lz4_decompress_blocks");
   const uint32_t grid = n_blocks < 1024 ? n_blocks : 1024;
   hipLaunchKernelGGL(lz4_large_kernel, dim3(grid), dim3(64), kLargeIn + kLargeOut, st, d_blocks, d_block_off,
                      n_blocks, d_out, d_out_off, d_status, list, count);
-  return hipGetLastError() == hipSuccess ? LSM_OK : LSM_HIP_ERROR;
+  return hip_status(hipGetLastError(), "lsm_lz4_decompress_blocks");
 }

@@ -19,6 +19,7 @@
 #include <hip/hip_runtime.h>
 
 #include "block_format.hpp"
+#include "decode.hpp"
 #include "lsmgpu.h"
 
 namespace lsmgpu {
@@ -191,8 +192,10 @@ extern "C" int lsm_point_read_blocks(const uint8_t* d_blocks, const uint64_t* d_
   if (!d_blocks || !d_block_off || !d_query_block || !d_needles || !d_needle_off || !d_snapshot || !d_out ||
       !d_out->item || !d_status)
     return LSM_BAD_ARG;
+  // the kernel reads blocks and needles through aligned 4-byte windows from 16-byte-aligned bases
+  if (((uintptr_t)d_blocks & 15) || ((uintptr_t)d_needles & 15)) return LSM_BAD_ARG;
   const hipError_t e = lsmgpu::launch_point_read(d_blocks, d_block_off, n_blocks, d_query_block, d_needles,
                                                  d_needle_off, d_snapshot, n_queries, *d_out, d_status,
                                                  (hipStream_t)stream);
-  return e == hipSuccess ? LSM_OK : LSM_HIP_ERROR;
+  return lsmgpu::hip_status(e, "lsm_point_read_blocks");
 }

@@ -48,13 +48,11 @@ class LsmPointResult(C.Structure):
 
 class LsmDecodeTuning(C.Structure):
     _fields_ = [("blocks_per_wave", C.c_uint32), ("stage_bytes", C.c_uint32), ("tile_items", C.c_uint32),
-                ("flags", C.c_uint32), ("ring_slots", C.c_uint32), ("ring_walkers", C.c_uint32),
-                ("ring_hashers", C.c_uint32), ("ring_loaders", C.c_uint32)]
+                ("flags", C.c_uint32)]
 
 
+ABI_VERSION = 2
 DECODE_ITEM_START_VALID = 1
-DECODE_LEGACY = 0x10000  # force the single-stage kernel
-DECODE_RING = 0x80000  # force the LDS-ring kernel
 
 
 class LsmError(RuntimeError):
@@ -129,6 +127,11 @@ def lib():
         L.lsm_lz4_decompress_blocks.restype = C.c_int
         L.lsm_lz4_decompress_blocks.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p,
                                                 C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]
+        L.lsm_lz4_plan_workspace_size.restype = C.c_size_t
+        L.lsm_lz4_plan_workspace_size.argtypes = [C.c_uint32]
+        L.lsm_lz4_plan_output.restype = C.c_int
+        L.lsm_lz4_plan_output.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint64, C.c_void_p, C.c_void_p,
+                                          C.c_size_t, C.c_void_p]
         _lib = L
     return _lib
 
@@ -138,7 +141,8 @@ EXPORTED_SYMBOLS = ["lsm_abi_version", "lsm_status_name", "lsm_last_error", "lsm
                     "lsm_encode_workspace_size", "lsm_encode_blocks", "lsm_cut_blocks", "lsm_xxh3_128_batch",
                     "lsm_point_read_blocks", "lsm_xxh3_128_file_workspace_size", "lsm_xxh3_128_file",
                     "lsm_bloom_calculate_m", "lsm_bloom_shape", "lsm_bloom_filter_size", "lsm_hash64_keys",
-                    "lsm_bloom_build", "lsm_bloom_contains", "lsm_lz4_workspace_size", "lsm_lz4_decompress_blocks"]
+                    "lsm_bloom_build", "lsm_bloom_contains", "lsm_lz4_workspace_size", "lsm_lz4_decompress_blocks",
+                    "lsm_lz4_plan_workspace_size", "lsm_lz4_plan_output"]
 
 
 def _check(rc, what):
@@ -363,19 +367,25 @@ def bloom_contains(filt, hashes, stream=None):
     return out[:hashes.numel()]
 
 
-def lz4_decompress_blocks(blocks, block_off, n_blocks=None, stream=None):
+# the largest uncompressed block the default writer makes is 4 MiB (writer/mod.rs:195-198)
+LZ4_MAX_BLOCK = 1 << 26
+
+
+def lz4_decompress_blocks(blocks, block_off, n_blocks=None, max_block_bytes=LZ4_MAX_BLOCK, stream=None):
     """Block::from_reader with CompressionType::Lz4 over a batch (block/mod.rs:87-128):
     blocks = padded uint8 cuda tensor of on-disk blocks, block_off = int64 cuda [n+1].
-    Output sizes come from each header's uncompressed_length (bytes 25..28).
+    Output sizes come from lsm_lz4_plan_output: each VERIFIED header's
+    uncompressed_length (a block whose header fails gets 0 bytes and reports the
+    header error; one above max_block_bytes reports OVERFLOW).
     Returns (out uint8 cuda, out_off int64 cuda [n+1], status int32 cuda [n])."""
     torch = _torch()
     n = block_off.numel() - 1 if n_blocks is None else n_blocks
     dev = blocks.device
-    hdr = block_off[:n].unsqueeze(1) + torch.arange(25, 29, device=dev)
-    raw = blocks[hdr].to(torch.int64)
-    raw_len = raw[:, 0] | (raw[:, 1] << 8) | (raw[:, 2] << 16) | (raw[:, 3] << 24)
     out_off = torch.zeros(n + 1, dtype=torch.int64, device=dev)
-    out_off[1:] = torch.cumsum(raw_len, 0)
+    if n:
+        pws = torch.empty(lib().lsm_lz4_plan_workspace_size(n), dtype=torch.uint8, device=dev)
+        _check(lib().lsm_lz4_plan_output(_ptr(blocks), _ptr(block_off), n, max_block_bytes, _ptr(out_off), _ptr(pws),
+                                         pws.numel(), _stream(stream)), "lsm_lz4_plan_output")
     total = int(out_off[-1].item()) if n else 0
     out = torch.empty(max(total, 1), dtype=torch.uint8, device=dev)
     status = torch.empty(max(n, 1), dtype=torch.int32, device=dev)

@@ -39,9 +39,20 @@ def test_library_exports_every_declared_symbol(L):
     assert set(declared_functions()) == set(L.EXPORTED_SYMBOLS)
 
 
+def test_library_exports_exactly_the_header(L):
+    """nm -D of the product library lists the header's functions and nothing else
+    (no diagnostic entry points, no C++ internals)."""
+    import subprocess
+    out = subprocess.run(["nm", "-D", "--defined-only", str(L.LIB_PATH)], check=True, capture_output=True,
+                         text=True).stdout
+    syms = {line.split()[-1] for line in out.splitlines() if line.strip()}
+    syms = {s for s in syms if not s.startswith("_init") and not s.startswith("_fini")}
+    assert syms == set(declared_functions())
+
+
 def test_abi_version_and_status_names(L):
     lib = L.lib()
-    assert lib.lsm_abi_version() == 1
+    assert lib.lsm_abi_version() == L.ABI_VERSION == 2
     for code, name in L.STATUS.items():
         assert lib.lsm_status_name(code).decode() == name
 
@@ -100,6 +111,41 @@ def test_bad_args_rejected_without_device(L):
     p = L.LsmBlockParams(16, 0, 0, 0, -1.0)  # negative hash ratio (builder.rs:40 asserts)
     assert lib.lsm_encode_blocks(C.byref(it), C.c_void_p(8), 1, C.byref(p), C.c_void_p(16), 100, C.c_void_p(24),
                                  C.c_void_p(32), C.c_void_p(48), 1 << 20, None) == 10
+    for bits in (1, 2, 4, 0x80):  # lsm_block_params.reserved must be 0 (diagnostic ablations are not in the release)
+        p = L.LsmBlockParams(16, 0, 0, bits, 0.0)
+        assert lib.lsm_encode_blocks(C.byref(it), C.c_void_p(8), 1, C.byref(p), C.c_void_p(16), 100, C.c_void_p(24),
+                                     C.c_void_p(32), C.c_void_p(48), 1 << 20, None) == 10
+
+
+def test_decode_tuning_flags_rejected(L):
+    """Only LSM_DECODE_ITEM_START_VALID is a public decode flag: diagnostic bits
+    that would skip the hash, the parse or the stores are LSM_BAD_ARG."""
+    import ctypes as C
+    lib = L.lib()
+    ps = L.LsmParsed()
+    ws = lib.lsm_decode_workspace_size(4)
+    for flags in (0x100, 0x200, 0x400, 0x800, 0x1000, 0x2000, 0x10000, 0x80000, 1 << 31):
+        t = L.LsmDecodeTuning(0, 0, 0, flags)
+        assert lib.lsm_decode_blocks_tuned(C.c_void_p(0x1000), C.c_void_p(0x2000), 4, -1, C.byref(ps), 10,
+                                           C.c_void_p(0x3000), C.c_void_p(0x4000), C.c_void_p(0x5000), ws,
+                                           C.byref(t), None) == 10
+    for bad in ((64, 0, 0, 0), (0, 128, 0, 0), (0, 1 << 17, 0, 0), (0, 0, 9000, 0)):
+        t = L.LsmDecodeTuning(*bad)
+        assert lib.lsm_decode_blocks_tuned(C.c_void_p(0x1000), C.c_void_p(0x2000), 4, -1, C.byref(ps), 10,
+                                           C.c_void_p(0x3000), C.c_void_p(0x4000), C.c_void_p(0x5000), ws,
+                                           C.byref(t), None) == 10
+
+
+def test_point_read_rejects_misaligned_buffers(L):
+    import ctypes as C
+    lib = L.lib()
+    res = L.LsmPointResult(C.c_void_p(0x9000), None, None, None, None)
+    args = [C.c_void_p(0x1000), C.c_void_p(0x2000), 4, C.c_void_p(0x3000), C.c_void_p(0x4000), C.c_void_p(0x5000),
+            C.c_void_p(0x6000), 8, C.byref(res), C.c_void_p(0x7000), None]
+    for i in (0, 4):  # d_blocks, d_needles
+        a = list(args)
+        a[i] = C.c_void_p(0x1000 + 8 * (i + 1))
+        assert lib.lsm_point_read_blocks(*a) == 10
 
 
 def test_product_path_has_no_cpu_fallback(L):

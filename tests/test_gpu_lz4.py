@@ -102,3 +102,31 @@ def test_lz4_status_codes(gpu):
     got, st = _run(gpu, [good, bytes(bad_ck), bytes(bad_hdr), bytes(bad_magic), short])
     assert st == [OK, CKSUM, HDR_CKSUM, BAD_MAGIC, DECOMPRESS]
     assert got[0] == r
+
+
+def test_lz4_corrupt_length_cannot_size_the_output(gpu):
+    """A bit flip in uncompressed_length (header bytes 25-28) is a header-checksum
+    failure, reported per block without the corrupt length sizing the output
+    (Block::from_reader allocates only after Header::decode_from passed,
+    block/mod.rs:91-112).  A verified length above the caller's cap is OVERFLOW;
+    a handle shorter than a header is TRUNCATED."""
+    r = _payloads(52, 16, "counter", 2)
+    good = _frame(lz4_compress(r), len(r))
+    huge = bytearray(good)
+    huge[28] ^= 0x80  # uncompressed_length += 2 GiB, header checksum now stale
+    got, st = _run(gpu, [good, bytes(huge), good])
+    assert st == [OK, HDR_CKSUM, OK] and got[0] == r and got[2] == r and got[1] == b""
+    # a correctly sealed header claiming 1 GiB: within the cap it is sized, above it OVERFLOW
+    import torch
+    big = _frame(lz4_compress(r), 1 << 30)
+    buf = gpu.to_device_bytes(np.frombuffer(big + good, np.uint8))
+    off = torch.tensor([0, len(big), len(big) + len(good)], dtype=torch.int64).cuda()
+    out, out_off, status = gpu.lz4_decompress_blocks(buf, off, max_block_bytes=1 << 20)
+    torch.cuda.synchronize()
+    assert status.cpu().tolist() == [OVERFLOW, OK] and out_off.cpu().tolist() == [0, 0, len(r)]
+    # truncated handles: fewer bytes than a header
+    buf = gpu.to_device_bytes(np.frombuffer(good[:20] + good, np.uint8))
+    off = torch.tensor([0, 20, 20 + len(good)], dtype=torch.int64).cuda()
+    out, out_off, status = gpu.lz4_decompress_blocks(buf, off)
+    torch.cuda.synchronize()
+    assert status.cpu().tolist()[1] == OK and status.cpu().tolist()[0] != OK and int(out_off[1]) == 0

@@ -87,29 +87,16 @@ def test_decode_golden_blocks(gpu, golden_blocks):
             assert pyoracle.materialize(payload, one, case["restart_interval"]) == case_expected_items(case), case["name"]
 
 
-LEG = 0x10000  # LSM_DECODE_LEGACY
-RING = 0x80000  # LSM_DECODE_RING
-DBL = 0x40000  # LSM_DECODE_DOUBLE
-SPLIT = 0x100000  # LSM_DECODE_SPLIT_WALK
-# (blocks_per_wave, slot/stage bytes, tile items, flags, ring slots, planners, hashers, loaders)
-TUNINGS = [None,                                 # library default kernel
-           (0, 0, 0, RING),                      # ring defaults
-           (0, 256, 64, RING),                   # every block larger than a slot: general path
-           (0, 4096, 64, RING, 8, 1, 1),         # 8 small slots, 1 planner, 1 hasher, 10 parsers
-           (0, 65536, 1024, RING, 2, 5, 6),      # 2 x 64 KiB slots, 1 parser
-           (0, 32768, 512, RING, 4, 2, 2, 8),    # 8 loader waves
-           (0, 32768, 512, RING, 3, 3, 3, 1),    # a single loader wave
-           (0, 32768, 512, RING | 0x20000, 3),   # nt DMA, 3 slots
-           (0, 16384, 256, RING, 2, 1, 1),       # 2-slot ring
-           (48, 65536, 1024, LEG), (1, 256, 64, LEG), (63, 65536, 2048, LEG),
-           (48, 32768, 512, LEG | DBL), (48, 65536, 1024, LEG | DBL), (1, 256, 64, LEG | DBL), (5, 4096, 64, LEG | DBL),
-           (48, 65536, 1024, LEG | SPLIT), (3, 8192, 128, LEG | SPLIT), (48, 32768, 512, LEG | DBL | SPLIT)]
+# (blocks_per_wave, stage bytes, tile items[, flags])
+TUNINGS = [None,                                 # library defaults
+           (48, 65536, 1024), (1, 256, 64),      # 64 KiB stage; every block larger than the stage: general path
+           (63, 65536, 2048), (5, 4096, 64), (3, 8192, 128), (8, 32768, 512)]
 
 
 @pytest.mark.parametrize("tuning", TUNINGS)
 def test_decode_golden_blocks_tunings(gpu, golden_blocks, tuning):
-    """Ring kernel under several slot/role shapes, the general path (tiny
-    slots) and the legacy single-stage kernel all agree with the oracle."""
+    """The group kernel under several stage / group shapes and the general path
+    (tiny stages) all agree with the oracle."""
     blocks = [bytes.fromhex(c["block"]) for c in golden_blocks]
     buf, off = pack(blocks)
     g = gpu_decode(gpu, buf, off, tuning=tuning)
@@ -299,7 +286,7 @@ def test_structurally_broken_payloads_with_valid_checksums(gpu):
             payload = payload[:rng.randint(0, 40)]
         blocks.append(pyoracle.block_write(bytes(payload)))
     buf, off = pack(blocks)
-    for tuning in (None, (1, 256, 64), (48, 65536, 1024, LEG | SPLIT)):
+    for tuning in (None, (1, 256, 64), (48, 65536, 1024)):
         g = gpu_decode(gpu, buf, off, tuning=tuning)
         parsed, item_start, status = pyoracle.decode_blocks(buf, off)
         compare_decode(g, parsed, item_start, status)
@@ -394,6 +381,6 @@ def test_resealed_mutation_fuzz(gpu):
     blocks = off[1:]
     parsed, item_start, status = pyoracle.decode_blocks(buf, off)
     assert (status == 0).sum() > len(blocks) // 4 and (status == 5).sum() > len(blocks) // 10
-    for tuning in (None, (1, 256, 64), (8, 8192, 256), (8, 8192, 256, LEG | SPLIT), (48, 65536, 1024, LEG | SPLIT)):
+    for tuning in (None, (1, 256, 64), (8, 8192, 256), (48, 65536, 1024)):
         g = gpu_decode(gpu, buf, off, tuning=tuning)
         compare_decode(g, parsed, item_start, status)
