@@ -23,6 +23,7 @@
  *   lsm_cut_blocks     <- Writer::write chunking   src/table/writer/mod.rs:243-296
  *   lsm_xxh3_128_batch <- hash128                  src/hash.rs:7-9 (checksum of arbitrary byte ranges)
  *   lsm_point_read_blocks <- DataBlock::point_read src/table/data_block/mod.rs:412-472
+ *   lsm_seek_blocks    <- data_block::Iter::seek / seek_upper (+ _exclusive)  data_block/iter.rs:37-176
  *   lsm_xxh3_128_file  <- ChecksummedWriter         src/checksum.rs:59-96 (whole-file checksum)
  *   lsm_lz4_decompress_blocks <- Block::from_reader/from_file, CompressionType::Lz4  block/mod.rs:87-182
  *   lsm_lz4_plan_output <- the builder_unzeroed(uncompressed_length) sizing of the same  block/mod.rs:104-112
@@ -218,6 +219,30 @@ int lsm_point_read_blocks(const uint8_t* d_blocks, const uint64_t* d_block_off, 
                           const uint32_t* d_query_block, const uint8_t* d_needles,
                           const uint64_t* d_needle_off, const uint64_t* d_snapshot, uint32_t n_queries,
                           const lsm_point_result* d_out, int32_t* d_status, void* stream);
+
+/* ---- range seek ------------------------------------------------------------
+ * Batched data-block iterator bounds: Iter::seek / seek_exclusive (lower bound)
+ * and Iter::seek_upper / seek_upper_exclusive (upper bound),
+ * src/table/data_block/iter.rs:37-176 over Decoder::partition_point
+ * (block/decoder.rs:153-207), the per-block step of Table::range
+ * (src/table/mod.rs:391-422).  Query q seeks block d_query_block[q] (same
+ * buffer rules as lsm_point_read_blocks) with the lower bound
+ * d_lo[d_lo_off[q] .. d_lo_off[q+1]) and the upper bound
+ * d_hi[d_hi_off[q] .. d_hi_off[q+1]) (arenas 16-byte aligned, readable
+ * LSM_INPUT_PADDING bytes past their end), d_flags[q] saying which apply.
+ * Result: items [d_first[q], d_end[q]) in block order (the rows
+ * lsm_decode_blocks gives them) are exactly what next(), next_back() or any
+ * mix of them yields; d_found[q] bit 0 / bit 1 = the return value of the lower
+ * / upper seek (needle present, or for the exclusive forms: an item beyond
+ * it).  d_status[q] as for lsm_point_read_blocks. */
+#define LSM_SEEK_LO 1u            /* apply the lower bound */
+#define LSM_SEEK_HI 2u            /* apply the upper bound */
+#define LSM_SEEK_LO_EXCLUSIVE 4u  /* seek_exclusive: skip keys equal to the lower bound */
+#define LSM_SEEK_HI_EXCLUSIVE 8u  /* seek_upper_exclusive: skip keys equal to the upper bound */
+int lsm_seek_blocks(const uint8_t* d_blocks, const uint64_t* d_block_off, uint32_t n_blocks,
+                    const uint32_t* d_query_block, const uint8_t* d_lo, const uint64_t* d_lo_off,
+                    const uint8_t* d_hi, const uint64_t* d_hi_off, const uint8_t* d_flags, uint32_t n_queries,
+                    uint32_t* d_first, uint32_t* d_end, uint8_t* d_found, int32_t* d_status, void* stream);
 
 /* ---- standard Bloom filter (src/table/filter/standard_bloom/) ---------------
  * The filter is the exact byte image of Builder::build (builder.rs:33-53):

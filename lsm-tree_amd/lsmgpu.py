@@ -109,6 +109,10 @@ def lib():
         L.lsm_point_read_blocks.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p,
                                             C.c_void_p, C.c_uint32, C.POINTER(LsmPointResult), C.c_void_p,
                                             C.c_void_p]
+        L.lsm_seek_blocks.restype = C.c_int
+        L.lsm_seek_blocks.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p,
+                                      C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p,
+                                      C.c_void_p, C.c_void_p, C.c_void_p]
         L.lsm_bloom_calculate_m.restype = C.c_uint64
         L.lsm_bloom_calculate_m.argtypes = [C.c_uint64, C.c_float]
         L.lsm_bloom_shape.restype = C.c_int
@@ -142,7 +146,7 @@ EXPORTED_SYMBOLS = ["lsm_abi_version", "lsm_status_name", "lsm_last_error", "lsm
                     "lsm_point_read_blocks", "lsm_xxh3_128_file_workspace_size", "lsm_xxh3_128_file",
                     "lsm_bloom_calculate_m", "lsm_bloom_shape", "lsm_bloom_filter_size", "lsm_hash64_keys",
                     "lsm_bloom_build", "lsm_bloom_contains", "lsm_lz4_workspace_size", "lsm_lz4_decompress_blocks",
-                    "lsm_lz4_plan_workspace_size", "lsm_lz4_plan_output"]
+                    "lsm_lz4_plan_workspace_size", "lsm_lz4_plan_output", "lsm_seek_blocks"]
 
 
 def _check(rc, what):
@@ -309,6 +313,28 @@ def point_read(blocks, block_off, n_blocks, query_block, needles, needle_off, sn
     _check(lib().lsm_point_read_blocks(_ptr(blocks), _ptr(block_off), n_blocks, _ptr(query_block), _ptr(needles),
                                        _ptr(needle_off), _ptr(snapshot), n, C.byref(res), _ptr(out["status"]),
                                        _stream(stream)), "lsm_point_read_blocks")
+    return out
+
+
+SEEK_LO, SEEK_HI, SEEK_LO_EXCLUSIVE, SEEK_HI_EXCLUSIVE = 1, 2, 4, 8
+
+
+def seek(blocks, block_off, n_blocks, query_block, lo, lo_off, hi, hi_off, flags, stream=None):
+    """Batched data_block::Iter::seek / seek_upper (+ exclusive) (data_block/iter.rs:37-176).
+    All inputs cuda tensors: blocks uint8 (padded), block_off int64 [n_blocks+1], query_block
+    int32 [n], lo / hi uint8 padded arenas with int64 [n+1] offsets, flags uint8 [n]
+    (SEEK_* bits).  Returns dict first/end (int32: item range in block order), found
+    (uint8: bit 0 lower, bit 1 upper seek's return value), status."""
+    torch = _torch()
+    n = int(query_block.numel())
+    dev = blocks.device
+    out = {"first": torch.empty(max(n, 1), dtype=torch.int32, device=dev),
+           "end": torch.empty(max(n, 1), dtype=torch.int32, device=dev),
+           "found": torch.empty(max(n, 1), dtype=torch.uint8, device=dev),
+           "status": torch.empty(max(n, 1), dtype=torch.int32, device=dev)}
+    _check(lib().lsm_seek_blocks(_ptr(blocks), _ptr(block_off), n_blocks, _ptr(query_block), _ptr(lo), _ptr(lo_off),
+                                 _ptr(hi), _ptr(hi_off), _ptr(flags), n, _ptr(out["first"]), _ptr(out["end"]),
+                                 _ptr(out["found"]), _ptr(out["status"]), _stream(stream)), "lsm_seek_blocks")
     return out
 
 

@@ -121,6 +121,27 @@ static void write_trailer(sink* s, uint8_t ri, const uint32_t* bin, uint32_t bin
     s_u32(s, item_count);
 }
 
+/* hash_index::Builder::set (hash_index/builder.rs:64-110): FREE -> idx, same idx
+ * -> kept, a different idx -> CONFLICT (sticky); bucket = hash64(key) % buckets
+ * (hash_index/mod.rs:35-41). */
+static void hash_set(uint8_t* hash, uint32_t buckets, const uint8_t* key, size_t klen, uint8_t idx) {
+    uint32_t pos = (uint32_t)(orc_xxh3_64(key, klen) % buckets);
+    uint8_t cur = hash[pos];
+    if (cur == HASH_FREE) hash[pos] = idx;
+    else if (cur != HASH_CONFLICT && cur != idx) hash[pos] = HASH_CONFLICT;
+}
+
+void orc_hash_index_build(const uint8_t* keys, const uint64_t* key_off, const uint8_t* idx, uint64_t n,
+                          uint32_t buckets, uint8_t* out) {
+    memset(out, HASH_FREE, buckets);              /* Builder::with_bucket_count, builder.rs:20-36 */
+    for (uint64_t i = 0; i < n; ++i)
+        hash_set(out, buckets, keys + key_off[i], (size_t)(key_off[i + 1] - key_off[i]), idx[i]);
+}
+
+uint8_t orc_hash_index_get(const uint8_t* bytes, uint32_t buckets, const uint8_t* key, size_t klen) {
+    return bytes[orc_xxh3_64(key, klen) % buckets];  /* hash_index/reader.rs:46-58 */
+}
+
 int64_t orc_data_block_encode(const orc_items* it, uint64_t first, uint64_t count,
                               uint8_t ri, float ratio, uint8_t* out, size_t cap) {
     if (count == 0 || ri == 0 || signbit(ratio)) return -ORC_BAD_ARG; /* mod.rs:530, encoder.rs:91, builder.rs:40 */
@@ -160,12 +181,8 @@ int64_t orc_data_block_encode(const orc_items* it, uint64_t first, uint64_t coun
             s_put(&s, val, vlen);
         }
         uint32_t restart_idx = bin_len - 1;
-        if (buckets > 0 && restart_idx < HASH_MAX_POINTERS) {  /* encoder.rs:148-154 */
-            uint32_t pos = (uint32_t)(orc_xxh3_64(key, klen) % buckets);  /* hash_index/mod.rs:35-41 */
-            uint8_t cur = hash[pos];                   /* builder.rs:64-110 */
-            if (cur == HASH_FREE) hash[pos] = (uint8_t)restart_idx;
-            else if (cur != HASH_CONFLICT && cur != (uint8_t)restart_idx) hash[pos] = HASH_CONFLICT;
-        }
+        if (buckets > 0 && restart_idx < HASH_MAX_POINTERS)  /* encoder.rs:148-154 */
+            hash_set(hash, buckets, key, klen, (uint8_t)restart_idx);
     }
     write_trailer(&s, ri, bin, bin_len, hash, buckets, (uint32_t)count);
     free(bin);
@@ -213,6 +230,20 @@ int64_t orc_block_write(const uint8_t* payload, size_t len, uint8_t block_type, 
     put32(out + 29, (uint32_t)hlo);
     memmove(out + HDR_LEN, payload, len);
     return (int64_t)(HDR_LEN + len);
+}
+
+/* Header::encode_into (header.rs:80-112) of arbitrary field values. */
+void orc_header_encode(uint8_t block_type, uint64_t ck_lo, uint64_t ck_hi, uint32_t data_length,
+                       uint32_t uncompressed_length, uint8_t* out) {
+    out[0] = 'L'; out[1] = 'S'; out[2] = 'M'; out[3] = 3;
+    out[4] = block_type;
+    put64(out + 5, ck_lo);
+    put64(out + 13, ck_hi);
+    put32(out + 21, data_length);
+    put32(out + 25, uncompressed_length);
+    uint64_t hlo, hhi;
+    orc_xxh3_128(out, 29, &hlo, &hhi);
+    put32(out + 29, (uint32_t)hlo);
 }
 
 int orc_header_decode(const uint8_t* buf, size_t len, orc_header* h) {
@@ -439,10 +470,18 @@ int64_t orc_data_block_point_read(const uint8_t* p, size_t len, const uint8_t* n
     uint64_t start = 0;
     int use_search = 1;
     if (t.hash_len > 0) {
+        /* the bucket bytes lie before the trailer (trailer.rs:100-111); a bucket naming a
+         * restart interval the block does not have is malformed (the reference would index
+         * past its binary index and panic) */
+        if ((uint64_t)t.hash_off + t.hash_len > len - TRAILER_LEN) { result = -2; goto done; }
         uint32_t pos = (uint32_t)(orc_xxh3_64(needle, nn) % t.hash_len);
         uint8_t m = p[t.hash_off + pos];
         if (m == HASH_FREE) { result = -1; goto done; }
-        if (m != HASH_CONFLICT) { start = (uint64_t)m * t.ri; use_search = 0; }
+        if (m != HASH_CONFLICT) {
+            if (m >= t.bin_len) { result = -2; goto done; }
+            start = (uint64_t)m * t.ri;
+            use_search = 0;
+        }
     }
     if (use_search) {
         uint32_t lo = 0, hi = t.bin_len;
@@ -469,6 +508,79 @@ int64_t orc_data_block_point_read(const uint8_t* p, size_t len, const uint8_t* n
 done:
     free(sq); free(ko); free(kl); free(pl);
     return result;
+}
+
+/* Iter::seek / seek_exclusive / seek_upper / seek_upper_exclusive
+ * (data_block/iter.rs:37-176) over Decoder::partition_point (decoder.rs:153-207):
+ * the restart interval is found by binary search over the restart heads, then a
+ * linear scan (forward for the lower bound, backward from the interval's last
+ * item for the upper bound) stops at the first key that ends the bound.  Result
+ * = the item range [first, end) every iteration order yields, plus the two
+ * return values.  Returns 0 or -status (malformed block). */
+int orc_data_block_seek(const uint8_t* p, size_t len, const uint8_t* lo, size_t lo_len, const uint8_t* hi,
+                        size_t hi_len, uint32_t flags, uint32_t* first, uint32_t* end, uint32_t* found) {
+    trailer_info t;
+    if (read_trailer(p, len, &t)) return -ORC_PARSE;
+    uint64_t n = t.item_count;
+    uint64_t* sq = (uint64_t*)malloc(8 * (n ? n : 1));
+    uint32_t* ko = (uint32_t*)malloc(4 * (n ? n : 1));
+    uint16_t* kl = (uint16_t*)malloc(2 * (n ? n : 1));
+    uint16_t* pl = (uint16_t*)malloc(2 * (n ? n : 1));
+    orc_parsed o;
+    memset(&o, 0, sizeof o);
+    o.seqno = sq; o.key_off = ko; o.key_len = kl; o.prefix_len = pl;
+    int rc = 0;
+    if (orc_data_block_decode(p, len, &o, 0, n) < 0) { rc = -ORC_PARSE; goto done; }
+    uint64_t a = 0, b = n;
+    uint32_t f = 0;
+#define KEY_CMP(i, nd, nn) (((i) % t.ri == 0) ? cmp_bytes(p + ko[i], kl[i], nd, nn) \
+        : cmp_prefixed(p + ko[((i) / t.ri) * t.ri], pl[i], p + ko[i], kl[i], nd, nn))
+    if (flags & ORC_SEEK_LO) {
+        /* partition_point(head < needle): last such head, else interval 0 */
+        uint32_t l = 0, r = t.bin_len;
+        while (l < r) {
+            uint32_t mid = l + (r - l) / 2;
+            uint64_t h = (uint64_t)mid * t.ri;
+            if (cmp_bytes(p + ko[h], kl[h], lo, lo_len) < 0) l = mid + 1; else r = mid;
+        }
+        uint32_t iv = l == 0 ? 0 : (l == t.bin_len ? t.bin_len - 1 : l - 1);
+        uint64_t i = (uint64_t)iv * t.ri;
+        const int excl = (flags & ORC_SEEK_LO_EXCL) != 0;
+        for (; i < n; ++i) {
+            int c = KEY_CMP(i, lo, lo_len);
+            if (!excl && c == 0) { f |= 1; break; }   /* Equal -> true */
+            if (c > 0) { if (excl) f |= 1; break; }  /* Greater -> false (exclusive: true) */
+        }
+        a = i;
+    }
+    if (flags & ORC_SEEK_HI) {
+        /* partition_point(head <= needle): last such head, else interval 0 */
+        uint32_t l = 0, r = t.bin_len;
+        while (l < r) {
+            uint32_t mid = l + (r - l) / 2;
+            uint64_t h = (uint64_t)mid * t.ri;
+            if (cmp_bytes(p + ko[h], kl[h], hi, hi_len) <= 0) l = mid + 1; else r = mid;
+        }
+        uint32_t iv = l == 0 ? 0 : (l == t.bin_len ? t.bin_len - 1 : l - 1);
+        uint64_t last = (uint64_t)(iv + 1) * t.ri;
+        if (last > n) last = n;
+        const int excl = (flags & ORC_SEEK_HI_EXCL) != 0;
+        uint64_t e = last;  /* one past the item the backward scan stops at */
+        for (; e > 0; --e) {
+            int c = KEY_CMP(e - 1, hi, hi_len);
+            if (!excl && c == 0) { f |= 2; break; }   /* Equal -> true */
+            if (c < 0) { if (excl) f |= 2; break; }  /* Less -> false (exclusive: true) */
+        }
+        b = e;
+    }
+#undef KEY_CMP
+    if (a > b) a = b;  /* the scanners crossed: an empty range */
+    *first = (uint32_t)a;
+    *end = (uint32_t)b;
+    *found = f;
+done:
+    free(sq); free(ko); free(kl); free(pl);
+    return rc;
 }
 
 uint64_t orc_cut_blocks(const orc_items* it, uint32_t block_size, uint32_t* starts,

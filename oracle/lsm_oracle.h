@@ -123,6 +123,27 @@ int64_t orc_index_block_decode(const uint8_t* payload, size_t len, orc_parsed* o
 int64_t orc_data_block_point_read(const uint8_t* payload, size_t len,
                                   const uint8_t* needle, size_t needle_len, uint64_t snapshot_seqno);
 
+/* Iter::seek / seek_upper (+ _exclusive) (data_block/iter.rs:37-176): item range
+ * [*first, *end) that iteration yields after the given bounds, *found bit 0 =
+ * the lower seek's return value, bit 1 = the upper seek's.  0 or -status. */
+#define ORC_SEEK_LO 1u
+#define ORC_SEEK_HI 2u
+#define ORC_SEEK_LO_EXCL 4u
+#define ORC_SEEK_HI_EXCL 8u
+int orc_data_block_seek(const uint8_t* payload, size_t len, const uint8_t* lo, size_t lo_len,
+                        const uint8_t* hi, size_t hi_len, uint32_t flags, uint32_t* first,
+                        uint32_t* end, uint32_t* found);
+
+/* hash_index::Builder (hash_index/builder.rs:20-110): n set(key, idx) calls into
+ * `buckets` bytes; Reader::get (hash_index/reader.rs:46-58). */
+void orc_hash_index_build(const uint8_t* keys, const uint64_t* key_off, const uint8_t* idx, uint64_t n,
+                          uint32_t buckets, uint8_t* out);
+uint8_t orc_hash_index_get(const uint8_t* bytes, uint32_t buckets, const uint8_t* key, size_t klen);
+
+/* Header::encode_into (header.rs:80-112) of arbitrary field values (33 bytes). */
+void orc_header_encode(uint8_t block_type, uint64_t ck_lo, uint64_t ck_hi, uint32_t data_length,
+                       uint32_t uncompressed_length, uint8_t* out);
+
 /* Writer::write chunking (src/table/writer/mod.rs:243-296): block cut when
  * sum(key.len()+value.len()) >= block_size.  Writes n_blocks+1 starts;
  * returns n_blocks. */

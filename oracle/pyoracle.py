@@ -96,6 +96,15 @@ def lib():
         L.orc_bloom_build.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64, C.c_uint64, C.c_void_p]
         L.orc_bloom_contains.restype = C.c_int
         L.orc_bloom_contains.argtypes = [C.c_void_p, C.c_uint64, C.c_uint64]
+        L.orc_data_block_seek.restype = C.c_int
+        L.orc_data_block_seek.argtypes = [C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t, C.c_void_p, C.c_size_t,
+                                          C.c_uint32, u32p, u32p, u32p]
+        L.orc_hash_index_build.restype = None
+        L.orc_hash_index_build.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p]
+        L.orc_hash_index_get.restype = C.c_uint8
+        L.orc_hash_index_get.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_size_t]
+        L.orc_header_encode.restype = None
+        L.orc_header_encode.argtypes = [C.c_uint8, C.c_uint64, C.c_uint64, C.c_uint32, C.c_uint32, C.c_void_p]
         L.orc_lz4_decompress.restype = C.c_int64
         L.orc_lz4_decompress.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_uint64]
         _lib = L
@@ -311,6 +320,48 @@ def point_read(payload: bytes, needle: bytes, snapshot: int) -> int:
     a = np.frombuffer(payload, np.uint8)
     nd = np.frombuffer(needle, np.uint8) if needle else np.zeros(1, np.uint8)
     return int(lib().orc_data_block_point_read(_ptr(a), len(payload), _ptr(nd), len(needle), snapshot))
+
+
+SEEK_LO, SEEK_HI, SEEK_LO_EXCL, SEEK_HI_EXCL = 1, 2, 4, 8
+
+
+def _arr(b: bytes):
+    return np.frombuffer(b, np.uint8) if b else np.zeros(1, np.uint8)
+
+
+def seek(payload: bytes, lo: bytes | None = None, hi: bytes | None = None, lo_excl=False, hi_excl=False):
+    """Iter::seek / seek_upper (+ exclusive forms) (data_block/iter.rs:37-176) ->
+    (first, end, lo_found, hi_found) or None for a malformed block."""
+    flags = (SEEK_LO if lo is not None else 0) | (SEEK_HI if hi is not None else 0) | \
+            (SEEK_LO_EXCL if lo_excl else 0) | (SEEK_HI_EXCL if hi_excl else 0)
+    a, la, b, lb = _arr(lo or b""), len(lo or b""), _arr(hi or b""), len(hi or b"")
+    first, end, found = C.c_uint32(), C.c_uint32(), C.c_uint32()
+    rc = lib().orc_data_block_seek(_ptr(_arr(payload)), len(payload), _ptr(a), la, _ptr(b), lb, flags,
+                                   C.byref(first), C.byref(end), C.byref(found))
+    if rc:
+        return None
+    return first.value, end.value, bool(found.value & 1), bool(found.value & 2)
+
+
+def hash_index_build(keys: list, idx: list, buckets: int) -> bytes:
+    """hash_index::Builder::with_bucket_count(buckets) + set(key, idx)... + into_inner."""
+    kb = b"".join(keys)
+    ko = np.concatenate([[0], np.cumsum([len(k) for k in keys])]).astype(np.uint64)
+    ix = np.array(idx, np.uint8) if idx else np.zeros(1, np.uint8)
+    out = np.zeros(max(buckets, 1), np.uint8)
+    lib().orc_hash_index_build(_ptr(_arr(kb)), _ptr(ko), _ptr(ix), len(keys), buckets, _ptr(out))
+    return out[:buckets].tobytes()
+
+
+def hash_index_get(bytes_: bytes, key: bytes) -> int:
+    return lib().orc_hash_index_get(_ptr(_arr(bytes_)), len(bytes_), _ptr(_arr(key)), len(key))
+
+
+def header_encode(block_type: int, checksum: int, data_length: int, uncompressed_length: int) -> bytes:
+    out = np.zeros(33, np.uint8)
+    lib().orc_header_encode(block_type, checksum & (2 ** 64 - 1), checksum >> 64, data_length, uncompressed_length,
+                            _ptr(out))
+    return out.tobytes()
 
 
 def cut_blocks(items: Items, block_size: int) -> np.ndarray:

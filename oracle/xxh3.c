@@ -12,6 +12,9 @@
 #include "lsm_oracle.h"
 
 #include <string.h>
+#ifdef __AVX2__
+#include <immintrin.h>
+#endif
 
 static const uint8_t kSecret[192] = {
     0xb8, 0xfe, 0x6c, 0x39, 0x23, 0xa4, 0x4b, 0xbe, 0x7c, 0x01, 0x81, 0x2c, 0xf7, 0x21, 0xad, 0x1c,
@@ -93,7 +96,7 @@ static uint64_t mix16(const uint8_t* in, const uint8_t* sec, uint64_t seed) {
 }
 
 /* long-input accumulation (> 240 B): stripes of 64 B, 16 stripes per 1 KiB block */
-static void accumulate_512(uint64_t acc[8], const uint8_t* in, const uint8_t* sec) {
+__attribute__((unused)) static void accumulate_512(uint64_t acc[8], const uint8_t* in, const uint8_t* sec) {
     for (int i = 0; i < 8; ++i) {
         uint64_t v = rd64(in + 8 * i);
         uint64_t k = v ^ rd64(sec + 8 * i);
@@ -101,7 +104,7 @@ static void accumulate_512(uint64_t acc[8], const uint8_t* in, const uint8_t* se
         acc[i] += (uint64_t)(uint32_t)k * (k >> 32);
     }
 }
-static void scramble(uint64_t acc[8], const uint8_t* sec) {
+__attribute__((unused)) static void scramble(uint64_t acc[8], const uint8_t* sec) {
     for (int i = 0; i < 8; ++i) {
         uint64_t a = acc[i];
         a ^= a >> 47;
@@ -110,6 +113,34 @@ static void scramble(uint64_t acc[8], const uint8_t* sec) {
         acc[i] = a;
     }
 }
+#ifdef __AVX2__
+/* The same two steps on 4 accumulators per 256-bit vector: XXH3's published
+ * AVX2 kernels (the SIMD path xxhash-rust takes), so the cpu_baseline leg is
+ * not handicapped by a scalar hash.  Identical results (tests/test_oracle.py KATs). */
+#define accumulate_512 accumulate_512_avx2
+#define scramble scramble_avx2
+static void accumulate_512_avx2(uint64_t acc[8], const uint8_t* in, const uint8_t* sec) {
+    for (int i = 0; i < 2; ++i) {
+        __m256i a = _mm256_loadu_si256((const __m256i*)(acc + 4 * i));
+        const __m256i d = _mm256_loadu_si256((const __m256i*)(in + 32 * i));
+        const __m256i k = _mm256_xor_si256(d, _mm256_loadu_si256((const __m256i*)(sec + 32 * i)));
+        const __m256i prod = _mm256_mul_epu32(k, _mm256_shuffle_epi32(k, _MM_SHUFFLE(0, 3, 0, 1)));
+        a = _mm256_add_epi64(a, _mm256_shuffle_epi32(d, _MM_SHUFFLE(1, 0, 3, 2)));
+        _mm256_storeu_si256((__m256i*)(acc + 4 * i), _mm256_add_epi64(a, prod));
+    }
+}
+static void scramble_avx2(uint64_t acc[8], const uint8_t* sec) {
+    const __m256i prime = _mm256_set1_epi32((int)P32_1);
+    for (int i = 0; i < 2; ++i) {
+        __m256i a = _mm256_loadu_si256((const __m256i*)(acc + 4 * i));
+        a = _mm256_xor_si256(a, _mm256_srli_epi64(a, 47));
+        a = _mm256_xor_si256(a, _mm256_loadu_si256((const __m256i*)(sec + 32 * i)));
+        const __m256i lo = _mm256_mul_epu32(a, prime);
+        const __m256i hi = _mm256_mul_epu32(_mm256_shuffle_epi32(a, _MM_SHUFFLE(0, 3, 0, 1)), prime);
+        _mm256_storeu_si256((__m256i*)(acc + 4 * i), _mm256_add_epi64(lo, _mm256_slli_epi64(hi, 32)));
+    }
+}
+#endif
 static void hash_long(uint64_t acc[8], const uint8_t* in, size_t len) {
     const size_t stripes_per_block = (192 - 64) / 8; /* 16 */
     const size_t block_len = 64 * stripes_per_block; /* 1024 */

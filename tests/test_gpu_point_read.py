@@ -101,3 +101,86 @@ def test_point_read_status(gpu):
     res = _run(gpu, pbuf, poff, [(0, k, 1 << 63), (1, k, 1 << 63), (2, k, 1 << 63)])
     assert list(res["status"]) == [0, 7, 5]
     assert int(res["item"][0]) == 0 and int(res["item"][1]) == -1 and int(res["item"][2]) == -1
+
+
+def test_point_read_corrupt_hash_index(gpu):
+    """Blocks whose hash index (bucket bytes, or the trailer's hash_len / hash_off)
+    is corrupted and re-sealed with a valid checksum: a bucket naming a restart
+    interval the block does not have, or a bucket region past the trailer, is
+    PARSE (the reference would index out of range and panic); any other bucket
+    value sends the scan to that interval, as the reference's seek does.  GPU
+    status and hit index equal the oracle's (-2 = its parse error)."""
+    rng = random.Random(77)
+    items = random_sorted_items(400, seed=3, kmin=2, kmax=8, vmax=30)
+    starts = np.array(list(range(0, 400, 40)) + [400], np.uint32)
+    blocks, queries = [], []
+    for b in range(len(starts) - 1):
+        one = pyoracle.Items(items.keys, items.key_off, items.vals, items.val_off, items.seqno, items.vtype)
+        payload = bytearray(pyoracle.data_block_encode(one, int(starts[b]), 40, restart_interval=4, hash_ratio=1.5))
+        tr = len(payload) - 31
+        hash_len = int.from_bytes(payload[tr + 10:tr + 14], "little")
+        hash_off = int.from_bytes(payload[tr + 14:tr + 18], "little")
+        assert hash_len > 0
+        kind = b % 4
+        if kind == 0:    # buckets -> restart indexes beyond bin_len, or other valid ones
+            for _ in range(hash_len // 2):
+                payload[hash_off + rng.randrange(hash_len)] = rng.choice([11, 12, 50, 200, 0, 1, 5])
+        elif kind == 1:  # bucket region runs into the trailer
+            payload[tr + 10:tr + 14] = (hash_len + rng.randint(1, 40)).to_bytes(4, "little")
+        elif kind == 2:  # hash_off moved
+            payload[tr + 14:tr + 18] = (hash_off + rng.choice([-3, 5, 1000])).to_bytes(4, "little", signed=True)
+        blocks.append(pyoracle.block_write(bytes(payload)))
+        for i in range(int(starts[b]), int(starts[b + 1])):
+            k = bytes(items.keys[int(items.key_off[i]):int(items.key_off[i + 1])])
+            queries.append((b, k, 1 << 63))
+    buf, off = pack(blocks)
+    res = _run(gpu, buf, off, queries)
+    for q, (b, needle, snap) in enumerate(queries):
+        payload = bytes(buf[int(off[b]) + 33:int(off[b + 1])])
+        exp = pyoracle.point_read(payload, needle, (1 << 63) - 1)
+        if exp == -2:
+            assert int(res["status"][q]) == 5, (q, b)
+        else:
+            assert int(res["status"][q]) == 0 and int(res["item"][q]) == exp, (q, b, exp, int(res["item"][q]))
+
+
+@pytest.mark.parametrize("ri", [1, 3, 16])
+def test_seek_random_bounds(gpu, ri):
+    """lsm_seek_blocks vs the oracle's Iter::seek / seek_upper restatement on random
+    MVCC blocks (few distinct keys, so equal keys span restart intervals), random
+    bounds (present keys, absent keys, empty needles) and every flag combination
+    including the exclusive forms (data_block/iter.rs:37-176)."""
+    import torch
+    rng = random.Random(ri)
+    items = random_sorted_items(700, seed=50 + ri, kmin=1, kmax=5, alphabet=b"abcd", vmax=20)
+    starts = [0]
+    while starts[-1] < items.n:
+        starts.append(min(items.n, starts[-1] + rng.randint(1, 70)))
+    starts = np.array(starts, np.uint32)
+    buf, off = pyoracle.encode_blocks(items, starts, restart_interval=ri, hash_ratio=rng.choice([0.0, 1.33]))
+    qs = []
+    for _ in range(3000):
+        b = rng.randrange(len(starts) - 1)
+
+        def bound():
+            if rng.random() < 0.6:
+                i = rng.randrange(items.n)
+                return bytes(items.keys[int(items.key_off[i]):int(items.key_off[i + 1])])
+            return bytes(rng.choice(b"abcde") for _ in range(rng.randint(0, 5)))
+        qs.append((b, bound(), bound(), rng.randrange(16)))
+    lo, loff = np.frombuffer(b"".join(q[1] for q in qs) or b"\0", np.uint8), np.zeros(len(qs) + 1, np.int64)
+    loff[1:] = np.cumsum([len(q[1]) for q in qs])
+    hi, hoff = np.frombuffer(b"".join(q[2] for q in qs) or b"\0", np.uint8), np.zeros(len(qs) + 1, np.int64)
+    hoff[1:] = np.cumsum([len(q[2]) for q in qs])
+    res = gpu.seek(gpu.to_device_bytes(buf), torch.from_numpy(off.astype(np.int64)).cuda(), len(starts) - 1,
+                   torch.tensor([q[0] for q in qs], dtype=torch.int32).cuda(), gpu.to_device_bytes(lo),
+                   torch.from_numpy(loff).cuda(), gpu.to_device_bytes(hi), torch.from_numpy(hoff).cuda(),
+                   torch.tensor([q[3] for q in qs], dtype=torch.uint8).cuda())
+    torch.cuda.synchronize()
+    res = {k: v.cpu().numpy() for k, v in res.items()}
+    assert (res["status"][:len(qs)] == 0).all()
+    for q, (b, lb, hb, fl) in enumerate(qs):
+        payload = bytes(buf[int(off[b]) + 33:int(off[b + 1])])
+        exp = pyoracle.seek(payload, lb if fl & 1 else None, hb if fl & 2 else None, bool(fl & 4), bool(fl & 8))
+        got = (int(res["first"][q]), int(res["end"][q]), bool(res["found"][q] & 1), bool(res["found"][q] & 2))
+        assert got == exp, (q, b, lb, hb, fl, got, exp)

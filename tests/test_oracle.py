@@ -219,3 +219,19 @@ def test_decode_rejects_corruption(oracle):
     bad[0] = 9  # invalid value type at the first record
     blk2 = oracle.block_write(bytes(bad))
     assert oracle.decode_blocks(np.frombuffer(blk2, np.uint8), np.array([0, len(blk2)], np.uint64))[2][0] == 5
+
+
+def test_oracle_asan():
+    """The oracle under ASan/UBSan on the host: oracle/fuzz_driver.c
+    runs seeded data_block fuzz properties (fuzz/data_block/src/main.rs:130-323:
+    round trip, materialize == input, every point_read) plus re-sealed byte-flip
+    mutations, truncated handles, random LZ4 streams and every XXH3 length class;
+    any sanitizer report or failed property is a non-zero exit."""
+    import subprocess
+    from pathlib import Path
+    oracle_dir = Path(__file__).resolve().parent.parent / "oracle"
+    subprocess.run(["make", "-s", "-C", str(oracle_dir), "asan"], check=True)
+    for seed in ("0x5EED", "0xC0FFEE", "7"):
+        r = subprocess.run([str(oracle_dir / "fuzz_asan"), seed, "1500"], capture_output=True, text=True, timeout=300)
+        assert r.returncode == 0, r.stderr[-4000:]
+        assert "fuzz_driver ok" in r.stdout
