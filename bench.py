@@ -1,33 +1,47 @@
 #!/usr/bin/env python3
-"""bench.py — BASELINE.json headline: device-resident data-block decode GiB/s,
-1 M x 4 KiB blocks, 16 B keys / 64 B values (configs[1]).
+"""bench.py — BASELINE.json headline: "device-resident data-block decode+encode
+GiB/s, 1 M x 4 KiB blocks" (configs[1] shape, configs[2] round trip).
 
-A "step" = one lsm_decode_blocks call over the whole batch of on-disk blocks
-already resident in HBM: trailer item counts + scan + verify (header and
-xxh3_128) + parse of every record into the parsed-item SoA.  value = total
-block bytes decoded by all ranks / (max over ranks of the timed K steps).
+A "step" is one pass of the hot path over the batch, both directions:
+  lsm_encode_blocks   the item SoA (keys, values, seqnos, types) of 1 M blocks
+                      -> on-disk blocks (DataBlock::encode_into + Block::write_into,
+                      payload xxh3_128 + header fused), then
+  lsm_decode_blocks   those blocks -> verified + parsed item SoA (Block::from_file
+                      + DataBlock::iter: trailer counts, scan, header / xxh3_128
+                      verify, full parse).
+Inputs are resident in HBM when the timed region starts; nothing is cached
+between steps (every step re-encodes and re-decodes the whole batch).
+value = block bytes that went through encode AND decode, all ranks, per second
+      = N_ranks x block_bytes x K / (max over ranks of the timed K steps).
+(SURVEY §8(d) counts a round trip as W_enc + R_dec = 2 x block_bytes; that
+figure is reported as `round_trip_traffic_GiB_per_s`, never as `value`.)
 
 Synthetic input: keys = 16 B big-endian counters, values 64 B
-uniform random, seqno 63, all Value, cut by the writer rule at 4096 B
-(52 items / 3769-3773 B per block), restart interval 16, hash ratio 0.
-The blocks are produced by the GPU encoder (lsm_encode_blocks) and a sample is
-checked bit-exactly against the oracle before timing.
+uniform random, seqno 63, all Value, cut by the writer rule at 4096 B (52 items /
+3769-3773 B per block), restart interval 16, hash ratio 0.  Outside the timed
+region EVERY block is checked: encoded bytes == the oracle's encode (memcmp),
+decoded fields == the oracle's decode (multithreaded oracle on the host).
 
-N > 1: one process per GPU (torch.distributed, RCCL), each rank decodes its own
-1 M-block shard (weak scaling, no data-path collective).
+N > 1: one process per GPU (torch.distributed, RCCL only for the max-time /
+byte-sum reductions), each rank round-trips its own 1 M-block batch (weak
+scaling, no data-path collective).
 
-Side legs in the same JSON line (not `value`): encode and the configs[2] round
-trip, configs[3] (prefix-heavy 16 KiB blocks, N = 1), configs[4] (8 GiB of
-mixed 4/16/64 KiB data + index blocks byte-split across the ranks: strong
-scaling), batched point reads, the whole-file checksum, the host-inclusive
-(PCIe) decode rate and the CPU baseline (oracle port on the host cores).
+Also in the same JSON line (not `value`): per-kernel rooflines (decode, encode)
+with the measured copy / LDS-DMA read ceilings, configs[3] (prefix-heavy 16 KiB),
+configs[4] (8 GiB mixed 4/16/64 KiB data + index blocks byte-split across ranks),
+point reads, range seeks, whole-file checksum, Bloom filter, LZ4, the
+host-inclusive rates (decode from an mmap'd file, encode from a host write
+buffer) and the CPU baseline (oracle port on the host cores, 1 thread and all).
 """
 from __future__ import annotations
 
 import argparse
+import ctypes as C
 import json
+import mmap
 import os
 import sys
+import tempfile
 import time
 from pathlib import Path
 
@@ -35,16 +49,41 @@ ROOT = Path(__file__).resolve().parent
 for p in (ROOT / "lsm-tree_amd", ROOT / "oracle", ROOT / "tests"):
     sys.path.insert(0, str(p))
 
-BASELINE_METRIC = "device-resident data-block decode+encode GiB/s, 1 M \u00d7 4 KiB blocks"  # BASELINE.json
+BASELINE_METRIC = "device-resident data-block decode+encode GiB/s, 1 M × 4 KiB blocks"  # BASELINE.json
 HBM_PEAK_GBPS = 8000.0  # MI355X HBM3E spec, /opt/skills/guides/MI355X_MICROARCH.md
 PARSED_BYTES_PER_ITEM = 8 + 4 + 4 + 4 + 2 + 2 + 1  # seqno key_off val_off val_len key_len prefix_len vtype
 PER_BLOCK_OUT = 8  # item_start u32 + status i32
+# encode input per item as the ABI reads it: key + value bytes, seqno u64, vtype u8, key_off / val_off u64
+ENC_IN_PER_ITEM = 8 + 1 + 8 + 8
+DATA_FIELDS = ["seqno", "key_off", "val_off", "val_len", "key_len", "prefix_len", "vtype"]
+FIELD_NP = {"seqno": "uint64", "key_off": "uint32", "val_off": "uint32", "val_len": "uint32", "key_len": "uint16",
+            "prefix_len": "uint16", "vtype": "uint8", "handle_off": "uint64"}
+HOST_THREADS = 16  # the GPU box's CPU share per GPU (nproc shows the whole machine)
 
 
 def log(*a):
     print(*a, file=sys.stderr, flush=True)
 
 
+def host_threads(world=1):
+    try:
+        n = len(os.sched_getaffinity(0))
+    except AttributeError:
+        n = os.cpu_count() or 1
+    return max(1, min(HOST_THREADS, n) // max(1, world))
+
+
+def cpu_model():
+    try:
+        for line in open("/proc/cpuinfo"):
+            if line.startswith("model name"):
+                return line.split(":", 1)[1].strip()
+    except OSError:
+        pass
+    return "unknown"
+
+
+# ---------------------------------------------------------------- workloads
 def make_workload(torch, lsmgpu, n_blocks, items_per_block=52, key_len=16, val_len=64, seed=0x5EED0002,
                   kind="counter"):
     """Synthetic items on the GPU, cut every items_per_block items (= the writer
@@ -92,155 +131,147 @@ def check_cut_rule(lsmgpu, items_per_block, key_len, val_len, block_size=4096):
     assert list(starts) == list(range(0, m + 1, items_per_block)), starts
 
 
-def verify_sample(torch, lsmgpu, items, starts, enc, dec, n_blocks, n_items, rank):
-    """Bit-exact check of sampled blocks against the oracle + size-independent
-    properties of the full batch (all statuses OK, item count, round trip)."""
+# ------------------------------------------------------- full oracle checks
+def host_items(items, n):
+    """Device item SoA -> pyoracle.Items over host copies (no dtype copies)."""
     import numpy as np
     import pyoracle
-
-    st_enc = enc["status"][:n_blocks]
-    st_dec = dec["status"][:n_blocks]
-    assert int((st_enc != 0).sum().item()) == 0, "encode status"
-    assert int((st_dec != 0).sum().item()) == 0, "decode status"
-    assert int(dec["item_start"][n_blocks].item()) == n_items, "item count"
-    # decoded seqnos / lengths equal the encoded input everywhere
-    assert bool((dec["seqno"][:n_items] == items["seqno"]).all().item())
-    assert bool((dec["val_len"][:n_items] == 64).all().item())
-    # a sample of blocks: GPU bytes == oracle bytes, GPU parsed fields == oracle
-    rng = np.random.default_rng(rank + 1)
-    picks = sorted(set(rng.integers(0, n_blocks, 64).tolist()) | {0, n_blocks - 1})
-    off = enc["block_off"]
-    for b in picks:
-        s0, s1 = int(starts[b].item()), int(starts[b + 1].item())
-        ko = items["key_off"][s0:s1 + 1].cpu().numpy().astype(np.uint64)
-        vo = items["val_off"][s0:s1 + 1].cpu().numpy().astype(np.uint64)
-        kb = items["keys"][int(ko[0]):int(ko[-1])].cpu().numpy()
-        vb = items["vals"][int(vo[0]):int(vo[-1])].cpu().numpy()
-        it = pyoracle.Items(kb, ko - ko[0], vb, vo - vo[0], items["seqno"][s0:s1].cpu().numpy().view(np.uint64),
-                            items["vtype"][s0:s1].cpu().numpy())
-        ref = pyoracle.block_write(pyoracle.data_block_encode(it, 0, s1 - s0))
-        o0, o1 = int(off[b].item()), int(off[b + 1].item())
-        got = enc["buf"][o0:o1].cpu().numpy().tobytes()
-        assert got == ref, f"block {b} bytes differ from oracle"
-        n, parsed = pyoracle.data_block_decode(ref[33:])
-        i0 = int(dec["item_start"][b].item())
-        for f, dt in (("seqno", np.uint64), ("key_off", np.uint32), ("val_off", np.uint32),
-                      ("key_len", np.uint16), ("prefix_len", np.uint16), ("vtype", np.uint8)):
-            gv = dec[f][i0:i0 + n].cpu().numpy().view(dt)
-            assert (gv == parsed[f].astype(dt)).all(), (b, f)
-    return len(picks)
+    ko = items["key_off"][:n + 1].cpu().numpy().view(np.uint64)
+    vo = items["val_off"][:n + 1].cpu().numpy().view(np.uint64) if "val_off" in items else np.zeros(n + 1, np.uint64)
+    kb = items["keys"][:int(ko[-1])].cpu().numpy()
+    vb = items["vals"][:int(vo[-1])].cpu().numpy() if "vals" in items else np.zeros(1, np.uint8)
+    seq = items["seqno"][:n].cpu().numpy().view(np.uint64)
+    vt = items["vtype"][:n].cpu().numpy() if "vtype" in items else np.zeros(n, np.uint8)
+    ho = items["handle_off"][:n].cpu().numpy().view(np.uint64) if "handle_off" in items else None
+    hs = items["handle_size"][:n].cpu().numpy().view(np.uint32) if "handle_size" in items else None
+    return pyoracle.Items(kb, ko, vb, vo, seq, vt, ho, hs)
 
 
-def cpu_baseline(torch, enc, n_blocks, min_seconds=10.0, sample_blocks=65536, threads=None):
-    """Oracle (scalar C port of the reference path) on the host cores: verify +
-    full forward parse of a bounded sample, repeated for >= min_seconds."""
+def check_encode_all(torch, items, starts, enc, nb, n_items, threads, restart_interval=16, block_type=0):
+    """Every encoded block == the oracle's DataBlock::encode_into + Block::write_into
+    of the same items (one memcmp over the whole batch).  Returns (ref_buf, ref_off)."""
     import numpy as np
     import pyoracle
+    assert int((enc["status"][:nb] != 0).sum().item()) == 0, "encode status"
+    it = host_items(items, n_items)
+    st = starts[:nb + 1].cpu().numpy().astype(np.uint32)
+    ref_buf, ref_off = pyoracle.encode_blocks(it, st, restart_interval=restart_interval, block_type=block_type,
+                                              nthreads=threads)
+    got_off = enc["block_off"][:nb + 1].cpu().numpy().view(np.uint64)
+    assert np.array_equal(got_off, ref_off), "block offsets differ from the oracle"
+    got = enc["buf"][:int(ref_off[-1])].cpu().numpy()
+    assert np.array_equal(got, ref_buf), "encoded bytes differ from the oracle"
+    return ref_buf, ref_off
 
-    nb = min(sample_blocks, n_blocks)
-    off = enc["block_off"][:nb + 1].cpu().numpy().view(np.uint64).copy()
-    blocks = enc["buf"][:int(off[-1])].cpu().numpy()
-    threads = threads or min(16, os.cpu_count() or 1)
+
+def check_decode_all(dec, ref_buf, ref_off, nb, threads, fields=DATA_FIELDS, expect_status_ok=True):
+    """Every block's status, item_start and every parsed field == the oracle's
+    Block::from_file + full forward DataBlock::iter / IndexBlock::iter."""
+    import numpy as np
+    import pyoracle
+    n_est = int(dec["item_start"][nb].item())
+    parsed, item_start, status = pyoracle.decode_blocks(ref_buf, ref_off, nthreads=threads, item_cap=max(n_est, 1))
+    got_st = dec["status"][:nb].cpu().numpy()
+    assert np.array_equal(got_st, status), "decode statuses differ from the oracle"
+    if expect_status_ok:
+        assert (status == 0).all(), "oracle rejects a block"
+    assert np.array_equal(dec["item_start"][:nb + 1].cpu().numpy().view(np.uint32), item_start), "item_start"
+    n = int(item_start[-1])
+    for f in fields:
+        g = dec[f][:n].cpu().numpy().view(FIELD_NP[f])
+        assert np.array_equal(g, parsed[f].astype(FIELD_NP[f])), f"decoded field {f} differs from the oracle"
+    return n
+
+
+# ------------------------------------------------------------- CPU baseline
+def cpu_baseline(ref_buf, ref_off, items_host, starts_np, sample_blocks=65536, min_seconds=2.0, world=1):
+    """The oracle (C restatement of the reference path, AVX2 XXH3) on the host
+    cores, same workload: encode (DataBlock::encode_into + Block::write_into) and
+    decode (Block::from_file + DataBlock::iter into the same parsed SoA as the
+    GPU) of a bounded sample of the batch; 1 thread and all threads."""
+    import numpy as np
+    import pyoracle
+    nb = min(sample_blocks, len(ref_off) - 1)
+    n_items = int(starts_np[nb])
+    off = np.ascontiguousarray(ref_off[:nb + 1])
+    blocks = ref_buf[:int(off[-1])]
     nbytes = int(off[-1])
-    passes, t0 = 0, time.perf_counter()
-    while True:
-        parsed, item_start, status = pyoracle.decode_blocks(blocks, off, nthreads=threads)
-        passes += 1
-        el = time.perf_counter() - t0
-        if el >= min_seconds or passes >= 2000:
-            break
-    assert (status == 0).all()
-    return {"value": round(nbytes * passes / el / 2 ** 30, 3), "unit": "GiB/s", "cores": threads, "kind": "port",
-            "sample": f"{nb} blocks ({nbytes / 1e6:.1f} MB) of the same batch, {passes} passes in {el:.1f} s: "
-                      f"header+xxh3_128 verify and full forward parse (oracle/batch.c)"}
+    ko = items_host.key_off[:n_items + 1]
+    vo = items_host.val_off[:n_items + 1]
+    it = pyoracle.Items(items_host.keys[:int(ko[-1])], ko, items_host.vals[:int(vo[-1])], vo,
+                        items_host.seqno[:n_items], items_host.vtype[:n_items])
+    st = np.ascontiguousarray(starts_np[:nb + 1], np.uint32)
+
+    def rate(fn, threads):
+        passes, t0 = 0, time.perf_counter()
+        while True:
+            fn(threads)
+            passes += 1
+            el = time.perf_counter() - t0
+            if el >= min_seconds or passes >= 200:
+                return nbytes * passes / el / 2 ** 30
+
+    def enc(t):
+        b, o = pyoracle.encode_blocks(it, st, nthreads=t)
+        assert int(o[-1]) == nbytes
+
+    def dec(t):
+        _, _, s = pyoracle.decode_blocks(blocks, off, nthreads=t, item_cap=n_items)
+        assert (s == 0).all()
+
+    tall = host_threads(world)
+    res = {}
+    for t in sorted({1, tall}):
+        e, d = rate(enc, t), rate(dec, t)
+        res[t] = {"encode_GiB_per_s": round(e, 3), "decode_GiB_per_s": round(d, 3),
+                  "round_trip_GiB_per_s": round(1.0 / (1.0 / e + 1.0 / d), 3)}
+    return {"value": res[tall]["round_trip_GiB_per_s"], "unit": "GiB/s", "cores": tall, "kind": "port",
+            "cpu_model": cpu_model(), "threads": {str(k): v for k, v in res.items()},
+            "sample": f"{nb} blocks ({nbytes / 1e6:.1f} MB) of the same batch, encode then decode, each leg repeated "
+                      f">= {min_seconds:.0f} s; value = block bytes / (t_enc + t_dec) with {tall} threads "
+                      f"(oracle/batch.c, AVX2 XXH3, -O3 -march=x86-64-v3)"}
 
 
-DATA_FIELDS = ["seqno", "key_off", "val_off", "val_len", "key_len", "prefix_len", "vtype"]
-
-
-def host_inclusive(torch, lsmgpu, enc, item_start, nb, chunk_blocks=131072, reps=2):
-    """Blocks start in pinned host memory (the mmap'd-SST case): chunked,
-    double-buffered H2D copy -> decode -> D2H of the parsed SoA on three
-    streams.  Returns input GiB/s over the whole pipeline (not `value`)."""
-    import numpy as np
-    off = enc["block_off"][:nb + 1].cpu().numpy().astype(np.int64)
-    ist = item_start[:nb + 1].cpu().numpy().astype(np.int64)
-    total = int(off[-1])
-    pad = lsmgpu.LSM_INPUT_PADDING
-    hbuf = torch.empty(total + pad, dtype=torch.uint8).pin_memory()
-    hbuf.copy_(enc["buf"][:total + pad].cpu())
-    chunks = []
-    for b0 in range(0, nb, chunk_blocks):
-        b1 = min(nb, b0 + chunk_blocks)
-        s0 = int(off[b0]) & ~15
-        rel = torch.from_numpy(off[b0:b1 + 1] - s0).pin_memory()
-        chunks.append((b0, b1, s0, int(off[b1]) - s0 + pad, rel, int(ist[b0]), int(ist[b1] - ist[b0])))
-    max_bytes = max(c[3] for c in chunks)
-    max_n = max(c[1] - c[0] for c in chunks)
-    cap = max(c[6] for c in chunks)
-    dev = enc["buf"].device
-    dbuf = [torch.empty(max_bytes, dtype=torch.uint8, device=dev) for _ in range(2)]
-    doff = [torch.empty(max_n + 1, dtype=torch.int64, device=dev) for _ in range(2)]
-    decs = [lsmgpu.Decoder(dev) for _ in range(2)]
-    outs = [decs[k].alloc_outputs(cap, max_n, fields=DATA_FIELDS) for k in range(2)]
-    hout = {f: torch.empty(int(ist[-1]) + 1, dtype=outs[0][f].dtype).pin_memory() for f in DATA_FIELDS}
-    s_in, s_dec, s_out = torch.cuda.Stream(), torch.cuda.Stream(), torch.cuda.Stream()
-    free = [torch.cuda.Event() for _ in range(2)]
-    best = None
-    for _ in range(reps):
+# ----------------------------------------------------------------- ceilings
+def ceilings(torch, nbytes=4 << 30, reps=5):
+    """Practical HBM ceilings measured in this run (lsm-tree_amd/ceiling):
+    a 16 B/lane streaming copy (R+W) and the decode kernel's LDS-DMA read shape."""
+    lib = C.CDLL(str(ROOT / "lsm-tree_amd" / "ceiling" / "liblsmceiling.so"))
+    lib.lsm_ceiling_copy.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p]
+    lib.lsm_ceiling_read.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p]
+    src = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    src.random_(0, 256)
+    dst = torch.empty(nbytes, dtype=torch.uint8, device="cuda")
+    sink = torch.zeros(4, dtype=torch.int32, device="cuda")
+    s = C.c_void_p(torch.cuda.current_stream().cuda_stream)
+    out = {}
+    for name, fn, moved in (("copy", lambda: lib.lsm_ceiling_copy(src.data_ptr(), dst.data_ptr(), nbytes, s),
+                             2 * nbytes),
+                            ("read", lambda: lib.lsm_ceiling_read(src.data_ptr(), nbytes, sink.data_ptr(), s),
+                             nbytes)):
+        assert fn() == 0
         torch.cuda.synchronize()
-        t0 = time.perf_counter()
-        for i, (b0, b1, s0, nbytes, rel, i0, ni) in enumerate(chunks):
-            k = i % 2
-            n = b1 - b0
-            with torch.cuda.stream(s_in):
-                if i >= 2:
-                    s_in.wait_event(free[k])
-                dbuf[k][:nbytes].copy_(hbuf[s0:s0 + nbytes], non_blocking=True)
-                doff[k][:n + 1].copy_(rel, non_blocking=True)
-            s_dec.wait_stream(s_in)
-            decs[k].decode(dbuf[k], doff[k], n, outs[k], cap, stream=s_dec)
-            s_out.wait_stream(s_dec)
-            with torch.cuda.stream(s_out):
-                for f in DATA_FIELDS:
-                    hout[f][i0:i0 + ni].copy_(outs[k][f][:ni], non_blocking=True)
-                free[k].record(s_out)
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            fn()
+        e1.record()
         torch.cuda.synchronize()
-        el = time.perf_counter() - t0
-        best = el if best is None else min(best, el)
-    # the host copy of the parsed SoA equals the device-resident decode
-    assert bool((hout["val_len"][:int(ist[-1])] == 64).all()) and bool((hout["seqno"][:int(ist[-1])] == 63).all())
-    return {"GiB_per_s": round(total / best / 2 ** 30, 3), "ms": round(best * 1e3, 3), "chunk_blocks": chunk_blocks,
-            "note": "pinned host blocks -> H2D -> decode -> D2H parsed SoA (25 B/item), 3 streams, double-buffered"}
+        ms = e0.elapsed_time(e1) / reps
+        out[f"{name}_GBps"] = round(moved / (ms * 1e-3) / 1e9, 1)
+    del src, dst
+    torch.cuda.empty_cache()
+    return out
 
 
-def check_blocks_vs_oracle(torch, items, starts, enc, picks, restart_interval=16):
-    """Encoded bytes of the picked blocks == oracle encode of the same items."""
-    import numpy as np
-    import pyoracle
-    off = enc["block_off"]
-    for b in picks:
-        s0, s1 = int(starts[b].item()), int(starts[b + 1].item())
-        ko = items["key_off"][s0:s1 + 1].cpu().numpy().astype(np.uint64)
-        vo = items["val_off"][s0:s1 + 1].cpu().numpy().astype(np.uint64)
-        it = pyoracle.Items(items["keys"][int(ko[0]):int(ko[-1])].cpu().numpy(), ko - ko[0],
-                            items["vals"][int(vo[0]):int(vo[-1])].cpu().numpy(), vo - vo[0],
-                            items["seqno"][s0:s1].cpu().numpy().view(np.uint64), items["vtype"][s0:s1].cpu().numpy())
-        ref = pyoracle.block_write(pyoracle.data_block_encode(it, 0, s1 - s0, restart_interval=restart_interval))
-        got = enc["buf"][int(off[b].item()):int(off[b + 1].item())].cpu().numpy().tobytes()
-        assert got == ref, f"block {b} bytes differ from oracle"
-    return len(picks)
-
-
-def time_decode(torch, lsmgpu, blocks, boff, nb, n_items, steps):
+# ------------------------------------------------------------- side legs
+def time_decode(torch, lsmgpu, blocks, boff, nb, n_items, steps, fields=DATA_FIELDS + ["handle_off"]):
     """Device-resident lsm_decode_blocks over a batch (count + scan + verify +
     parse), HIP events on the launch stream; checks every status and the count."""
     dec = lsmgpu.Decoder(blocks.device)
-    out = dec.alloc_outputs(n_items, nb, fields=DATA_FIELDS + ["handle_off"])
+    out = dec.alloc_outputs(n_items, nb, fields=fields)
     dec.decode(blocks, boff, nb, out, n_items)
     torch.cuda.synchronize()
-    assert int((out["status"][:nb] != 0).sum().item()) == 0, "decode status"
-    assert int(out["item_start"][nb].item()) == n_items, "item count"
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(steps):
@@ -250,9 +281,10 @@ def time_decode(torch, lsmgpu, blocks, boff, nb, n_items, steps):
     return e0.elapsed_time(e1) / steps, out
 
 
-def bench_config4(torch, lsmgpu, steps, rank):
+def bench_config4(torch, lsmgpu, steps, rank, threads):
     """configs[3]: prefix-heavy keys (32 B shared prefix + 8 B suffix), 256 B
-    values, 16 KiB blocks (56 items, 14953 B on disk), 262144 blocks."""
+    values, 16 KiB blocks (56 items, 14953 B on disk), 262144 blocks; every
+    block checked against the oracle (encode bytes and decoded fields)."""
     nb = 262144
     check_cut_rule(lsmgpu, 56, 40, 256, 16384)
     items, starts, n = make_workload(torch, lsmgpu, nb, items_per_block=56, key_len=40, val_len=256,
@@ -260,10 +292,8 @@ def bench_config4(torch, lsmgpu, steps, rank):
     enc_ctx = lsmgpu.Encoder()
     enc = enc_ctx.encode(items, starts, nb)
     torch.cuda.synchronize()
-    assert int((enc["status"][:nb] != 0).sum().item()) == 0
     total = int(enc["block_off"][nb].item())
     assert int(enc["block_off"][1].item()) == 14953  # SURVEY 8 table (first block; later ones vary by a byte)
-    checked = check_blocks_vs_oracle(torch, items, starts, enc, [0, 1, nb // 2, nb - 1])
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(3):
@@ -272,13 +302,15 @@ def bench_config4(torch, lsmgpu, steps, rank):
     torch.cuda.synchronize()
     enc_ms = e0.elapsed_time(e1) / 3
     dec_ms, out = time_decode(torch, lsmgpu, enc["buf"], enc["block_off"], nb, n, steps)
-    assert bool((out["prefix_len"][:n].view(torch.int16)[1::56] >= 32).all().item())  # shared 32 B prefix
+    ref_buf, ref_off = check_encode_all(torch, items, starts, enc, nb, n, threads)
+    check_decode_all(out, ref_buf, ref_off, nb, threads)
     res = {"workload": "BASELINE configs[3]: 16 KiB blocks, 32 B shared prefix + 8 B suffix keys, 256 B values",
            "blocks": nb, "bytes": total, "decode_ms": round(dec_ms, 4),
            "decode_GiB_per_s": round(total / (dec_ms * 1e-3) / 2 ** 30, 3),
            "encode_ms": round(enc_ms, 4), "encode_GiB_per_s": round(total / (enc_ms * 1e-3) / 2 ** 30, 3),
-           "oracle_checked_blocks": checked}
-    del items, enc, out
+           "round_trip_GiB_per_s": round(total / ((enc_ms + dec_ms) * 1e-3) / 2 ** 30, 3),
+           "oracle_checked_blocks": nb}
+    del items, enc, out, ref_buf
     torch.cuda.empty_cache()
     return res
 
@@ -291,11 +323,13 @@ C5_SEGMENTS = [(4096, 52, "counter", 3769), (4096, 52, "random", 4466), (16384, 
 C5_TABLE = 64 << 20
 
 
-def build_config5_shard(torch, lsmgpu, shard_bytes, rank):
+def build_config5_shard(torch, lsmgpu, shard_bytes, rank, threads):
     """This rank's byte share of the configs[4] batch, GPU-encoded: data blocks
-    of the six segments, each followed by its index blocks (one per table)."""
+    of the six segments, each followed by its index blocks (one per table).
+    Every data and index block's bytes are checked against the oracle."""
+    import numpy as np
     segs, n_items, n_data_blocks, n_index_blocks = [], 0, 0, 0
-    picks_checked = 0
+    checked = 0
     for si, (bs, ipb, kind, est) in enumerate(C5_SEGMENTS):
         nb = max(1, int(shard_bytes / len(C5_SEGMENTS) / est))
         check_cut_rule(lsmgpu, ipb, 16, 64, bs)
@@ -303,8 +337,7 @@ def build_config5_shard(torch, lsmgpu, shard_bytes, rank):
                                          kind=kind)
         enc = lsmgpu.Encoder().encode(items, starts, nb)
         torch.cuda.synchronize()
-        assert int((enc["status"][:nb] != 0).sum().item()) == 0
-        picks_checked += check_blocks_vs_oracle(torch, items, starts, enc, [0, nb - 1])
+        check_encode_all(torch, items, starts, enc, nb, n, threads)
         boff = enc["block_off"][:nb + 1]
         dev = boff.device
         # index entries: end key, seqno of each block's last item, handle (offset in its table, size)
@@ -324,7 +357,8 @@ def build_config5_shard(torch, lsmgpu, shard_bytes, rank):
         nt = int(first.numel())
         ienc = lsmgpu.Encoder().encode(ix, istarts, nt, restart_interval=1, block_type=lsmgpu.BLOCK_INDEX)
         torch.cuda.synchronize()
-        assert int((ienc["status"][:nt] != 0).sum().item()) == 0
+        check_encode_all(torch, ix, istarts, ienc, nt, nb, threads, restart_interval=1, block_type=1)
+        checked += nb + nt
         dbytes, ibytes = int(boff[nb].item()), int(ienc["block_off"][nt].item())
         segs.append((enc["buf"][:dbytes], boff[:-1].clone(), ienc["buf"][:ibytes], ienc["block_off"][:nt] + dbytes,
                      dbytes + ibytes))
@@ -342,14 +376,22 @@ def build_config5_shard(torch, lsmgpu, shard_bytes, rank):
     block_off = torch.cat(offl + [torch.tensor([base], dtype=torch.int64, device=blocks.device)])
     del segs, pieces
     torch.cuda.empty_cache()
-    return blocks, block_off, n_data_blocks + n_index_blocks, n_items, base, n_index_blocks, picks_checked
+    return blocks, block_off, n_data_blocks + n_index_blocks, n_items, base, n_index_blocks, checked
 
 
-def bench_config5(torch, lsmgpu, steps, rank, world, dist, dev, total_bytes=8 << 30):
+def bench_config5(torch, lsmgpu, steps, rank, world, dist, dev, threads, total_bytes=8 << 30):
     """configs[4]: 8 GiB of mixed data + index blocks, byte-split across the
-    ranks (strong scaling: the batch is fixed, each rank decodes its share)."""
-    blocks, boff, nb, n_items, nbytes, n_idx, checked = build_config5_shard(torch, lsmgpu, total_bytes / world, rank)
+    ranks (strong scaling: the batch is fixed, each rank decodes its share).
+    Every block's decode (status, item_start, all fields incl. handle_off) is
+    checked against the oracle."""
+    import numpy as np
+    blocks, boff, nb, n_items, nbytes, n_idx, checked = build_config5_shard(torch, lsmgpu, total_bytes / world,
+                                                                            rank, threads)
     ms, out = time_decode(torch, lsmgpu, blocks, boff, nb, n_items, steps)
+    host = blocks[:nbytes].cpu().numpy()
+    hoff = boff.cpu().numpy().view(np.uint64)
+    check_decode_all(out, host, hoff, nb, threads, fields=DATA_FIELDS + ["handle_off"])
+    del host
     t = torch.tensor([ms, float(nbytes)], dtype=torch.float64, device=dev)
     if dist is not None:
         mx = t.clone()
@@ -365,10 +407,10 @@ def bench_config5(torch, lsmgpu, steps, rank, world, dist, dev, total_bytes=8 <<
                         "byte-split across ranks (strong scaling)",
             "total_bytes": int(bytes_all), "blocks_per_rank": nb, "index_blocks_per_rank": n_idx,
             "decode_ms_max_rank": round(ms_all, 4), "GiB_per_s": round(bytes_all / (ms_all * 1e-3) / 2 ** 30, 3),
-            "oracle_checked_blocks": checked}
+            "oracle_checked_blocks_per_rank": {"encode": checked, "decode": nb}}
 
 
-def bench_point_read(torch, lsmgpu, items, starts, enc, nb, n_items, n_queries=1 << 20, reps=5):
+def bench_point_read(torch, lsmgpu, items, enc, nb, n_items, n_queries=1 << 20, reps=5):
     """Batched DataBlock::point_read: random existing keys of the config 2 batch,
     snapshot = max; every query must hit its own item."""
     g = torch.Generator(device="cuda")
@@ -390,8 +432,30 @@ def bench_point_read(torch, lsmgpu, items, starts, enc, nb, n_items, n_queries=1
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / reps
+    # range seeks: [key(i), key(i + 20)] inside the block of i (Table::range's per-block step)
+    lo_i = qi
+    hi_i = torch.minimum(qi + 20, (qb.to(torch.int64) + 1) * 52 - 1)
+    kv = items["keys"][:n_items * 16].view(n_items, 16)
+    pad = torch.zeros(lsmgpu.LSM_INPUT_PADDING, dtype=torch.uint8, device="cuda")
+    lo = torch.cat([kv[lo_i].reshape(-1), pad])
+    hi = torch.cat([kv[hi_i].reshape(-1), pad])
+    flags = torch.full((n_queries,), lsmgpu.SEEK_LO | lsmgpu.SEEK_HI, dtype=torch.uint8, device="cuda")
+    sk = lsmgpu.seek(enc["buf"], enc["block_off"], nb, qb, lo, noff, hi, noff, flags)
+    torch.cuda.synchronize()
+    base = qb.to(torch.int64) * 52
+    assert int((sk["status"] != 0).sum().item()) == 0
+    assert bool((sk["first"].to(torch.int64) == lo_i - base).all().item()), "seek lower bounds"
+    assert bool((sk["end"].to(torch.int64) == hi_i - base + 1).all().item()), "seek upper bounds"
+    e0.record()
+    for _ in range(reps):
+        lsmgpu.seek(enc["buf"], enc["block_off"], nb, qb, lo, noff, hi, noff, flags)
+    e1.record()
+    torch.cuda.synchronize()
+    ms_seek = e0.elapsed_time(e1) / reps
     return {"queries": n_queries, "ms": round(ms, 4), "Mqueries_per_s": round(n_queries / ms / 1e3, 1),
-            "note": "lane per query straight from HBM (hash index off: restart binary search + MVCC scan)"}
+            "seek_ms": round(ms_seek, 4), "seek_Mqueries_per_s": round(n_queries / ms_seek / 1e3, 1),
+            "note": "lane per query straight from HBM (restart binary search + MVCC scan); seek = lower + upper "
+                    "bound of a 21-key range per query"}
 
 
 def bench_file_checksum(torch, lsmgpu, enc, total_bytes, reps=5):
@@ -410,10 +474,7 @@ def bench_file_checksum(torch, lsmgpu, enc, total_bytes, reps=5):
 
 def bench_bloom(torch, lsmgpu, items, n_items, reps=5):
     """Standard Bloom filter over the configs[1] batch's keys (FullFilterWriter,
-    src/table/writer/filter/full.rs:47-92, BitsPerKey(10) default): hash64 of every
-    key, filter build (k scattered atomicOr per key), then one probe per key.
-    Two sizes: one table's worth of keys (1 M, filter 1.25 MB, L2-resident) and
-    the whole batch as one filter (HBM-resident)."""
+    src/table/writer/filter/full.rs:47-92, BitsPerKey(10) default)."""
     out = {}
     for name, n in (("table_1M", min(1 << 20, n_items)), ("batch", n_items)):
         ko = items["key_off"][:n + 1]
@@ -444,11 +505,9 @@ def bench_bloom(torch, lsmgpu, items, n_items, reps=5):
 
 def bench_lz4(torch, lsmgpu, enc, n_blocks, reps=5, sample=131072):
     """Block::from_reader with CompressionType::Lz4 (src/table/block/mod.rs:87-128)
-    over LZ4 copies of the first `sample` configs[1] blocks: the payloads are
-    compressed on the host by liblz4 (pyarrow "lz4_raw", the block format
-    lz4_flex writes) and re-framed (header checksums by python-xxhash); then the
-    batch is checked + decompressed on the device.  Random 64 B values make the
-    payloads barely compressible, so this is the literal-heavy worst case."""
+    over LZ4 copies of the first `sample` configs[1] blocks (payloads compressed on
+    the host by liblz4, pyarrow "lz4_raw", headers sealed with python-xxhash),
+    checked + decompressed on the device."""
     import numpy as np
     try:
         import pyarrow as pa
@@ -463,8 +522,7 @@ def bench_lz4(torch, lsmgpu, enc, n_blocks, reps=5, sample=131072):
     for b in range(nb):
         payload = host[off[b] + 33:off[b + 1]]
         c = codec.compress(payload, asbytes=True)
-        ck = xxhash.xxh3_128_intdigest(c)
-        h = b"LSM\x03\x00" + ck.to_bytes(16, "little") + len(c).to_bytes(4, "little") + \
+        h = b"LSM\x03\x00" + xxhash.xxh3_128_intdigest(c).to_bytes(16, "little") + len(c).to_bytes(4, "little") + \
             len(payload).to_bytes(4, "little")
         parts.append(h + xxhash.xxh3_128_intdigest(h).to_bytes(16, "little")[:4] + c)
         raw_total += len(payload)
@@ -475,9 +533,8 @@ def bench_lz4(torch, lsmgpu, enc, n_blocks, reps=5, sample=131072):
     out, out_off, status = lsmgpu.lz4_decompress_blocks(dbuf, doff)
     torch.cuda.synchronize()
     assert int((status != 0).sum().item()) == 0, "lz4: block status"
-    o0 = int(off[0]) + 33
-    if "DIAG" not in str(lsmgpu.LIB_PATH):  # diagnostic variants (scripts/lz4_ablation.py) skip work
-        assert out[:int(off[1]) - o0].cpu().numpy().tobytes() == host[o0:int(off[1])], "lz4: block 0 bytes"
+    raw = b"".join(host[off[b] + 33:off[b + 1]] for b in range(nb))
+    assert out[:len(raw)].cpu().numpy().tobytes() == raw, "lz4: decompressed bytes"
     e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
     e0.record()
     for _ in range(reps):
@@ -487,25 +544,240 @@ def bench_lz4(torch, lsmgpu, enc, n_blocks, reps=5, sample=131072):
     ms = e0.elapsed_time(e1) / reps
     return {"blocks": nb, "stored_bytes": int(loff[-1]), "raw_bytes": raw_total, "ms": round(ms, 4),
             "GiB_per_s_raw": round(raw_total / (ms * 1e-3) / 2 ** 30, 1),
-            "note": "header + xxh3_128 verify + LZ4 decode, wave per block; host-side size scan included"}
+            "note": "plan (verified headers -> output offsets) + header / xxh3_128 verify + LZ4 decode, every "
+                    "decompressed byte checked"}
 
 
-def load_traffic(n_blocks):
-    """HBM bytes of one decode_blocks_kernel launch over n_blocks, from the
-    newest committed rocprofv3 PMC summary (profiles/traffic_*.json: FETCH_SIZE
-    x2 per the gfx950 guide + WRITE_SIZE), scaled per block when the profiled
-    launch had a different block count."""
+# ----------------------------------------------------------- host-inclusive
+def _hip():
+    L = C.CDLL("libamdhip64.so")
+    L.hipHostRegister.argtypes = [C.c_void_p, C.c_size_t, C.c_uint]
+    L.hipHostRegister.restype = C.c_int
+    L.hipHostUnregister.argtypes = [C.c_void_p]
+    L.hipHostUnregister.restype = C.c_int
+    return L
+
+
+def host_inclusive_decode(torch, lsmgpu, enc, nb_all, ipb=52, max_blocks=262144, chunk_blocks=32768, reps=2):
+    """Blocks start in an mmap'd SST file (the Scanner / compaction read side):
+    the file's pages are registered with hipHostRegister once (the page-cache
+    mapping, no host copy), then chunked H2D -> decode -> D2H of the parsed SoA
+    on three streams, double-buffered.  Returns input GiB/s of the pipeline."""
+    import numpy as np
+    nb = min(max_blocks, nb_all)
+    off = enc["block_off"][:nb + 1].cpu().numpy().astype(np.int64)
+    total = int(off[-1])
+    pad = lsmgpu.LSM_INPUT_PADDING
+    fd, path = tempfile.mkstemp(prefix="lsm_sst_", dir="/tmp")
+    try:
+        os.write(fd, enc["buf"][:total].cpu().numpy().tobytes() + bytes(pad))  # the GPU-encoded table
+        os.fsync(fd)
+        size = total + pad
+        mm = mmap.mmap(fd, size, mmap.MAP_SHARED, mmap.PROT_READ | mmap.PROT_WRITE)
+        hbuf_np = np.frombuffer(mm, dtype=np.uint8)
+        hbuf = torch.from_numpy(hbuf_np)
+        hip = _hip()
+        t0 = time.perf_counter()
+        rc = hip.hipHostRegister(hbuf.data_ptr(), size, 0)
+        reg_ms = (time.perf_counter() - t0) * 1e3
+        registered = rc == 0
+        chunks = []
+        for b0 in range(0, nb, chunk_blocks):
+            b1 = min(nb, b0 + chunk_blocks)
+            s0 = int(off[b0]) & ~15
+            rel = torch.from_numpy(off[b0:b1 + 1] - s0).pin_memory()
+            chunks.append((b0, b1, s0, int(off[b1]) - s0 + pad, rel))
+        dev = torch.device("cuda")
+        max_bytes = max(c[3] for c in chunks)
+        max_n = max(c[1] - c[0] for c in chunks)
+        cap = max_n * 1200  # items of a chunk are bounded by its bytes / 3
+        cap = min(cap, max_bytes // 3 + 1)
+        dbuf = [torch.empty(max_bytes, dtype=torch.uint8, device=dev) for _ in range(2)]
+        doff = [torch.empty(max_n + 1, dtype=torch.int64, device=dev) for _ in range(2)]
+        decs = [lsmgpu.Decoder(dev) for _ in range(2)]
+        outs = [decs[k].alloc_outputs(cap, max_n, fields=DATA_FIELDS) for k in range(2)]
+        hout = {f: torch.empty(total // 3 + 1, dtype=outs[0][f].dtype).pin_memory() for f in DATA_FIELDS}
+        hstart = torch.empty(nb + 1, dtype=torch.int32).pin_memory()
+        s_in, s_dec, s_out = torch.cuda.Stream(), torch.cuda.Stream(), torch.cuda.Stream()
+        free = [torch.cuda.Event() for _ in range(2)]
+        staging = None if registered else [torch.empty(max_bytes, dtype=torch.uint8).pin_memory() for _ in range(2)]
+        best = None
+        for _ in range(reps):
+            torch.cuda.synchronize()
+            t0 = time.perf_counter()
+            item_base = 0
+            for i, (b0, b1, s0, nbytes, rel) in enumerate(chunks):
+                k = i % 2
+                n = b1 - b0
+                with torch.cuda.stream(s_in):
+                    if i >= 2:
+                        s_in.wait_event(free[k])
+                    if registered:
+                        dbuf[k][:nbytes].copy_(hbuf[s0:s0 + nbytes], non_blocking=True)
+                    else:  # page-cache copy into pinned staging, then DMA
+                        free[k].synchronize()
+                        staging[k][:nbytes].copy_(hbuf[s0:s0 + nbytes])
+                        dbuf[k][:nbytes].copy_(staging[k][:nbytes], non_blocking=True)
+                    doff[k][:n + 1].copy_(rel, non_blocking=True)
+                s_dec.wait_stream(s_in)
+                decs[k].decode(dbuf[k], doff[k], n, outs[k], cap, stream=s_dec)
+                s_out.wait_stream(s_dec)
+                with torch.cuda.stream(s_out):
+                    # item counts of this chunk: known from the fixed shape only after decode; copy the
+                    # item_start row and the SoA prefix sized by the chunk's trailer counts
+                    hstart[b0:b1 + 1].copy_(outs[k]["item_start"][:n + 1], non_blocking=True)
+                    ni = n * ipb  # the fixed-shape workload; item_start is checked after the run
+                    for f in DATA_FIELDS:
+                        hout[f][item_base:item_base + ni].copy_(outs[k][f][:ni], non_blocking=True)
+                    free[k].record(s_out)
+                item_base += n * ipb
+            torch.cuda.synchronize()
+            el = time.perf_counter() - t0
+            best = el if best is None else min(best, el)
+        assert bool((hout["val_len"][:nb * ipb] == 64).all()) and bool((hout["seqno"][:nb * ipb] == 63).all())
+        rel_starts = hstart[:nb + 1].numpy().astype(np.int64)
+        chunk_first = np.repeat([c[0] for c in chunks], [c[1] - c[0] + 1 for c in chunks])
+        assert (rel_starts[:len(chunk_first)] % ipb == 0).all()
+        if registered:
+            hip.hipHostUnregister(hbuf.data_ptr())
+        del hbuf, hbuf_np
+        mm.close()
+    finally:
+        os.close(fd)
+        os.unlink(path)
+    return {"GiB_per_s": round(total / best / 2 ** 30, 3), "ms": round(best * 1e3, 3), "blocks": nb,
+            "chunk_blocks": chunk_blocks, "register_ms": round(reg_ms, 2),
+            "path": "hipHostRegister of the mmap'd file pages" if registered else "page cache -> pinned staging",
+            "note": "mmap'd SST file -> H2D -> decode -> D2H parsed SoA (25 B/item), 3 streams, double-buffered"}
+
+
+def host_inclusive_encode(torch, lsmgpu, items_host, starts_np, nb_all, max_blocks=262144, chunk_blocks=32768,
+                          reps=2):
+    """Items start in a pinned host write buffer (the flush / compaction output
+    side): chunked H2D of the item SoA -> encode -> D2H of the on-disk blocks
+    into a pinned host output, three streams, double-buffered."""
+    import numpy as np
+    nb = min(max_blocks, nb_all)
+    n_items = int(starts_np[nb])
+    ko, vo = items_host.key_off, items_host.val_off
+    hk = torch.from_numpy(items_host.keys[:int(ko[n_items])]).pin_memory()
+    hv = torch.from_numpy(items_host.vals[:int(vo[n_items])]).pin_memory()
+    hko = torch.from_numpy(ko[:n_items + 1].view(np.int64)).pin_memory()
+    hvo = torch.from_numpy(vo[:n_items + 1].view(np.int64)).pin_memory()
+    hsq = torch.from_numpy(items_host.seqno[:n_items].view(np.int64)).pin_memory()
+    hvt = torch.from_numpy(items_host.vtype[:n_items]).pin_memory()
+    hst = torch.from_numpy(starts_np[:nb + 1].astype(np.int32)).pin_memory()
+    chunks = []
+    for b0 in range(0, nb, chunk_blocks):
+        b1 = min(nb, b0 + chunk_blocks)
+        i0, i1 = int(starts_np[b0]), int(starts_np[b1])
+        chunks.append((b0, b1, i0, i1))
+    dev = torch.device("cuda")
+    mi = max(c[3] - c[2] for c in chunks)
+    mk = max(int(ko[c[3]] - ko[c[2]]) for c in chunks)
+    mv = max(int(vo[c[3]] - vo[c[2]]) for c in chunks)
+    mb = max(c[1] - c[0] for c in chunks)
+    pad = lsmgpu.LSM_INPUT_PADDING
+    bufs = [{"keys": torch.zeros(mk + pad, dtype=torch.uint8, device=dev),
+             "vals": torch.zeros(mv + pad, dtype=torch.uint8, device=dev),
+             "key_off": torch.empty(mi + 1, dtype=torch.int64, device=dev),
+             "val_off": torch.empty(mi + 1, dtype=torch.int64, device=dev),
+             "seqno": torch.empty(mi, dtype=torch.int64, device=dev),
+             "vtype": torch.empty(mi, dtype=torch.uint8, device=dev),
+             "starts": torch.empty(mb + 1, dtype=torch.int32, device=dev)} for _ in range(2)]
+    encs = [lsmgpu.Encoder(dev) for _ in range(2)]
+    outs = [None, None]
+    hout = torch.empty(int(ko[n_items]) + int(vo[n_items]) + 64 * nb + 4096, dtype=torch.uint8).pin_memory()
+    hoff = torch.empty(nb + 1, dtype=torch.int64).pin_memory()
+    s_in, s_enc, s_out = torch.cuda.Stream(), torch.cuda.Stream(), torch.cuda.Stream()
+    free = [torch.cuda.Event() for _ in range(2)]
+    # output placement: a chunk's encoded size is only known after its encode; the host stream
+    # waits for the chunk's last block offset (8 B) before issuing its D2H (pipelined one chunk behind)
+    best = None
+    written = 0
+    for _ in range(reps):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        pos = 0
+        pending = None
+        for i, (b0, b1, i0, i1) in enumerate(chunks):
+            k = i % 2
+            n, ni = b1 - b0, i1 - i0
+            kb, vb = int(ko[i0]), int(vo[i0])
+            with torch.cuda.stream(s_in):
+                if i >= 2:
+                    s_in.wait_event(free[k])
+                d = bufs[k]
+                d["keys"][:int(ko[i1]) - kb].copy_(hk[kb:int(ko[i1])], non_blocking=True)
+                d["vals"][:int(vo[i1]) - vb].copy_(hv[vb:int(vo[i1])], non_blocking=True)
+                d["key_off"][:ni + 1].copy_(hko[i0:i1 + 1], non_blocking=True)
+                d["val_off"][:ni + 1].copy_(hvo[i0:i1 + 1], non_blocking=True)
+                d["seqno"][:ni].copy_(hsq[i0:i1], non_blocking=True)
+                d["vtype"][:ni].copy_(hvt[i0:i1], non_blocking=True)
+                d["starts"][:n + 1].copy_(hst[b0:b1 + 1], non_blocking=True)
+                d["key_off"][:ni + 1].sub_(kb)
+                d["val_off"][:ni + 1].sub_(vb)
+                d["starts"][:n + 1].sub_(i0)
+            s_enc.wait_stream(s_in)
+            it = {"keys": d["keys"], "vals": d["vals"], "key_off": d["key_off"][:ni + 1],
+                  "val_off": d["val_off"][:ni + 1], "seqno": d["seqno"][:ni], "vtype": d["vtype"][:ni]}
+            outs[k] = encs[k].encode(it, d["starts"][:n + 1], n, out=outs[k], stream=s_enc)
+            s_out.wait_stream(s_enc)
+            if pending is not None:  # D2H of the previous chunk, now that its size is on the host
+                pk, pn, pb0 = pending
+                torch.cuda.current_stream().synchronize()
+                s_out.synchronize()
+                sz = int(hoff[pb0 + pn].item())
+                with torch.cuda.stream(s_out):
+                    hout[pos:pos + sz].copy_(outs[pk]["buf"][:sz], non_blocking=True)
+                    free[pk].record(s_out)
+                pos += sz
+            with torch.cuda.stream(s_out):
+                hoff[b0:b1 + 1].copy_(outs[k]["block_off"][:n + 1], non_blocking=True)
+            pending = (k, n, b0)
+        s_out.synchronize()
+        pk, pn, pb0 = pending
+        sz = int(hoff[pb0 + pn].item())
+        with torch.cuda.stream(s_out):
+            hout[pos:pos + sz].copy_(outs[pk]["buf"][:sz], non_blocking=True)
+        torch.cuda.synchronize()
+        pos += sz
+        el = time.perf_counter() - t0
+        best = el if best is None else min(best, el)
+        written = pos
+    return {"GiB_per_s": round(written / best / 2 ** 30, 3), "ms": round(best * 1e3, 3), "blocks": nb,
+            "bytes_out": written, "chunk_blocks": chunk_blocks,
+            "note": "pinned host item SoA -> H2D -> encode -> D2H on-disk blocks, 3 streams, double-buffered; "
+                    "rate = encoded bytes / wall"}
+
+
+def load_traffic(kernel, n_blocks):
+    """HBM bytes of one launch of `kernel` over n_blocks, from the newest committed
+    rocprofv3 PMC summary (profiles/traffic_*.json), scaled per block."""
     best, src = None, None
     for p in sorted((ROOT / "profiles").glob("traffic_*.json")):
         try:
-            best, src = json.loads(p.read_text()), p.name
+            d = json.loads(p.read_text())
         except Exception:
-            pass
+            continue
+        entry = d.get(kernel) if isinstance(d, dict) and kernel in d else (d if d.get("kernel") == kernel else None)
+        if entry:
+            best, src = entry, p.name
     if not best:
         return None, None
     return int(round(best["bytes_per_launch"] * n_blocks / best["blocks"])), f"{src} ({best['blocks']} blocks)"
 
 
+def roofline_entry(name, alg_bytes, ms, ceil, traffic_kernel, nb):
+    achieved = alg_bytes / (ms * 1e-3) / 1e9
+    traffic, src = load_traffic(traffic_kernel, nb)
+    return {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
+            "frac": round(achieved / HBM_PEAK_GBPS, 4), "traffic": traffic, "traffic_source": src,
+            "kernel": name, "kernel_ms": round(ms, 4), "alg_bytes_per_launch": alg_bytes,
+            "practical_peak": ceil, "frac_of_copy_ceiling": round(achieved / ceil["copy_GBps"], 4) if ceil else None}
+
+
+# --------------------------------------------------------------------- main
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -513,13 +785,13 @@ def main():
     ap.add_argument("--warmup", type=int, default=3)
     ap.add_argument("--blocks", type=int, default=1 << 20)
     ap.add_argument("--no-cpu", action="store_true")
-    ap.add_argument("--no-host", action="store_true", help="skip the host-inclusive (PCIe) measurement")
-    ap.add_argument("--cpu-seconds", type=float, default=10.0)
-    ap.add_argument("--tuning", type=str, default="", help="bpw,stage_bytes,tile_items")
-    ap.add_argument("--skip-verify", action="store_true")
-    ap.add_argument("--no-extra", action="store_true", help="skip the configs[3]/[4] and point-read legs")
+    ap.add_argument("--no-host", action="store_true", help="skip the host-inclusive (PCIe) measurements")
+    ap.add_argument("--cpu-seconds", type=float, default=2.0, help="minimum seconds per CPU baseline leg")
+    ap.add_argument("--skip-verify", action="store_true", help="(profiling only) skip the full oracle checks")
+    ap.add_argument("--no-extra", action="store_true", help="skip the configs[3]/[4] and side legs")
     args = ap.parse_args()
 
+    import numpy as np
     import torch
     import lsmgpu
 
@@ -534,6 +806,7 @@ def main():
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
+    threads = host_threads(world)
 
     def barrier():
         if dist is not None:
@@ -541,7 +814,6 @@ def main():
         torch.cuda.synchronize()
 
     nb = args.blocks
-    tuning = tuple(int(x) for x in args.tuning.split(",")) if args.tuning else None
     check_cut_rule(lsmgpu, 52, 16, 64)
     t_gen = time.perf_counter()
     items, starts, n_items = make_workload(torch, lsmgpu, nb, seed=0x5EED0002 + rank)
@@ -549,20 +821,26 @@ def main():
     enc = encoder.encode(items, starts, nb)
     torch.cuda.synchronize()
     total_bytes = int(enc["block_off"][nb].item())
+    dec_ctx = lsmgpu.Decoder(dev)
+    out = dec_ctx.alloc_outputs(n_items, nb, fields=DATA_FIELDS)
     log(f"[rank {rank}] generated+encoded {nb} blocks, {n_items} items, {total_bytes / 2**30:.3f} GiB "
         f"in {time.perf_counter() - t_gen:.1f}s")
 
-    dec_ctx = lsmgpu.Decoder(dev)
-    item_cap = n_items
-    out = dec_ctx.alloc_outputs(item_cap, nb, fields=DATA_FIELDS)
-    blocks, boff = enc["buf"], enc["block_off"]
-
-    def step(tun=tuning):
-        dec_ctx.decode(blocks, boff, nb, out, item_cap, tuning=tun)
+    def step():
+        encoder.encode(items, starts, nb, out=enc)
+        dec_ctx.decode(enc["buf"], enc["block_off"], nb, out, n_items)
 
     step()
     torch.cuda.synchronize()
-    checked = 0 if args.skip_verify else verify_sample(torch, lsmgpu, items, starts, enc, out, nb, n_items, rank)
+    ref_buf = ref_off = items_host = starts_np = None
+    if not args.skip_verify:
+        t_chk = time.perf_counter()
+        ref_buf, ref_off = check_encode_all(torch, items, starts, enc, nb, n_items, threads)
+        check_decode_all(out, ref_buf, ref_off, nb, threads)
+        items_host = host_items(items, n_items)
+        starts_np = starts.cpu().numpy().astype(np.uint32)
+        log(f"[rank {rank}] all {nb} blocks bit-exact vs the oracle (encode bytes + decoded fields) "
+            f"in {time.perf_counter() - t_chk:.1f}s")
 
     for _ in range(args.warmup):
         step()
@@ -574,9 +852,8 @@ def main():
         step()
     e1.record()
     barrier()
-    wall = time.perf_counter() - t0
+    el = time.perf_counter() - t0
     gpu_ms = e0.elapsed_time(e1)
-    el = wall
     if dist is not None:
         t = torch.tensor([el], dtype=torch.float64, device=dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
@@ -589,54 +866,59 @@ def main():
     ms_per_step = el * 1e3 / args.steps
     value = all_bytes * args.steps / el / 2 ** 30
 
-    # dominant kernel alone (decode_blocks_kernel, item_start precomputed), HIP events on its stream
-    base = tuning or (0, 0, 0)
-    ktun = (base[0], base[1], base[2], lsmgpu.DECODE_ITEM_START_VALID)
-    for _ in range(2):
-        step(ktun)
-    k0, k1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    k0.record()
-    for _ in range(args.steps):
-        step(ktun)
-    k1.record()
-    torch.cuda.synchronize()
-    kernel_ms = k0.elapsed_time(k1) / args.steps
-    alg_bytes = total_bytes + n_items * PARSED_BYTES_PER_ITEM + nb * PER_BLOCK_OUT
-    achieved = alg_bytes / (kernel_ms * 1e-3) / 1e9
-    traffic, traffic_src = load_traffic(nb)
+    # each direction alone, HIP events on its launch stream
+    def timed(fn, reps):
+        fn()
+        torch.cuda.synchronize()
+        a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        a.record()
+        for _ in range(reps):
+            fn()
+        b.record()
+        torch.cuda.synchronize()
+        return a.elapsed_time(b) / reps
 
-    # encode (config 3 round trip) throughput on the same batch
-    torch.cuda.synchronize()
-    c0, c1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
-    esteps = max(3, args.steps // 4)
-    c0.record()
-    for _ in range(esteps):
-        encoder.encode(items, starts, nb, out=enc)
-    c1.record()
-    torch.cuda.synchronize()
-    enc_ms = c0.elapsed_time(c1) / esteps
+    reps = max(5, args.steps // 2)
+    enc_ms = timed(lambda: encoder.encode(items, starts, nb, out=enc), reps)
+    dec_ms = timed(lambda: dec_ctx.decode(enc["buf"], enc["block_off"], nb, out, n_items), reps)
+    kdec_ms = timed(lambda: dec_ctx.decode(enc["buf"], enc["block_off"], nb, out, n_items,
+                                           tuning=(0, 0, 0, lsmgpu.DECODE_ITEM_START_VALID)), reps)
+    ceil = ceilings(torch) if rank == 0 else None
+    dec_alg = total_bytes + n_items * PARSED_BYTES_PER_ITEM + nb * PER_BLOCK_OUT
+    key_val = int(items["key_off"][n_items].item()) + int(items["val_off"][n_items].item())
+    enc_alg = key_val + n_items * ENC_IN_PER_ITEM + 4 * (nb + 1) + total_bytes + 8 * (nb + 1) + 4 * nb
+    r_dec = roofline_entry("decode_blocks_kernel (item_start precomputed)", dec_alg, kdec_ms, ceil,
+                           "decode_blocks_kernel", nb)
+    r_dec["read_only_frac"] = round(total_bytes / (kdec_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
+    r_enc = roofline_entry("lsm_encode_blocks (encode_sizes_kernel + scan + encode_write_kernel)", enc_alg, enc_ms,
+                           ceil, "lsm_encode_blocks", nb)
+    dominant = r_enc if enc_ms >= kdec_ms else r_dec
 
-    dec_ms = kernel_ms  # the decode kernel alone (item_start precomputed), for the round trip
     extra = {}
     if not args.no_extra:
-        extra["point_read"] = bench_point_read(torch, lsmgpu, items, starts, enc, nb, n_items)
+        extra["point_read"] = bench_point_read(torch, lsmgpu, items, enc, nb, n_items)
         extra["file_checksum"] = bench_file_checksum(torch, lsmgpu, enc, total_bytes)
         extra["bloom"] = bench_bloom(torch, lsmgpu, items, n_items)
         if rank == 0:
             extra["lz4"] = bench_lz4(torch, lsmgpu, enc, nb)
+    hostinc = {}
+    if rank == 0 and world == 1 and not args.no_host and ref_buf is not None:
+        hostinc["decode_from_mmap"] = host_inclusive_decode(torch, lsmgpu, enc, nb)
+        hostinc["encode_from_host_buffer"] = host_inclusive_encode(torch, lsmgpu, items_host, starts_np, nb)
+    del out, items
+    torch.cuda.empty_cache()
+    if not args.no_extra and not args.skip_verify:
         if world == 1:
-            extra["config4"] = bench_config4(torch, lsmgpu, max(3, args.steps // 4), rank)
-        extra["config5"] = bench_config5(torch, lsmgpu, max(3, args.steps // 4), rank, world, dist, dev)
-
-    hostinc = None
-    if rank == 0 and world == 1 and not args.no_host:
-        hostinc = host_inclusive(torch, lsmgpu, enc, out["item_start"], nb)
+            extra["config4"] = bench_config4(torch, lsmgpu, max(3, args.steps // 4), rank, threads)
+        extra["config5"] = bench_config5(torch, lsmgpu, max(3, args.steps // 4), rank, world, dist, dev, threads)
 
     cpu = None
-    if rank == 0 and world == 1 and not args.no_cpu:
-        cpu = cpu_baseline(torch, enc, nb, min_seconds=args.cpu_seconds)
+    if rank == 0 and world == 1 and not args.no_cpu and ref_buf is not None:
+        cpu = cpu_baseline(ref_buf, ref_off, items_host, starts_np, min_seconds=args.cpu_seconds)
 
     if rank == 0:
+        verified = "skipped" if args.skip_verify else f"all {nb} blocks per rank bit-exact vs the oracle (encoded bytes " \
+                                                      f"and every decoded field)"
         line = {
             "metric": BASELINE_METRIC,
             "value": round(value, 3),
@@ -649,28 +931,24 @@ def main():
             "scaling": "weak",
             "vs_baseline": None,
             "dtype": "u8",
-            "data": "synthetic (16 B BE-counter keys, 64 B random values, seqno 63; GPU-encoded, sample "
-                    f"checked bit-exact vs oracle: {checked} blocks)",
-            "config": {"workload": "BASELINE configs[1]: decode 1 M x 4 KiB data blocks, device-resident",
+            "data": f"synthetic (16 B BE-counter keys, 64 B random values, seqno 63); {verified}",
+            "config": {"workload": "BASELINE configs[1]/[2]: encode + decode round trip of 1 M x 4 KiB data blocks, "
+                                   "device-resident",
                        "blocks_per_gpu": nb, "items_per_gpu": n_items, "block_bytes_per_gpu": total_bytes,
                        "restart_interval": 16, "hash_ratio": 0.0, "key_len": 16, "val_len": 64,
-                       "parallelism": f"shard{world} (independent block batches, no collective)",
-                       "tuning": list(tuning) if tuning else "default"},
-            "roofline": {"bound": "hbm", "achieved": round(achieved, 1), "peak": HBM_PEAK_GBPS, "unit": "GB/s",
-                         "frac": round(achieved / HBM_PEAK_GBPS, 4),
-                         "traffic": traffic, "traffic_source": traffic_src,
-                         "kernel": "decode_blocks_kernel", "kernel_ms": round(kernel_ms, 4),
-                         "alg_bytes_per_launch": alg_bytes,
-                         "read_only_frac": round(total_bytes / (kernel_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)},
+                       "step": "lsm_encode_blocks (item SoA -> blocks) + lsm_decode_blocks (blocks -> parsed SoA)",
+                       "parallelism": f"shard{world} (independent block batches, no collective)"},
+            "roofline": dominant,
+            "roofline_decode": r_dec,
+            "roofline_encode": r_enc,
             "cpu_baseline": cpu,
-            "encode": {"GiB_per_s_written": round(total_bytes / (enc_ms * 1e-3) / 2 ** 30, 3),
-                       "ms": round(enc_ms, 4)},
-            "config3_roundtrip": {"workload": "BASELINE configs[2]: encode + checksum + decode of the same batch, "
-                                              "bit-exact block bytes vs the oracle (sampled)",
-                                  "encode_ms": round(enc_ms, 4), "decode_ms": round(dec_ms, 4),
-                                  "GiB_per_s": round(total_bytes / ((enc_ms + dec_ms) * 1e-3) / 2 ** 30, 3)},
+            "encode": {"ms": round(enc_ms, 4), "GiB_per_s_written": round(total_bytes / (enc_ms * 1e-3) / 2 ** 30, 3)},
+            "decode": {"ms": round(dec_ms, 4), "GiB_per_s": round(total_bytes / (dec_ms * 1e-3) / 2 ** 30, 3),
+                       "kernel_ms": round(kdec_ms, 4),
+                       "note": "whole lsm_decode_blocks call (trailer counts + scan + decode kernel)"},
+            "round_trip_traffic_GiB_per_s": round(2 * value, 3),
             **extra,
-            "host_inclusive_decode": hostinc,
+            "host_inclusive": hostinc or None,
             "gpu_event_ms_per_step": round(gpu_ms / args.steps, 4),
         }
         print(json.dumps(line), flush=True)

@@ -166,4 +166,5 @@ def test_gpu_reference_headers(gpu):
     torch.cuda.synchronize()
     st = dec["status"][:3].cpu().numpy().tolist()
     assert st[0] == want[0] and st[2] == want[1]
-    assert want[1] == 3 and want[0] == 4  # HDR_CKSUM for the mutation; CKSUM (no payload) for the round trip
+    # sorted names: [block_header_detect_corruption, block_header_serde_roundtrip]
+    assert want == [3, 4]  # HDR_CKSUM for the mutation; CKSUM for the round trip (the test header has no payload)
