@@ -7,19 +7,20 @@
 // the payload xxh3_128 and the 33-byte header are fused into the same pass.
 //
 // Pipeline (all on one stream, DESIGN.md "Encode kernels"):
-//   E1  size pass, one wave per block: per item (lane) the shared prefix
-//       with the restart head (encoder.rs:140-143) and the record length;
-//       wave scan -> records bytes, binary-index step, hash-index size.
+//   E1  encode_plan_kernel, thread per item over runs of 16 blocks: shared
+//       prefix with the restart head (encoder.rs:140-143), record length,
+//       LDS-atomic sums per block -> block size, binary-index step,
+//       hash-index size, size class, key / value span starts.
 //   S   device exclusive scan of block sizes -> d_block_off (packed output).
-//   E2  write pass, one wave per block: key/value spans staged HBM->LDS in
-//       coalesced 16 B/lane sweeps, each lane assembles its record in the LDS
-//       payload image (dword stores inside records, byte stores at seams),
-//       binary index, hash index (LDS min/max atomics reproduce the
-//       order-independent FREE/idx/CONFLICT rule, hash_index/builder.rs:64-110),
-//       trailer, wave xxh3_128 over the image, header, then one coalesced
-//       16 B/lane copy-out to the block's place in the packed output.
-//   E3  same algorithm straight on HBM for blocks whose staging does not fit
-//       the LDS budget (grid-stride over a device list).
+//   E2  encode_group_kernel: 4-wave workgroups write runs of consecutive
+//       blocks in groups staged by LDS-DMA (key and value spans), thread per
+//       record into an LDS image of the group's output span, binary index,
+//       hash index (LDS min/max atomics reproduce the order-independent
+//       FREE/idx/CONFLICT rule, hash_index/builder.rs:64-110), trailer, the
+//       payload xxh3_128 split over the workgroup's 16 DPP rows in 1 KiB
+//       units, headers, one coalesced 16 B/lane copy-out.
+//   L   blocks that do not fit a group: listed 1-wave kernels (LDS image of
+//       20 / 96 KiB) or E3 straight in HBM.
 #include <hip/hip_runtime.h>
 
 #include <math.h>
@@ -31,15 +32,13 @@
 
 namespace lsmgpu {
 
-// Block classes by the LDS image a block needs (e2_need): small blocks are
-// written by 4-wave workgroups with kImgSmall bytes of LDS per wave (8
-// workgroups per CU), medium and big ones by listed 1-wave workgroups, and
-// the rest straight in HBM (E3).
+// Block classes: blocks that fit the group kernel's budget (group_fits) are
+// written by encode_group_kernel; the others are listed by the size scan and
+// written, by the LDS image they need (e2_need), by 1-wave workgroups with a
+// 20 KiB (medium) or 96 KiB (big) image, or straight in HBM (E3, huge).
 constexpr uint32_t kPlanHuge = 1, kPlanBad = 2, kPlanMedium = 4, kPlanBig = 8;
-constexpr uint32_t kImgSmall = 5 * 1024;
 constexpr uint32_t kImgMedium = 20 * 1024;
 constexpr uint32_t kImgBig = 96 * 1024;
-constexpr uint32_t kSmallWaves = 4;
 constexpr uint32_t kE3HashChunk = 4096;    // buckets per LDS pass in E3
 constexpr uint64_t kListedOne = 1ULL << 40, kOffMask = kListedOne - 1;
 
@@ -110,7 +109,8 @@ struct EncodeParams {
   uint64_t out_cap;
   uint64_t* block_off;
   int32_t* status;
-  uint16_t* shared;     // [n_items]
+  uint64_t* kspan;      // [n_blocks + 1] key_off of each block's first item (E1 -> E2 stage spans)
+  uint64_t* vspan;      // [n_blocks + 1] val_off of each block's first item
   uint64_t* sizes;      // [n_blocks] block bytes (E1) -> exclusive scan -> block_off
   BlockPlan* plans;     // [n_blocks]
   uint32_t* lists;      // [n_blocks]: the listed blocks in block order (from the size scan)
@@ -484,15 +484,13 @@ __device__ __forceinline__ void write_block_lds(const EncodeParams& P, uint32_t 
   uint32_t carry = 0;
   for (uint32_t c = 0; c < n; c += kWave) {
     const uint32_t j = c + lane;
-    const uint64_t i = (uint64_t)s + j;
     const bool head = j % ri == 0;
     ItemMeta m;
     RecordCopy rc;
     uint32_t rec = 0;
     if (j < n) {
       bool bad = false;
-      m = load_item(P, i, bad);
-      if (!is_index(P)) m.sh = P.shared[i];
+      m = load_item_lcp(P, s, j, ri, bad);
       rec = (uint32_t)item_record_len(P, m, head);
     }
     const uint32_t incl = wave_incl_scan_u32(rec);
@@ -513,112 +511,533 @@ __device__ __forceinline__ void write_block_lds(const EncodeParams& P, uint32_t 
   finish_block_lds(P, b, pl, n, ri, img, hlo, hhi, pad, total, reinterpret_cast<uint8_t*>(dabs & ~15ULL));
 }
 
-// ---------------------------------------------------------------- E1: sizes
-// One wave per block: item fields, shared prefixes (stored for E2) and record
-// sizes -> block bytes, binary-index step, hash-index size, size class.
-__global__ __launch_bounds__(256) void encode_sizes_kernel(EncodeParams P) {
-  const int lane = threadIdx.x & 63;
-  const uint32_t b = blockIdx.x * 4 + (threadIdx.x >> 6);
-  if (b >= P.n_blocks) return;
-  const uint32_t s = P.starts[b], e = P.starts[b + 1];
-  const uint32_t ri = is_index(P) ? 1 : P.ri;
-  bool bad = e <= s;
-  const uint32_t n = bad ? 0 : e - s;
-  uint64_t carry = 0, last_head = 0;
-  const uint32_t lh = n ? ((n - 1) / ri) * ri : 0;
-  for (uint32_t c = 0; c < n; c += kWave) {
-    const uint32_t j = c + lane;
-    uint64_t rec = 0;
-    if (j < n) {
-      const ItemMeta m = load_item_lcp(P, s, j, ri, bad);
-      if (!is_index(P)) P.shared[(uint64_t)s + j] = (uint16_t)m.sh;
-      rec = item_record_len(P, m, j % ri == 0);
-    }
-    const uint64_t incl = wave_incl_scan_u64(rec);
-    if (lh >= c && lh < c + kWave) last_head = carry + wave_bcast_u64(incl - rec, lh - c);
-    carry += wave_bcast_u64(incl, 63);
+// Group write kernel (E2) budget, see encode_group_kernel.
+constexpr uint32_t kGWaves = 4, kGThreads = kGWaves * kWave;
+constexpr uint32_t kGRun = 32;                 // blocks per workgroup
+constexpr uint32_t kGBlocks = 16;              // blocks per group
+constexpr uint32_t kGItems = 256;              // items per group (one thread each)
+constexpr uint32_t kGSlack = 48;               // readable bytes past each staged span
+constexpr uint32_t kGKeys = 4096, kGVals = 14400, kGImg = 15872;
+constexpr uint32_t kGUnits = kGImg / 1024 + kGBlocks + 1;  // hash units per group
+constexpr uint32_t kGUnion = 4096;             // kofs + xs + hash votes | hash contributions
+constexpr uint32_t kGHash = (kGUnion - 4 * (kGItems + 4) - 4 * kGItems) / 8;  // vote pairs
+static_assert(kGUnits * 64 <= kGUnion, "hash contributions");
+
+
+__device__ __host__ __forceinline__ bool group_fits(uint64_t n, uint64_t kspan, uint64_t vspan, uint64_t total,
+                                                    uint32_t hash_w) {
+  return n <= kGItems && kspan + 15 <= kGKeys && vspan + 15 <= kGVals && total + 15 <= kGImg && hash_w <= kGHash;
+}
+
+// ---------------------------------------------------------------- E1: plan
+// Flat over items: a 256-thread workgroup owns kPlanBlocks consecutive blocks
+// and walks their items (contiguous) with one thread per item, so every load
+// is coalesced and all of a workgroup's items are in flight together.  Per
+// item: key / value lengths, the shared prefix with its restart head
+// (encoder.rs:140-143, util.rs:125-130, head key read from L1/L2) and the
+// record length; LDS atomics sum them per block (and from the last restart
+// head on, for the binary-index step).  Per block: size, binary-index step,
+// hash-index size, size class, and the key / value span starts E2 stages.
+constexpr uint32_t kPlanBlocks = 16;
+
+__global__ __launch_bounds__(256) void encode_plan_kernel(EncodeParams P) {
+  __shared__ uint32_t bst[kPlanBlocks + 1];
+  __shared__ unsigned long long recs[kPlanBlocks], tail[kPlanBlocks];
+  __shared__ uint32_t badf[kPlanBlocks];
+  __shared__ uint32_t mono;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t b0 = blockIdx.x * kPlanBlocks;
+  const uint32_t nb = min(kPlanBlocks, P.n_blocks - b0);
+  if (tid <= nb) bst[tid] = P.starts[b0 + tid];
+  if (tid < nb) {
+    recs[tid] = 0;
+    tail[tid] = 0;
+    badf[tid] = 0;
   }
-  bad = __ballot(bad) != 0;
-  if (lane != 0) return;
+  if (tid == 0) mono = 1;
+  __syncthreads();
+  if (tid < nb && bst[tid + 1] < bst[tid]) mono = 0;  // (benign race: every writer stores 0)
+  __syncthreads();
+  const uint32_t ri = is_index(P) ? 1 : P.ri;
+  // a non-monotone item_start run is a caller error: its blocks are rejected below
+  const uint64_t i_begin = bst[0], i_end = mono ? bst[nb] : bst[0];
+  for (uint64_t i = i_begin + tid; i < i_end; i += 256) {
+    uint32_t lo = 0, hi = nb;  // block j: bst[j] <= i < bst[j + 1]
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (bst[mid] <= i) lo = mid;
+      else hi = mid;
+    }
+    const uint32_t j = lo, s = bst[j], e = bst[j + 1];
+    const uint32_t jj = (uint32_t)(i - s);
+    bool bad = false;
+    const ItemMeta m = load_item_lcp(P, s, jj, ri, bad);
+    const uint64_t rec = item_record_len(P, m, jj % ri == 0);
+    atomicAdd(&recs[j], (unsigned long long)rec);
+    if (jj >= ((e - s - 1) / ri) * ri) atomicAdd(&tail[j], (unsigned long long)rec);
+    if (bad) atomicOr(&badf[j], 1u);
+  }
+  __syncthreads();
+  if (tid >= nb) return;
+  const uint32_t b = b0 + tid, s = bst[tid], e = bst[tid + 1];
+  bool bad = !mono || e <= s || badf[tid];
+  const uint32_t n = bad ? 0 : e - s;
+  const uint64_t carry = recs[tid], last_head = carry - tail[tid];
   const uint32_t bin_len = n ? (n + ri - 1) / ri : 0;
   const uint32_t step = last_head <= 0xFFFF ? 2 : 4;
   const uint32_t buckets = is_index(P) ? 0 : bucket_count(n, P.ratio);
   const uint32_t hash_w = (buckets > 0 && bin_len <= kHashMaxPointers) ? buckets : 0;
   const uint64_t total = kHdrLen + carry + 1 + (uint64_t)bin_len * step + hash_w + kTrailerLen;
   if (carry > 0xFFFFFFF0ULL || total > 0xFFFFFF00ULL) bad = true;
+  const uint64_t ks = P.it.key_off[s], ke = P.it.key_off[e];
+  const uint64_t vs = is_index(P) ? 0 : P.it.val_off[s], ve = is_index(P) ? 0 : P.it.val_off[e];
   uint32_t flags = 0;
   if (bad) {
     flags = kPlanBad;
     P.status[b] = ST_BAD_ARG;
-  } else {
+  } else if (!group_fits(n, ke - ks, ve - vs, total, hash_w)) {
     const uint64_t need = e2_need(total, hash_w);
-    if (need > kImgSmall || n > kWave)
-      flags = need <= kImgMedium ? kPlanMedium : need <= kImgBig ? kPlanBig : kPlanHuge;
+    flags = need <= kImgMedium ? kPlanMedium : need <= kImgBig ? kPlanBig : kPlanHuge;
   }
   P.plans[b] = BlockPlan{(uint32_t)carry, bin_len, hash_w, step | (flags << 8)};
-  // bits 40.. count the listed (not small) blocks: the size scan numbers them
-  // (no global atomics: one counter serialised a batch of uniformly large blocks)
+  // bits 40.. count the listed (not group) blocks: the size scan numbers them
   P.sizes[b] = (bad ? 0 : total) | ((flags & (kPlanMedium | kPlanBig | kPlanHuge)) ? kListedOne : 0);
+  P.kspan[b] = ks;
+  P.vspan[b] = vs;
+  if (b + 1 == P.n_blocks) {
+    P.kspan[b + 1] = ke;
+    P.vspan[b + 1] = ve;
+  }
 }
 
-// ------------------------------------------------- E2: small blocks in LDS
-// kSmallWaves waves per workgroup, one block (<= 64 items, image <= kImgSmall)
-// per wave, lane = item: all of a lane's loads (item fields, key and value
-// windows) are in flight together, then the record is stored into the image.
-#ifndef LSM_ENC_WPE
-#define LSM_ENC_WPE 5
-#endif
-__global__ __launch_bounds__(kSmallWaves * kWave) __attribute__((amdgpu_waves_per_eu(LSM_ENC_WPE))) void encode_write_kernel(EncodeParams P) {
-  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
-  const uint32_t wave = __builtin_amdgcn_readfirstlane(threadIdx.x >> 6);
-  const int lane = threadIdx.x & 63;
-  const uint32_t b = blockIdx.x * kSmallWaves + wave;
-  if (b >= P.n_blocks) return;
-  const BlockPlan pl = P.plans[b];
-  if ((pl.step_flags >> 8) != 0) return;  // listed (medium / big / huge) or rejected
-  const uint32_t s = P.starts[b], n = P.starts[b + 1] - s;
-  const uint64_t off = P.block_off[b], end = P.block_off[b + 1];
-  if (end > P.out_cap) {
-    if (lane == 0) P.status[b] = ST_OVERFLOW;
-    return;
+// ------------------------------------------------ E2: group write kernel
+// One 4-wave workgroup owns kGRun consecutive blocks and writes them in
+// GROUPS: the longest run of consecutive group-class blocks whose items,
+// key bytes, value bytes, encoded bytes and hash-index buckets fit the LDS
+// budget (one 4 KiB data block is ~1/4 of a group; a 16 KiB one fills it).
+// Consecutive blocks' items are contiguous in the arenas and their encoded
+// bytes are contiguous in the output, so per group:
+//   DMA    key and value spans HBM -> LDS stage (global_load_lds, 1 KiB per
+//          wave instruction); thread t loads item t's offsets, seqno, type
+//   shape  thread = item: shared prefix with its restart head (from the
+//          stage), record length, workgroup scan -> record offset in block
+//   write  thread = item: its record (header bytes, key suffix, value LEB +
+//          bytes) into the LDS image of the group's output span, binary
+//          index entry, hash-index vote; the next group's DMA is issued
+//   tails  wave per block: marker, hash-index bytes, trailer
+//   hash   the 16 DPP rows of the workgroup split every block's payload
+//          into 1 KiB units (XXH3 per-KiB contributions, then one short
+//          serial scramble chain per block)
+//   header wave 0, lane per block: header fields + 29-byte checksum
+//   out    one contiguous 16 B/lane copy of the group's span
+// Blocks that do not fit are written by the list / HBM kernels.
+struct GBlk {
+  uint32_t it0, n;         // first item (group-relative), items
+  uint32_t img, plen;      // header position in the image, payload length
+  uint32_t recs, bin_len;  // record bytes, restart heads
+  uint32_t step, hash_w;   // binary-index step, hash-index buckets
+  uint32_t hash_base, u0;  // first vote pair, first hash unit
+  uint32_t nbk, pad;       // full KiB units of the payload
+  uint64_t ck_lo, ck_hi;   // payload xxh3_128
+};
+static_assert(sizeof(GBlk) == 64, "GBlk");
+
+struct GroupLds {
+  uint8_t keys[kGKeys + kGSlack];
+  uint8_t vals[kGVals + kGSlack];
+  uint8_t img[kGImg + kGSlack];
+  uint32_t uni[kGUnion / 4];
+  GBlk blk[kGBlocks];
+  LongSecret secret;
+  uint32_t wsum[kGWaves];
+};
+
+
+// n bytes src[s ..) (LDS) -> dst[d ..) (LDS): byte stores for the dst bytes
+// that share a dword with a neighbour record, aligned dword stores inside
+// (each from two source dwords and v_alignbyte); reads up to 8 bytes past.
+__device__ __forceinline__ void lds_copy(uint8_t* dst, uint32_t d, const uint8_t* src, uint32_t s, uint32_t n) {
+  if (!n) return;
+  const uint32_t h = min(n, (4u - (d & 3u)) & 3u);
+  for (uint32_t k = 0; k < h; ++k) dst[d + k] = src[s + k];
+  if (n == h) return;
+  const uint32_t d1 = d + h, e = d + n, body = ((e & ~3u) - d1) >> 2;
+  const uint32_t sp = s + h, sh = sp & 3u;
+  const uint32_t* s32 = reinterpret_cast<const uint32_t*>(src + (sp & ~3u));
+  uint32_t* d32 = reinterpret_cast<uint32_t*>(dst + d1);
+  uint32_t prev = s32[0];
+  uint32_t q = 0;
+  for (; q + 4 <= body; q += 4) {
+    const uint32_t a = s32[q + 1], b = s32[q + 2], c = s32[q + 3], x = s32[q + 4];
+    d32[q] = alignbyte(a, prev, sh);
+    d32[q + 1] = alignbyte(b, a, sh);
+    d32[q + 2] = alignbyte(c, b, sh);
+    d32[q + 3] = alignbyte(x, c, sh);
+    prev = x;
   }
+  for (; q < body; ++q) {
+    const uint32_t a = s32[q + 1];
+    d32[q] = alignbyte(a, prev, sh);
+    prev = a;
+  }
+  for (uint32_t k = d1 + 4 * body; k < e; ++k) dst[k] = src[s + (k - d)];
+}
+
+__device__ __forceinline__ uint32_t lds_put_leb(uint8_t* dst, uint32_t pos, uint64_t v) {
+  while (v >= 0x80) {
+    dst[pos++] = (uint8_t)(v | 0x80);
+    v >>= 7;
+  }
+  dst[pos++] = (uint8_t)v;
+  return pos;
+}
+
+// longest_shared_prefix_length (util.rs:125-130) of two staged keys.
+__device__ __forceinline__ uint32_t lcp_lds(const uint8_t* keys, uint32_t a, uint32_t b, uint32_t n) {
+  for (uint32_t k = 0; k < n; k += 16) {
+    const Win16 wa = read_win16(keys, a + k), wb = read_win16(keys, b + k);
+    const uint64_t x0 = wa.lo ^ wb.lo, x1 = wa.hi ^ wb.hi;
+    if (x0) return min(n, k + (uint32_t)(__builtin_ctzll(x0) >> 3));
+    if (x1) return min(n, k + 8 + (uint32_t)(__builtin_ctzll(x1) >> 3));
+  }
+  return n;
+}
+
+// Header::encode_into (header.rs:80-112) of one block by one lane.
+__device__ __forceinline__ void lane_header(uint8_t* dst, uint32_t hp, uint32_t type, uint64_t ck_lo, uint64_t ck_hi,
+                                            uint32_t plen) {
+  const uint64_t w0 = 0x034D534CULL | ((uint64_t)type << 32) | (ck_lo << 40);
+  const uint64_t w1 = (ck_lo >> 24) | (ck_hi << 40);
+  const uint64_t w2 = (ck_hi >> 24) | ((uint64_t)plen << 40);
+  const uint64_t w3 = ((uint64_t)plen >> 24) | ((uint64_t)plen << 8);
+  auto r64 = [&](uint32_t o) -> uint64_t {
+    const uint32_t q = o >> 3, sft = (o & 7) * 8;
+    const uint64_t a = q == 0 ? w0 : q == 1 ? w1 : q == 2 ? w2 : w3;
+    const uint64_t b = q == 0 ? w1 : q == 1 ? w2 : q == 2 ? w3 : 0;
+    return sft ? (a >> sft) | (b << (64 - sft)) : a;
+  };
+  auto r8 = [&](uint32_t o) -> uint32_t { return (uint32_t)(r64(o) & 0xFF); };
+  uint64_t hlo, hhi;
+  xxh3_128_short(29, r8, r64, hlo, hhi);
+  const uint64_t w[4] = {w0, w1, w2, w3};
+#pragma unroll
+  for (int k = 0; k < 29; ++k) dst[hp + k] = (uint8_t)(w[k >> 3] >> (8 * (k & 7)));
+#pragma unroll
+  for (int k = 0; k < 4; ++k) dst[hp + 29 + k] = (uint8_t)((uint32_t)hlo >> (8 * k));
+}
+
+__device__ __forceinline__ void group_barrier() {
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+  __builtin_amdgcn_s_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+}
+
+__global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(4))) void encode_group_kernel(EncodeParams P) {
+  __shared__ GroupLds L;
+  typedef __attribute__((address_space(3))) void lds_void_t;
+  typedef const __attribute__((address_space(1))) void gbl_void_t;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid / kWave);
+  const int lane = tid & (kWave - 1);
+  const uint32_t b_begin = blockIdx.x * kGRun;
+  const uint32_t b_end = min(b_begin + kGRun, P.n_blocks);
   const uint32_t ri = is_index(P) ? 1 : P.ri;
-  const uint32_t step = pl.step_flags & 0xFF;
-  const uint32_t total = (uint32_t)(end - off);
-  const uint64_t dabs = (uint64_t)(uintptr_t)P.out + off;
-  const uint32_t pad = (uint32_t)(dabs & 15);
-  const uint32_t p0 = pad + kHdrLen;
-  const bool head = lane % ri == 0;
-  ItemMeta m;
-  RecordCopy rc;
-  uint32_t rec = 0;
-  if ((uint32_t)lane < n) {
-    bool bad = false;
-    m = load_item(P, (uint64_t)s + lane, bad);
-    if (!is_index(P)) m.sh = P.shared[(uint64_t)s + lane];
-    rec = (uint32_t)item_record_len(P, m, head);
-  }
-  const uint32_t roff = wave_incl_scan_u32(rec) - rec;
-  if ((uint32_t)lane < n) rc.issue(P, m, head, p0 + roff);
-  uint8_t* img = smem + wave * kImgSmall;
-  uint32_t* hlo = reinterpret_cast<uint32_t*>(img + ((pad + total + 15) & ~15u) + 32);
-  uint32_t* hhi = hlo + ((pl.hash_w + 3) & ~3u);
-  for (uint32_t k = lane; k < pl.hash_w; k += kWave) {
-    hlo[k] = 0xFFFFFFFFu;
-    hhi[k] = 0;
-  }
-  wave_lds_sync();
-  if ((uint32_t)lane < n && !(kDiagBuild && (P.diag & 1))) {
-    rc.store(P, m, head, img);
-    if (head) store_le(img, p0 + pl.recs + 1 + (lane / ri) * step, roff, step);
-    if (pl.hash_w) {
-      const uint32_t bk = key_bucket(P, m.ko, m.klen, pl.hash_w);
-      atomicMin(&hlo[bk], lane / ri);
-      atomicMax(&hhi[bk], lane / ri);
+  const bool index = is_index(P);
+  if (tid < sizeof(LongSecret) / 8)
+    reinterpret_cast<uint64_t*>(&L.secret)[tid] = reinterpret_cast<const uint64_t*>(&kLongSecret)[tid];
+  // the run's blocks, lane l = block b_begin + l (every wave holds the same registers)
+  const uint32_t rb = b_begin + lane;
+  const bool in_run = rb <= b_end;
+  const uint32_t r_start = in_run ? P.starts[rb] : 0;
+  const uint64_t r_off = in_run ? P.block_off[rb] : 0;
+  const uint64_t r_ks = in_run ? P.kspan[rb] : 0, r_vs = in_run ? P.vspan[rb] : 0;
+  const BlockPlan r_plan = (in_run && rb < b_end) ? P.plans[rb] : BlockPlan{0, 0, 0, 0};
+  const uint32_t r_hash = r_plan.hash_w;
+  const uint32_t r_hpre = wave_incl_scan_u32(r_hash) - r_hash;  // exclusive prefix over the run
+  auto lane_u32 = [&](uint32_t v, uint32_t l) { return (uint32_t)__shfl((int)v, (int)min(l, 63u)); };
+  auto lane_u64 = [&](uint64_t v, uint32_t l) { return wave_shfl_u64(v, (int)min(l, 63u)); };
+  struct Grp {
+    uint32_t b, k;
+  };
+  // the longest group from block b (k = 0: block b is listed / rejected / over capacity)
+  auto form = [&](uint32_t b) -> Grp {
+    const uint32_t r0 = b - b_begin, rj = r0 + lane;
+    const uint32_t s0 = lane_u32(r_start, r0), s1 = lane_u32(r_start, rj + 1);
+    const uint64_t o0 = lane_u64(r_off, r0), o1 = lane_u64(r_off, rj + 1);
+    const uint64_t k0 = lane_u64(r_ks, r0), k1 = lane_u64(r_ks, rj + 1);
+    const uint64_t v0 = lane_u64(r_vs, r0), v1 = lane_u64(r_vs, rj + 1);
+    const uint32_t flags = lane_u32(r_plan.step_flags, rj) >> 8;
+    const uint32_t hsum = lane_u32(r_hpre, rj + 1) - lane_u32(r_hpre, r0);
+    const bool ok = b + lane < b_end && lane < (int)kGBlocks && flags == 0 && o1 <= P.out_cap &&
+                    group_fits(s1 - s0, k1 - (k0 & ~15ULL), v1 - (v0 & ~15ULL), o1 - (o0 & ~15ULL), hsum);
+    return Grp{b, (uint32_t)__builtin_ctzll(~__ballot(ok))};
+  };
+  auto next_group = [&](uint32_t b) -> Grp {
+    for (;;) {
+      if (b >= b_end) return Grp{b, 0};
+      const Grp g = form(b);
+      if (g.k) return g;
+      const uint32_t fl = lane_u32(r_plan.step_flags, b - b_begin) >> 8;
+      if (fl == 0 && lane == 0) P.status[b] = ST_OVERFLOW;  // group class, but past out_cap
+      ++b;
     }
+  };
+  auto issue_dma = [&](const Grp& g) {
+    const uint32_t r0 = g.b - b_begin;
+    const uint64_t ka = lane_u64(r_ks, r0) & ~15ULL, kb = lane_u64(r_ks, r0 + g.k);
+    const uint64_t va = lane_u64(r_vs, r0) & ~15ULL, vb = lane_u64(r_vs, r0 + g.k);
+    const uint32_t kc = (uint32_t)((kb - ka + 15) >> 4), vc = index ? 0 : (uint32_t)((vb - va + 15) >> 4);
+    const uint8_t* ks = P.it.keys + ka + 16 * lane;
+    for (uint32_t i = wave; i * kWave < kc; i += kGWaves)
+      if (i * kWave + lane < kc)
+        __builtin_amdgcn_global_load_lds((gbl_void_t*)(ks + 1024 * i), (lds_void_t*)(L.keys + 1024 * i), 16, 0, 0);
+    const uint8_t* vs = P.it.vals + va + 16 * lane;
+    for (uint32_t i = wave; i * kWave < vc; i += kGWaves)
+      if (i * kWave + lane < vc)
+        __builtin_amdgcn_global_load_lds((gbl_void_t*)(vs + 1024 * i), (lds_void_t*)(L.vals + 1024 * i), 16, 0, 0);
+  };
+  uint32_t* kofs = L.uni;                          // [kGItems + 1] key offsets in the stage
+  uint32_t* xs = L.uni + kGItems + 4;              // [kGItems] exclusive record-length scan
+  uint32_t* hlo = L.uni + 2 * kGItems + 4;         // [kGHash] vote min
+  uint32_t* hhi = hlo + kGHash;                    // [kGHash] vote max
+  uint64_t* contrib = reinterpret_cast<uint64_t*>(L.uni);  // [kGUnits][4][2] (after the records)
+
+  Grp G = next_group(b_begin);
+  if (G.k) issue_dma(G);
+  while (G.k) {
+    const uint32_t r0 = G.b - b_begin, k = G.k;
+    const uint32_t i0 = lane_u32(r_start, r0), n_items = lane_u32(r_start, r0 + k) - i0;
+    const uint64_t kbase = lane_u64(r_ks, r0) & ~15ULL, vbase = lane_u64(r_vs, r0) & ~15ULL;
+    const uint64_t obase = lane_u64(r_off, r0);
+    const uint64_t dabs = (uint64_t)(uintptr_t)P.out + obase;
+    const uint32_t pad = (uint32_t)(dabs & 15);
+    // ---- item t: fields (in flight with the DMA)
+    const bool live = tid < n_items;
+    const uint64_t gi = (uint64_t)i0 + tid;
+    ItemMeta m{};
+    bool bad = false;
+    if (live) m = load_item(P, gi, bad);
+    // ---- wave 0: the group's block table (lane j = group block j; shuffles with every lane active)
+    if (wave == 0) {
+      const uint32_t rj = r0 + lane;
+      const uint32_t st = lane_u32(r_start, rj), st1 = lane_u32(r_start, rj + 1);
+      const uint64_t of = lane_u64(r_off, rj), of1 = lane_u64(r_off, rj + 1);
+      const uint32_t recs = lane_u32(r_plan.recs, rj), bin_len = lane_u32(r_plan.bin_len, rj);
+      const uint32_t sf = lane_u32(r_plan.step_flags, rj), hw = lane_u32(r_plan.hash_w, rj);
+      const uint32_t hb = lane_u32(r_hpre, rj) - lane_u32(r_hpre, r0);
+      const bool in = (uint32_t)lane < k;
+      const uint32_t plen = in ? (uint32_t)(of1 - of) - kHdrLen : 0;
+      const uint32_t nbk = plen > 240 ? (plen - 1) / 1024 : 0;
+      const uint32_t units = plen > 240 ? nbk + 1 : 0;
+      const uint32_t u0 = wave_incl_scan_u32(units) - units;
+      if (in) {
+        GBlk B;
+        B.it0 = st - i0;
+        B.n = st1 - st;
+        B.img = (uint32_t)(of - obase) + pad;
+        B.plen = plen;
+        B.recs = recs;
+        B.bin_len = bin_len;
+        B.step = sf & 0xFF;
+        B.hash_w = hw;
+        B.hash_base = hb;
+        B.u0 = u0;
+        B.nbk = nbk;
+        B.pad = 0;
+        B.ck_lo = B.ck_hi = 0;
+        L.blk[lane] = B;
+      }
+    }
+    __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0): this wave's DMA pieces and item loads have landed
+    if (live) {
+      kofs[tid] = (uint32_t)(m.ko - kbase);
+      if (tid + 1 == n_items) kofs[tid + 1] = (uint32_t)(m.ko + m.klen - kbase);
+    }
+    // (shuffles only with every lane active: a bpermute from an inactive lane is undefined)
+    const uint32_t hsum = lane_u32(r_hpre, r0 + k) - lane_u32(r_hpre, r0);
+    for (uint32_t h = tid; h < hsum; h += kGThreads) {
+      hlo[h] = 0xFFFFFFFFu;
+      hhi[h] = 0;
+    }
+    group_barrier();
+    // ---- item t: block, shared prefix, record length
+    uint32_t j = 0;
+    if (live) {
+      uint32_t lo = 0, hi = k;
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (L.blk[mid].it0 <= tid) lo = mid;
+        else hi = mid;
+      }
+      j = lo;
+    }
+    const uint32_t it0 = L.blk[j].it0;
+    const uint32_t jj = tid - it0;
+    const bool head = jj % ri == 0;
+    if (live && !index && !head) {
+      const uint32_t ht = it0 + (jj / ri) * ri;
+      const uint32_t hk = kofs[ht], hkl = kofs[ht + 1] - hk;
+      m.sh = lcp_lds(L.keys, hk, kofs[tid], min(hkl, m.klen));
+    }
+    const uint32_t rec = live ? (uint32_t)item_record_len(P, m, head) : 0;
+    const uint32_t incl = wave_incl_scan_u32(rec);
+    if (lane == 63) L.wsum[wave] = incl;
+    group_barrier();
+    uint32_t wbase = 0;
+    for (uint32_t w = 0; w < wave; ++w) wbase += L.wsum[w];
+    const uint32_t ex = wbase + incl - rec;
+    if (live) xs[tid] = ex;
+    group_barrier();
+    // ---- item t: its record into the image
+    if (live) {
+      const GBlk& B = L.blk[j];
+      const uint32_t roff = ex - xs[it0];
+      const uint32_t p0 = B.img + kHdrLen;
+      uint32_t pos = p0 + roff;
+      const uint32_t kst = kofs[tid];
+      if (index) {
+        L.img[pos++] = 0;
+        pos = lds_put_leb(L.img, pos, m.vo);
+        pos = lds_put_leb(L.img, pos, m.vl);
+        pos = lds_put_leb(L.img, pos, m.seq);
+        pos = lds_put_leb(L.img, pos, m.klen);
+        lds_copy(L.img, pos, L.keys, kst, m.klen);
+      } else {
+        L.img[pos++] = (uint8_t)m.vt;
+        pos = lds_put_leb(L.img, pos, m.seq);
+        const uint32_t from = head ? 0 : m.sh;
+        if (!head) pos = lds_put_leb(L.img, pos, m.sh);
+        pos = lds_put_leb(L.img, pos, m.klen - from);
+        lds_copy(L.img, pos, L.keys, kst + from, m.klen - from);
+        pos += m.klen - from;
+        if (!is_tombstone(m.vt)) {
+          pos = lds_put_leb(L.img, pos, m.vl);
+          lds_copy(L.img, pos, L.vals, (uint32_t)(m.vo - vbase), m.vl);
+        }
+      }
+      if (head) {
+        const uint32_t bp = p0 + B.recs + 1 + (jj / ri) * B.step;
+        for (uint32_t q = 0; q < B.step; ++q) L.img[bp + q] = (uint8_t)(roff >> (8 * q));
+      }
+      if (B.hash_w) {
+        const uint64_t hv = xxh3_64_any(m.klen, BaseReader8{L.keys, kst}, BaseReader64{L.keys, kst});
+        const uint32_t bk = B.hash_base + (uint32_t)(hv % B.hash_w);
+        atomicMin(&hlo[bk], jj / ri);
+        atomicMax(&hhi[bk], jj / ri);
+      }
+    }
+    group_barrier();
+    // the stage is free: the next group's DMA runs under the tails, hash and copy-out
+    const Grp Gn = next_group(G.b + k);
+    if (Gn.k) issue_dma(Gn);
+    // ---- tails, wave per block: marker, hash-index bytes, trailer (trailer.rs:78-173)
+    for (uint32_t jb = wave; jb < k; jb += kGWaves) {
+      const GBlk& B = L.blk[jb];
+      const uint32_t p0 = B.img + kHdrLen, bin_off = B.recs + 1;
+      if (lane == 0) L.img[p0 + B.recs] = kTrailerMarker;
+      const uint32_t hash_off = B.hash_w ? bin_off + B.bin_len * B.step : 0;
+      for (uint32_t q = lane; q < B.hash_w; q += kWave)
+        L.img[p0 + hash_off + q] = (uint8_t)bucket_byte(hlo[B.hash_base + q], hhi[B.hash_base + q]);
+      write_trailer_bytes(L.img, p0 + B.plen - kTrailerLen, ri, B.step, B.bin_len, bin_off, B.hash_w, hash_off, B.n);
+    }
+    group_barrier();
+    // ---- payload xxh3_128: 1 KiB units over the 16 DPP rows
+    {
+      const uint32_t row = wave * 4 + (lane >> 4), r = lane & 15, q = r & 3, s = r >> 2;
+      const uint32_t units = L.blk[k - 1].u0 + (L.blk[k - 1].plen > 240 ? L.blk[k - 1].nbk + 1 : 0);
+      const uint64_t* acc = L.secret.acc + s + 2 * q;
+      for (uint32_t u = row; u < units; u += 16) {
+        uint32_t jb = 0;
+        while (jb + 1 < k && L.blk[jb + 1].u0 <= u) ++jb;
+        const GBlk& B = L.blk[jb];
+        const uint32_t n = u - B.u0, p0 = B.img + kHdrLen;
+        uint64_t c0 = 0, c1 = 0;
+        if (n < B.nbk) {
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            const Win16 w = read_win16(L.img, p0 + n * 1024 + 256 * t + 16 * r);
+            stripe_part(w, acc[4 * t], acc[4 * t + 1], c0, c1);
+          }
+        } else {  // the tail stripes and the last stripe (secret + 121)
+          const uint32_t tail0 = B.nbk * 1024, nb_stripes = ((B.plen - 1) - tail0) / 64;
+#pragma unroll
+          for (int t = 0; t < 4; ++t) {
+            if ((uint32_t)(4 * t + s) < nb_stripes) {
+              const Win16 w = read_win16(L.img, p0 + tail0 + 256 * t + 16 * r);
+              stripe_part(w, acc[4 * t], acc[4 * t + 1], c0, c1);
+            }
+          }
+          if (r < 4) {
+            const Win16 w = read_win16(L.img, p0 + B.plen - 64 + 16 * r);
+            stripe_part(w, L.secret.last[2 * q], L.secret.last[2 * q + 1], c0, c1);
+          }
+        }
+        c0 = row_quad_sum64(c0);
+        c1 = row_quad_sum64(c1);
+        if (r < 4) {
+          contrib[8 * u + 2 * q] = c0;
+          contrib[8 * u + 2 * q + 1] = c1;
+        }
+      }
+    }
+    group_barrier();
+    // ---- wave per block: the scramble chain and the merge (or the short path)
+    for (uint32_t jb = wave; jb < k; jb += kGWaves) {
+      GBlk& B = L.blk[jb];
+      const uint32_t p0 = B.img + kHdrLen;
+      uint64_t lo, hi;
+      if (B.plen > 240) {
+        const int q = lane & 3;
+        uint64_t a0 = q == 0 ? (uint64_t)P32_3 : q == 1 ? P64_2 : q == 2 ? P64_4 : P64_5;
+        uint64_t a1 = q == 0 ? P64_1 : q == 1 ? P64_3 : q == 2 ? (uint64_t)P32_2 : (uint64_t)P32_1;
+        const uint64_t scr0 = L.secret.acc[16 + 2 * q], scr1 = L.secret.acc[16 + 2 * q + 1];
+        for (uint32_t n = 0; n < B.nbk; ++n) {
+          a0 += contrib[8 * (B.u0 + n) + 2 * q];
+          a0 ^= a0 >> 47; a0 ^= scr0; a0 *= P32_1;
+          a1 += contrib[8 * (B.u0 + n) + 2 * q + 1];
+          a1 ^= a1 >> 47; a1 ^= scr1; a1 *= P32_1;
+        }
+        a0 += contrib[8 * (B.u0 + B.nbk) + 2 * q];
+        a1 += contrib[8 * (B.u0 + B.nbk) + 2 * q + 1];
+        uint64_t tlo = mul_fold64(a0 ^ L.secret.mlo[2 * q], a1 ^ L.secret.mlo[2 * q + 1]);
+        uint64_t thi = mul_fold64(a0 ^ L.secret.mhi[2 * q], a1 ^ L.secret.mhi[2 * q + 1]);
+        tlo = quad_sum64(tlo);
+        thi = quad_sum64(thi);
+        lo = xxh3_avalanche((uint64_t)B.plen * P64_1 + tlo);
+        hi = xxh3_avalanche(~((uint64_t)B.plen * P64_2) + thi);
+      } else {
+        xxh3_128_short(B.plen, BaseReader8{L.img, p0}, BaseReader64{L.img, p0}, lo, hi);
+      }
+      if (lane == 0) {
+        B.ck_lo = lo;
+        B.ck_hi = hi;
+      }
+    }
+    group_barrier();
+    // ---- headers: wave 0, lane per block
+    if (wave == 0 && (uint32_t)lane < k) {
+      const GBlk& B = L.blk[lane];
+      lane_header(L.img, B.img, P.type, B.ck_lo, B.ck_hi, B.plen);
+      P.status[G.b + lane] = ST_OK;
+    }
+    group_barrier();
+    // ---- copy-out: the group's span [block_off[b], block_off[b + k]) in 16 B pieces
+    {
+      const uint32_t total = (uint32_t)(lane_u64(r_off, r0 + k) - obase);
+      uint8_t* gdst = reinterpret_cast<uint8_t*>(dabs & ~15ULL);
+      const uint32_t chunks = (pad + total + 15) >> 4;
+      for (uint32_t c = tid; c < chunks; c += kGThreads) {
+        const uint32_t lo = c * 16, hi = lo + 16;
+        if (lo >= pad && hi <= pad + total) {
+          __builtin_nontemporal_store(reinterpret_cast<const u32x4*>(L.img)[c], reinterpret_cast<u32x4*>(gdst) + c);
+        } else {
+          for (uint32_t x = max(lo, pad); x < min(hi, pad + total); ++x)
+            ((__attribute__((address_space(1))) uint8_t*)gdst)[x] = L.img[x];
+        }
+      }
+    }
+    G = Gn;
   }
-  wave_lds_sync();
-  finish_block_lds(P, b, pl, n, ri, img, hlo, hhi, pad, total, reinterpret_cast<uint8_t*>(dabs & ~15ULL));
 }
 
 // Listed medium / big blocks: one wave per workgroup, grid-stride over the list.
@@ -658,15 +1077,13 @@ __global__ __launch_bounds__(64) void encode_large_kernel(EncodeParams P) {
     uint32_t carry = 0;
     for (uint32_t c = 0; c < n; c += kWave) {
       const uint32_t j = c + lane;
-      const uint64_t i = (uint64_t)s + j;
       const bool head = j % ri == 0;
       ItemMeta m;
       RecordCopy rc;
       uint32_t rec = 0;
       if (j < n) {
         bool bad = false;
-        m = load_item(P, i, bad);
-        if (!is_index(P)) m.sh = P.shared[i];
+        m = load_item_lcp(P, s, j, ri, bad);
         rec = (uint32_t)item_record_len(P, m, head);
       }
       const uint32_t incl = wave_incl_scan_u32(rec);
@@ -726,8 +1143,9 @@ struct EncodeOffOut {
 static size_t al256(size_t x) { return (x + 255) / 256 * 256; }
 
 size_t encode_workspace_size(uint64_t n_items, uint32_t n_blocks) {
-  return al256(n_items * 2) + al256((size_t)n_blocks * 8) + al256((size_t)n_blocks * sizeof(BlockPlan)) +
-         al256((size_t)n_blocks * 4) + 256 + al256(scan_tiles(n_blocks) * 8);
+  (void)n_items;
+  return 2 * al256(((size_t)n_blocks + 1) * 8) + al256((size_t)n_blocks * 8) +
+         al256((size_t)n_blocks * sizeof(BlockPlan)) + al256((size_t)n_blocks * 4) + 256 + al256(scan_tiles(n_blocks) * 8);
 }
 
 uint64_t encode_bound(uint64_t n_items, uint32_t n_blocks, uint64_t key_bytes, uint64_t val_bytes,
@@ -755,21 +1173,21 @@ hipError_t launch_encode(const lsm_items& items, const uint32_t* starts, uint32_
   P.block_off = block_off;
   P.status = status;
   uint8_t* w = (uint8_t*)ws;
-  P.shared = (uint16_t*)w; w += al256(items.n_items * 2);
+  P.kspan = (uint64_t*)w; w += al256(((size_t)n_blocks + 1) * 8);
+  P.vspan = (uint64_t*)w; w += al256(((size_t)n_blocks + 1) * 8);
   P.sizes = (uint64_t*)w; w += al256((size_t)n_blocks * 8);
   P.plans = (BlockPlan*)w; w += al256((size_t)n_blocks * sizeof(BlockPlan));
   P.lists = (uint32_t*)w; w += al256((size_t)n_blocks * 4);
   P.list_count = (uint32_t*)w; w += 256;
   uint64_t* tiles = (uint64_t*)w;
   hipError_t e;
-  hipLaunchKernelGGL(encode_sizes_kernel, dim3((n_blocks + 3) / 4), dim3(256), 0, st, P);
+  hipLaunchKernelGGL(encode_plan_kernel, dim3((n_blocks + kPlanBlocks - 1) / kPlanBlocks), dim3(256), 0, st, P);
   if ((e = launch_excl_scan(P.sizes, n_blocks, tiles,
                             EncodeOffOut{block_off, P.sizes, P.lists, P.list_count, n_blocks}, st)) != hipSuccess)
     return e;
   static uint64_t attr_done = 0;
   if ((e = set_lds_attr((const void*)encode_write_list_kernel, kImgBig, &attr_done)) != hipSuccess) return e;
-  hipLaunchKernelGGL(encode_write_kernel, dim3((n_blocks + kSmallWaves - 1) / kSmallWaves), dim3(kSmallWaves * kWave),
-                     kSmallWaves * kImgSmall, st, P);
+  hipLaunchKernelGGL(encode_group_kernel, dim3((n_blocks + kGRun - 1) / kGRun), dim3(kGThreads), 0, st, P);
   hipLaunchKernelGGL(encode_write_list_kernel, dim3(2048), dim3(kWave), kImgMedium, st, P, kPlanMedium);
   hipLaunchKernelGGL(encode_write_list_kernel, dim3(512), dim3(kWave), kImgBig, st, P, kPlanBig);
   hipLaunchKernelGGL(encode_large_kernel, dim3(1024), dim3(64), 0, st, P);
