@@ -115,6 +115,7 @@ struct EncodeParams {
   BlockPlan* plans;     // [n_blocks]
   uint32_t* lists;      // [n_blocks]: the listed blocks in block order (from the size scan)
   uint32_t* list_count; // [1]
+  unsigned long long* phase;  // diagnostic builds: per-phase cycle totals [16]
 };
 
 __device__ __forceinline__ bool is_index(const EncodeParams& P) { return P.type == 1; }
@@ -519,8 +520,8 @@ constexpr uint32_t kGItems = 256;              // items per group (one thread ea
 constexpr uint32_t kGSlack = 48;               // readable bytes past each staged span
 constexpr uint32_t kGKeys = 4096, kGVals = 14400, kGImg = 15872;
 constexpr uint32_t kGUnits = kGImg / 1024 + kGBlocks + 1;  // hash units per group
-constexpr uint32_t kGUnion = 4096;             // kofs + xs + hash votes | hash contributions
-constexpr uint32_t kGHash = (kGUnion - 4 * (kGItems + 4) - 4 * kGItems) / 8;  // vote pairs
+constexpr uint32_t kGUnion = 4096;             // kofs + hash votes | hash contributions
+constexpr uint32_t kGHash = (kGUnion - 4 * (kGItems + 4)) / 8;  // vote pairs
 static_assert(kGUnits * 64 <= kGUnion, "hash contributions");
 
 
@@ -637,7 +638,7 @@ struct GBlk {
   uint32_t recs, bin_len;  // record bytes, restart heads
   uint32_t step, hash_w;   // binary-index step, hash-index buckets
   uint32_t hash_base, u0;  // first vote pair, first hash unit
-  uint32_t nbk, pad;       // full KiB units of the payload
+  uint32_t nbk, rbase;     // full KiB units of the payload, group record bytes before
   uint64_t ck_lo, ck_hi;   // payload xxh3_128
 };
 static_assert(sizeof(GBlk) == 64, "GBlk");
@@ -703,34 +704,24 @@ __device__ __forceinline__ uint32_t lcp_lds(const uint8_t* keys, uint32_t a, uin
   return n;
 }
 
-// Header::encode_into (header.rs:80-112) of one block by one lane.
-__device__ __forceinline__ void lane_header(uint8_t* dst, uint32_t hp, uint32_t type, uint64_t ck_lo, uint64_t ck_hi,
-                                            uint32_t plen) {
-  const uint64_t w0 = 0x034D534CULL | ((uint64_t)type << 32) | (ck_lo << 40);
-  const uint64_t w1 = (ck_lo >> 24) | (ck_hi << 40);
-  const uint64_t w2 = (ck_hi >> 24) | ((uint64_t)plen << 40);
-  const uint64_t w3 = ((uint64_t)plen >> 24) | ((uint64_t)plen << 8);
-  auto r64 = [&](uint32_t o) -> uint64_t {
-    const uint32_t q = o >> 3, sft = (o & 7) * 8;
-    const uint64_t a = q == 0 ? w0 : q == 1 ? w1 : q == 2 ? w2 : w3;
-    const uint64_t b = q == 0 ? w1 : q == 1 ? w2 : q == 2 ? w3 : 0;
-    return sft ? (a >> sft) | (b << (64 - sft)) : a;
-  };
-  auto r8 = [&](uint32_t o) -> uint32_t { return (uint32_t)(r64(o) & 0xFF); };
-  uint64_t hlo, hhi;
-  xxh3_128_short(29, r8, r64, hlo, hhi);
-  const uint64_t w[4] = {w0, w1, w2, w3};
-#pragma unroll
-  for (int k = 0; k < 29; ++k) dst[hp + k] = (uint8_t)(w[k >> 3] >> (8 * (k & 7)));
-#pragma unroll
-  for (int k = 0; k < 4; ++k) dst[hp + 29 + k] = (uint8_t)((uint32_t)hlo >> (8 * k));
-}
-
 __device__ __forceinline__ void group_barrier() {
   __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
   __builtin_amdgcn_s_barrier();
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
+
+#ifdef LSM_DIAG
+// Diagnostic per-phase cycle totals of wave 0 of every group workgroup
+// (lsm_block_params.reserved bit 0x80; read by lsm_diag_encode_phases).
+#define ENC_PHASE(i)                                 \
+  if (P.diag & 0x80) {                              \
+    const uint64_t t_ = __builtin_amdgcn_s_memtime(); \
+    ph_acc[i] += (uint32_t)(t_ - t_last);            \
+    t_last = t_;                                     \
+  }
+#else
+#define ENC_PHASE(i)
+#endif
 
 __global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(4))) void encode_group_kernel(EncodeParams P) {
   __shared__ GroupLds L;
@@ -756,18 +747,25 @@ __global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(4))) 
   const uint32_t r_hpre = wave_incl_scan_u32(r_hash) - r_hash;  // exclusive prefix over the run
   auto lane_u32 = [&](uint32_t v, uint32_t l) { return (uint32_t)__shfl((int)v, (int)min(l, 63u)); };
   auto lane_u64 = [&](uint64_t v, uint32_t l) { return wave_shfl_u64(v, (int)min(l, 63u)); };
+  // the same for a wave-uniform lane index: v_readlane into a scalar register
+  auto rl32 = [&](uint32_t v, uint32_t l) { return (uint32_t)__builtin_amdgcn_readlane((int)v, (int)min(l, 63u)); };
+  auto rl64 = [&](uint64_t v, uint32_t l) {
+    const int q = (int)min(l, 63u);
+    return (uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)v, q) |
+           ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)(v >> 32), q) << 32);
+  };
   struct Grp {
     uint32_t b, k;
   };
   // the longest group from block b (k = 0: block b is listed / rejected / over capacity)
   auto form = [&](uint32_t b) -> Grp {
     const uint32_t r0 = b - b_begin, rj = r0 + lane;
-    const uint32_t s0 = lane_u32(r_start, r0), s1 = lane_u32(r_start, rj + 1);
-    const uint64_t o0 = lane_u64(r_off, r0), o1 = lane_u64(r_off, rj + 1);
-    const uint64_t k0 = lane_u64(r_ks, r0), k1 = lane_u64(r_ks, rj + 1);
-    const uint64_t v0 = lane_u64(r_vs, r0), v1 = lane_u64(r_vs, rj + 1);
+    const uint32_t s0 = rl32(r_start, r0), s1 = lane_u32(r_start, rj + 1);
+    const uint64_t o0 = rl64(r_off, r0), o1 = lane_u64(r_off, rj + 1);
+    const uint64_t k0 = rl64(r_ks, r0), k1 = lane_u64(r_ks, rj + 1);
+    const uint64_t v0 = rl64(r_vs, r0), v1 = lane_u64(r_vs, rj + 1);
     const uint32_t flags = lane_u32(r_plan.step_flags, rj) >> 8;
-    const uint32_t hsum = lane_u32(r_hpre, rj + 1) - lane_u32(r_hpre, r0);
+    const uint32_t hsum = lane_u32(r_hpre, rj + 1) - rl32(r_hpre, r0);
     const bool ok = b + lane < b_end && lane < (int)kGBlocks && flags == 0 && o1 <= P.out_cap &&
                     group_fits(s1 - s0, k1 - (k0 & ~15ULL), v1 - (v0 & ~15ULL), o1 - (o0 & ~15ULL), hsum);
     return Grp{b, (uint32_t)__builtin_ctzll(~__ballot(ok))};
@@ -777,15 +775,15 @@ __global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(4))) 
       if (b >= b_end) return Grp{b, 0};
       const Grp g = form(b);
       if (g.k) return g;
-      const uint32_t fl = lane_u32(r_plan.step_flags, b - b_begin) >> 8;
+      const uint32_t fl = rl32(r_plan.step_flags, b - b_begin) >> 8;
       if (fl == 0 && lane == 0) P.status[b] = ST_OVERFLOW;  // group class, but past out_cap
       ++b;
     }
   };
   auto issue_dma = [&](const Grp& g) {
     const uint32_t r0 = g.b - b_begin;
-    const uint64_t ka = lane_u64(r_ks, r0) & ~15ULL, kb = lane_u64(r_ks, r0 + g.k);
-    const uint64_t va = lane_u64(r_vs, r0) & ~15ULL, vb = lane_u64(r_vs, r0 + g.k);
+    const uint64_t ka = rl64(r_ks, r0) & ~15ULL, kb = rl64(r_ks, r0 + g.k);
+    const uint64_t va = rl64(r_vs, r0) & ~15ULL, vb = rl64(r_vs, r0 + g.k);
     const uint32_t kc = (uint32_t)((kb - ka + 15) >> 4), vc = index ? 0 : (uint32_t)((vb - va + 15) >> 4);
     const uint8_t* ks = P.it.keys + ka + 16 * lane;
     for (uint32_t i = wave; i * kWave < kc; i += kGWaves)
@@ -797,26 +795,49 @@ __global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(4))) 
         __builtin_amdgcn_global_load_lds((gbl_void_t*)(vs + 1024 * i), (lds_void_t*)(L.vals + 1024 * i), 16, 0, 0);
   };
   uint32_t* kofs = L.uni;                          // [kGItems + 1] key offsets in the stage
-  uint32_t* xs = L.uni + kGItems + 4;              // [kGItems] exclusive record-length scan
-  uint32_t* hlo = L.uni + 2 * kGItems + 4;         // [kGHash] vote min
+  uint32_t* hlo = L.uni + kGItems + 4;             // [kGHash] vote min
   uint32_t* hhi = hlo + kGHash;                    // [kGHash] vote max
   uint64_t* contrib = reinterpret_cast<uint64_t*>(L.uni);  // [kGUnits][4][2] (after the records)
 
+  // item t's fields of group g (loads only; consumed by the next iteration)
+  // (the plan pass has vetted every group-class item: `bad` is not needed here)
+  auto load_items = [&](const Grp& g, ItemMeta& m) {
+    const uint32_t r0 = g.b - b_begin;
+    const uint32_t i0 = rl32(r_start, r0), n = rl32(r_start, r0 + g.k) - i0;
+    bool bad = false;
+    if (tid < n) m = load_item(P, (uint64_t)i0 + tid, bad);
+  };
+
+  // Software pipeline: group G's stage DMA and item fields are issued one
+  // group ahead and waited for (vmcnt(0)) just before the previous group's
+  // copy-out, so no group waits on HBM latency after its stores.
+#ifdef LSM_DIAG
+  uint64_t t_last = __builtin_amdgcn_s_memtime();
+  uint32_t ph_acc[12] = {};
+  uint32_t ph_n = 0;
+#endif
   Grp G = next_group(b_begin);
-  if (G.k) issue_dma(G);
+  ItemMeta m{};
+  if (G.k) {
+    issue_dma(G);
+    load_items(G, m);
+  }
+  __builtin_amdgcn_s_waitcnt(0x0070);
+  ENC_PHASE(11);
   while (G.k) {
+    ENC_PHASE(0);
     const uint32_t r0 = G.b - b_begin, k = G.k;
-    const uint32_t i0 = lane_u32(r_start, r0), n_items = lane_u32(r_start, r0 + k) - i0;
-    const uint64_t kbase = lane_u64(r_ks, r0) & ~15ULL, vbase = lane_u64(r_vs, r0) & ~15ULL;
-    const uint64_t obase = lane_u64(r_off, r0);
+    const uint32_t i0 = rl32(r_start, r0), n_items = rl32(r_start, r0 + k) - i0;
+    const uint64_t kbase = rl64(r_ks, r0) & ~15ULL, vbase = rl64(r_vs, r0) & ~15ULL;
+    const uint64_t obase = rl64(r_off, r0);
     const uint64_t dabs = (uint64_t)(uintptr_t)P.out + obase;
     const uint32_t pad = (uint32_t)(dabs & 15);
-    // ---- item t: fields (in flight with the DMA)
     const bool live = tid < n_items;
-    const uint64_t gi = (uint64_t)i0 + tid;
-    ItemMeta m{};
-    bool bad = false;
-    if (live) m = load_item(P, gi, bad);
+    // the next group's item fields: in flight under this whole group
+    const Grp Gn = next_group(G.b + k);
+    ItemMeta mn{};
+    if (Gn.k) load_items(Gn, mn);
+    ENC_PHASE(9);
     // ---- wave 0: the group's block table (lane j = group block j; shuffles with every lane active)
     if (wave == 0) {
       const uint32_t rj = r0 + lane;
@@ -824,12 +845,14 @@ __global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(4))) 
       const uint64_t of = lane_u64(r_off, rj), of1 = lane_u64(r_off, rj + 1);
       const uint32_t recs = lane_u32(r_plan.recs, rj), bin_len = lane_u32(r_plan.bin_len, rj);
       const uint32_t sf = lane_u32(r_plan.step_flags, rj), hw = lane_u32(r_plan.hash_w, rj);
-      const uint32_t hb = lane_u32(r_hpre, rj) - lane_u32(r_hpre, r0);
+      const uint32_t hb = lane_u32(r_hpre, rj) - rl32(r_hpre, r0);
       const bool in = (uint32_t)lane < k;
       const uint32_t plen = in ? (uint32_t)(of1 - of) - kHdrLen : 0;
       const uint32_t nbk = plen > 240 ? (plen - 1) / 1024 : 0;
       const uint32_t units = plen > 240 ? nbk + 1 : 0;
       const uint32_t u0 = wave_incl_scan_u32(units) - units;
+      const uint32_t rin = in ? recs : 0;
+      const uint32_t rbase = wave_incl_scan_u32(rin) - rin;
       if (in) {
         GBlk B;
         B.it0 = st - i0;
@@ -843,23 +866,23 @@ __global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(4))) 
         B.hash_base = hb;
         B.u0 = u0;
         B.nbk = nbk;
-        B.pad = 0;
+        B.rbase = rbase;
         B.ck_lo = B.ck_hi = 0;
         L.blk[lane] = B;
       }
     }
-    __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0): this wave's DMA pieces and item loads have landed
     if (live) {
       kofs[tid] = (uint32_t)(m.ko - kbase);
       if (tid + 1 == n_items) kofs[tid + 1] = (uint32_t)(m.ko + m.klen - kbase);
     }
     // (shuffles only with every lane active: a bpermute from an inactive lane is undefined)
-    const uint32_t hsum = lane_u32(r_hpre, r0 + k) - lane_u32(r_hpre, r0);
+    const uint32_t hsum = rl32(r_hpre, r0 + k) - rl32(r_hpre, r0);
     for (uint32_t h = tid; h < hsum; h += kGThreads) {
       hlo[h] = 0xFFFFFFFFu;
       hhi[h] = 0;
     }
     group_barrier();
+    ENC_PHASE(1);
     // ---- item t: block, shared prefix, record length
     uint32_t j = 0;
     if (live) {
@@ -874,7 +897,7 @@ __global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(4))) 
     const uint32_t it0 = L.blk[j].it0;
     const uint32_t jj = tid - it0;
     const bool head = jj % ri == 0;
-    if (live && !index && !head) {
+    if (live && !index && !head && !(kDiagBuild && (P.diag & 8))) {
       const uint32_t ht = it0 + (jj / ri) * ri;
       const uint32_t hk = kofs[ht], hkl = kofs[ht + 1] - hk;
       m.sh = lcp_lds(L.keys, hk, kofs[tid], min(hkl, m.klen));
@@ -883,15 +906,14 @@ __global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(4))) 
     const uint32_t incl = wave_incl_scan_u32(rec);
     if (lane == 63) L.wsum[wave] = incl;
     group_barrier();
+    ENC_PHASE(2);
     uint32_t wbase = 0;
     for (uint32_t w = 0; w < wave; ++w) wbase += L.wsum[w];
     const uint32_t ex = wbase + incl - rec;
-    if (live) xs[tid] = ex;
-    group_barrier();
     // ---- item t: its record into the image
-    if (live) {
+    if (live && !(kDiagBuild && (P.diag & 9))) {
       const GBlk& B = L.blk[j];
-      const uint32_t roff = ex - xs[it0];
+      const uint32_t roff = ex - B.rbase;
       const uint32_t p0 = B.img + kHdrLen;
       uint32_t pos = p0 + roff;
       const uint32_t kst = kofs[tid];
@@ -927,11 +949,12 @@ __global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(4))) 
       }
     }
     group_barrier();
-    // the stage is free: the next group's DMA runs under the tails, hash and copy-out
-    const Grp Gn = next_group(G.b + k);
-    if (Gn.k) issue_dma(Gn);
+    ENC_PHASE(3);
+    // the stage is free: the next group's DMA runs under the tails and the hash
+    if (Gn.k && !(kDiagBuild && (P.diag & 16))) issue_dma(Gn);
+    ENC_PHASE(10);
     // ---- tails, wave per block: marker, hash-index bytes, trailer (trailer.rs:78-173)
-    for (uint32_t jb = wave; jb < k; jb += kGWaves) {
+    for (uint32_t jb = wave; jb < (kDiagBuild && (P.diag & 8) ? 0 : k); jb += kGWaves) {
       const GBlk& B = L.blk[jb];
       const uint32_t p0 = B.img + kHdrLen, bin_off = B.recs + 1;
       if (lane == 0) L.img[p0 + B.recs] = kTrailerMarker;
@@ -941,10 +964,12 @@ __global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(4))) 
       write_trailer_bytes(L.img, p0 + B.plen - kTrailerLen, ri, B.step, B.bin_len, bin_off, B.hash_w, hash_off, B.n);
     }
     group_barrier();
+    ENC_PHASE(4);
     // ---- payload xxh3_128: 1 KiB units over the 16 DPP rows
     {
       const uint32_t row = wave * 4 + (lane >> 4), r = lane & 15, q = r & 3, s = r >> 2;
-      const uint32_t units = L.blk[k - 1].u0 + (L.blk[k - 1].plen > 240 ? L.blk[k - 1].nbk + 1 : 0);
+      const uint32_t units = (kDiagBuild && (P.diag & 10))
+                                 ? 0 : L.blk[k - 1].u0 + (L.blk[k - 1].plen > 240 ? L.blk[k - 1].nbk + 1 : 0);
       const uint64_t* acc = L.secret.acc + s + 2 * q;
       for (uint32_t u = row; u < units; u += 16) {
         uint32_t jb = 0;
@@ -981,8 +1006,9 @@ __global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(4))) 
       }
     }
     group_barrier();
+    ENC_PHASE(5);
     // ---- wave per block: the scramble chain and the merge (or the short path)
-    for (uint32_t jb = wave; jb < k; jb += kGWaves) {
+    for (uint32_t jb = wave; jb < (kDiagBuild && (P.diag & 10) ? 0 : k); jb += kGWaves) {
       GBlk& B = L.blk[jb];
       const uint32_t p0 = B.img + kHdrLen;
       uint64_t lo, hi;
@@ -1008,24 +1034,18 @@ __global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(4))) 
       } else {
         xxh3_128_short(B.plen, BaseReader8{L.img, p0}, BaseReader64{L.img, p0}, lo, hi);
       }
-      if (lane == 0) {
-        B.ck_lo = lo;
-        B.ck_hi = hi;
-      }
+      write_header_bytes(L.img, B.img, P.type, lo, hi, B.plen);
+      if (lane == 0) P.status[G.b + jb] = ST_OK;
     }
     group_barrier();
-    // ---- headers: wave 0, lane per block
-    if (wave == 0 && (uint32_t)lane < k) {
-      const GBlk& B = L.blk[lane];
-      lane_header(L.img, B.img, P.type, B.ck_lo, B.ck_hi, B.plen);
-      P.status[G.b + lane] = ST_OK;
-    }
-    group_barrier();
+    ENC_PHASE(6);
+    __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0): the next group's DMA pieces and item fields
+    ENC_PHASE(7);
     // ---- copy-out: the group's span [block_off[b], block_off[b + k]) in 16 B pieces
     {
-      const uint32_t total = (uint32_t)(lane_u64(r_off, r0 + k) - obase);
+      const uint32_t total = (uint32_t)(rl64(r_off, r0 + k) - obase);
       uint8_t* gdst = reinterpret_cast<uint8_t*>(dabs & ~15ULL);
-      const uint32_t chunks = (pad + total + 15) >> 4;
+      const uint32_t chunks = (kDiagBuild && (P.diag & 4)) ? 0 : (pad + total + 15) >> 4;
       for (uint32_t c = tid; c < chunks; c += kGThreads) {
         const uint32_t lo = c * 16, hi = lo + 16;
         if (lo >= pad && hi <= pad + total) {
@@ -1036,8 +1056,19 @@ __global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(4))) 
         }
       }
     }
+    ENC_PHASE(8);
+#ifdef LSM_DIAG
+    ++ph_n;
+#endif
     G = Gn;
+    m = mn;
   }
+#ifdef LSM_DIAG
+  if ((P.diag & 0x80) && tid == 0) {
+    for (int i = 0; i < 12; ++i) atomicAdd(&P.phase[i], (unsigned long long)ph_acc[i]);
+    atomicAdd(&P.phase[15], (unsigned long long)ph_n);
+  }
+#endif
 }
 
 // Listed medium / big blocks: one wave per workgroup, grid-stride over the list.
@@ -1140,6 +1171,14 @@ struct EncodeOffOut {
   }
 };
 
+#ifdef LSM_DIAG
+static unsigned long long* diag_phase_buffer() {
+  static unsigned long long* d = nullptr;
+  if (!d && hipMalloc(&d, 16 * sizeof(unsigned long long)) == hipSuccess) hipMemset(d, 0, 16 * sizeof(unsigned long long));
+  return d;
+}
+#endif
+
 static size_t al256(size_t x) { return (x + 255) / 256 * 256; }
 
 size_t encode_workspace_size(uint64_t n_items, uint32_t n_blocks) {
@@ -1168,6 +1207,11 @@ hipError_t launch_encode(const lsm_items& items, const uint32_t* starts, uint32_
   P.ratio = params.block_type == 1 ? 0.0f : params.hash_ratio;
   P.type = params.block_type;
   P.diag = params.reserved;
+#ifdef LSM_DIAG
+  P.phase = diag_phase_buffer();
+#else
+  P.phase = nullptr;
+#endif
   P.out = out;
   P.out_cap = out_cap;
   P.block_off = block_off;
@@ -1195,3 +1239,13 @@ hipError_t launch_encode(const lsm_items& items, const uint32_t* starts, uint32_
 }
 
 }  // namespace lsmgpu
+
+#ifdef LSM_DIAG
+// Diagnostic builds only: copy out and clear the per-phase cycle totals.
+extern "C" int lsm_diag_encode_phases(uint64_t* out16) {
+  unsigned long long* d = lsmgpu::diag_phase_buffer();
+  if (!d || hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpy(out16, d, 16 * sizeof(uint64_t), hipMemcpyDeviceToHost) != hipSuccess) return -1;
+  return hipMemset(d, 0, 16 * sizeof(uint64_t)) == hipSuccess ? 0 : -1;
+}
+#endif

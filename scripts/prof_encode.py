@@ -19,6 +19,7 @@ def main():
     ap.add_argument("--blocks", type=int, default=1 << 20)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--workload", default="counter", choices=["counter", "prefix16k"])
+    ap.add_argument("--phases", action="store_true", help="per-phase cycles of the group kernel (diagnostic build)")
     ap.add_argument("--ablate", action="store_true", help="diagnostic ablations (lsm_block_params.reserved bits)")
     args = ap.parse_args()
     torch.cuda.set_device(0)
@@ -39,10 +40,31 @@ def main():
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / args.reps
     assert int((enc["status"][:nb] != 0).sum()) == 0
+    if args.phases:
+        import ctypes as C
+        L = lsmgpu.lib()
+        orig = lsmgpu.LsmBlockParams
+        lsmgpu.LsmBlockParams = lambda ri, bt, c, r, hr: orig(ri, bt, c, 0x80, hr)
+        buf = (C.c_uint64 * 16)()
+        rc0 = L.lsm_diag_encode_phases(buf)
+        enc_ctx.encode(items, starts, nb, out=enc)
+        torch.cuda.synchronize()
+        rc1 = L.lsm_diag_encode_phases(buf)
+        print("phase readout rc", rc0, rc1, "status nonzero", int((enc["status"][:nb] != 0).sum()), list(buf))
+        lsmgpu.LsmBlockParams = orig
+        n = max(1, buf[15])
+        names = {11: "kernel start", 0: "loop top", 9: "next items issue", 1: "setup", 2: "scan", 3: "records",
+                 10: "next DMA issue", 4: "tails", 5: "hash", 6: "scramble+hdr", 7: "wait", 8: "copy-out"}
+        tot = sum(buf[i] for i in names)
+        print(f"group iterations {n}; s_memtime ticks per iteration (wave 0):")
+        for i, nm in names.items():
+            print(f"  {nm:16s} {buf[i] / n:9.0f}  {100 * buf[i] / max(1, tot):5.1f}%")
     if args.ablate:
         import ctypes as C
         L = lsmgpu.lib()
-        for bits, name in ((1, "no record stores"), (2, "no hash/header"), (4, "no copy-out"), (7, "none of them")):
+        for bits, name in ((1, "no record stores"), (2, "no hash/header"), (4, "no copy-out"), (7, "none of them"),
+                           (8, "no group compute"), (12, "no compute/copy-out"), (16, "no next-group DMA"),
+                           (28, "barriers + item loads")):
             orig = lsmgpu.LsmBlockParams
             class P2(C.Structure):  # noqa: E306
                 _fields_ = orig._fields_
