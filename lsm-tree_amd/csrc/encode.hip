@@ -115,6 +115,7 @@ struct EncodeParams {
   BlockPlan* plans;     // [n_blocks]
   uint32_t* lists;      // [n_blocks]: the listed blocks in block order (from the size scan)
   uint32_t* list_count; // [1]
+  uint32_t* erec;       // [n_items] E1 -> E2, see kErec*
   unsigned long long* phase;  // diagnostic builds: per-phase cycle totals [16]
 };
 
@@ -251,6 +252,7 @@ struct SpanCopy {
 struct ItemMeta {
   uint64_t ko, vo, seq;
   uint32_t klen, vl, vt, sh;
+  uint32_t e;  // E2 only: the plan's erec word
 };
 
 __device__ __forceinline__ ItemMeta load_item(const EncodeParams& P, uint64_t i, bool& bad) {
@@ -261,6 +263,7 @@ __device__ __forceinline__ ItemMeta load_item(const EncodeParams& P, uint64_t i,
   m.klen = (uint32_t)min(kl, (uint64_t)0xFFFF);
   m.seq = P.it.seqno[i];
   m.sh = 0;
+  m.e = 0;
   if (is_index(P)) {
     m.vo = P.it.handle_off[i];
     m.vl = P.it.handle_size[i];
@@ -512,6 +515,12 @@ __device__ __forceinline__ void write_block_lds(const EncodeParams& P, uint32_t 
   finish_block_lds(P, b, pl, n, ri, img, hlo, hhi, pad, total, reinterpret_cast<uint8_t*>(dabs & ~15ULL));
 }
 
+// Per-item word from E1 to E2 (read for group-class blocks, whose payload is
+// < 32 KiB and whose items are < 2^16): bits 0-14 the record's offset in the
+// block payload, bit 15 restart head, bits 16-31 the restart index (heads)
+// or the shared-prefix length (keys are < 2^16 bytes).
+constexpr uint32_t kErecHead = 0x8000u;
+
 // Group write kernel (E2) budget, see encode_group_kernel.
 constexpr uint32_t kGWaves = 4, kGThreads = kGWaves * kWave;
 constexpr uint32_t kGRun = 32;                 // blocks per workgroup
@@ -520,8 +529,8 @@ constexpr uint32_t kGItems = 256;              // items per group (one thread ea
 constexpr uint32_t kGSlack = 48;               // readable bytes past each staged span
 constexpr uint32_t kGKeys = 4096, kGVals = 14400, kGImg = 15872;
 constexpr uint32_t kGUnits = kGImg / 1024 + kGBlocks + 1;  // hash units per group
-constexpr uint32_t kGUnion = 4096;             // kofs + hash votes | hash contributions
-constexpr uint32_t kGHash = (kGUnion - 4 * (kGItems + 4)) / 8;  // vote pairs
+constexpr uint32_t kGUnion = 4096;             // hash votes | hash contributions
+constexpr uint32_t kGHash = kGUnion / 8;       // vote pairs
 static_assert(kGUnits * 64 <= kGUnion, "hash contributions");
 
 
@@ -535,24 +544,24 @@ __device__ __host__ __forceinline__ bool group_fits(uint64_t n, uint64_t kspan, 
 // and walks their items (contiguous) with one thread per item, so every load
 // is coalesced and all of a workgroup's items are in flight together.  Per
 // item: key / value lengths, the shared prefix with its restart head
-// (encoder.rs:140-143, util.rs:125-130, head key read from L1/L2) and the
-// record length; LDS atomics sum them per block (and from the last restart
-// head on, for the binary-index step).  Per block: size, binary-index step,
+// (encoder.rs:140-143, util.rs:125-130, head key read from L1/L2), the record
+// length and (workgroup scan, in item order) the record's offset in its
+// block, kept for E2 in erec.  Per block: size, binary-index step,
 // hash-index size, size class, and the key / value span starts E2 stages.
 constexpr uint32_t kPlanBlocks = 16;
 
 __global__ __launch_bounds__(256) void encode_plan_kernel(EncodeParams P) {
   __shared__ uint32_t bst[kPlanBlocks + 1];
-  __shared__ unsigned long long recs[kPlanBlocks], tail[kPlanBlocks];
+  __shared__ unsigned long long bfirst[kPlanBlocks], bend[kPlanBlocks], lhead[kPlanBlocks];
+  __shared__ unsigned long long psum[4];
   __shared__ uint32_t badf[kPlanBlocks];
   __shared__ uint32_t mono;
-  const uint32_t tid = threadIdx.x;
+  const uint32_t tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
   const uint32_t b0 = blockIdx.x * kPlanBlocks;
   const uint32_t nb = min(kPlanBlocks, P.n_blocks - b0);
   if (tid <= nb) bst[tid] = P.starts[b0 + tid];
   if (tid < nb) {
-    recs[tid] = 0;
-    tail[tid] = 0;
+    bfirst[tid] = bend[tid] = lhead[tid] = 0;
     badf[tid] = 0;
   }
   if (tid == 0) mono = 1;
@@ -562,34 +571,67 @@ __global__ __launch_bounds__(256) void encode_plan_kernel(EncodeParams P) {
   const uint32_t ri = is_index(P) ? 1 : P.ri;
   // a non-monotone item_start run is a caller error: its blocks are rejected below
   const uint64_t i_begin = bst[0], i_end = mono ? bst[nb] : bst[0];
-  for (uint64_t i = i_begin + tid; i < i_end; i += 256) {
-    uint32_t lo = 0, hi = nb;  // block j: bst[j] <= i < bst[j + 1]
-    while (hi - lo > 1) {
-      const uint32_t mid = (lo + hi) >> 1;
-      if (bst[mid] <= i) lo = mid;
-      else hi = mid;
+  uint64_t carry = 0;
+  for (uint64_t base = i_begin; base < i_end; base += 256) {
+    const uint64_t i = base + tid;
+    const bool live = i < i_end;
+    uint32_t j = 0, n = 0, jj = 0, ridx = 0;
+    uint64_t rec = 0;
+    ItemMeta m{};
+    if (live) {
+      uint32_t lo = 0, hi = nb;  // block j: bst[j] <= i < bst[j + 1]
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (bst[mid] <= i) lo = mid;
+        else hi = mid;
+      }
+      j = lo;
+      const uint32_t s = bst[j];
+      n = bst[j + 1] - s;
+      jj = (uint32_t)(i - s);
+      ridx = jj / ri;
+      bool bad = false;
+      m = load_item_lcp(P, s, jj, ri, bad);
+      rec = item_record_len(P, m, jj == ridx * ri);
+      if (bad) atomicOr(&badf[j], 1u);
     }
-    const uint32_t j = lo, s = bst[j], e = bst[j + 1];
-    const uint32_t jj = (uint32_t)(i - s);
-    bool bad = false;
-    const ItemMeta m = load_item_lcp(P, s, jj, ri, bad);
-    const uint64_t rec = item_record_len(P, m, jj % ri == 0);
-    atomicAdd(&recs[j], (unsigned long long)rec);
-    if (jj >= ((e - s - 1) / ri) * ri) atomicAdd(&tail[j], (unsigned long long)rec);
-    if (bad) atomicOr(&badf[j], 1u);
+    const uint64_t incl = wave_incl_scan_u64(rec);
+    if (lane == kWave - 1) psum[wave] = incl;
+    __syncthreads();
+    uint64_t wbase = 0, ptot = 0;
+#pragma unroll
+    for (uint32_t w = 0; w < 4; ++w) {
+      const uint64_t v = psum[w];
+      wbase += w < wave ? v : 0;
+      ptot += v;
+    }
+    const uint64_t ex = carry + wbase + incl - rec;
+    const bool head = jj == ridx * ri;
+    if (live) {
+      if (jj == 0) bfirst[j] = ex;
+      if (jj + 1 == n) bend[j] = ex + rec;
+      if (head && ridx == (n - 1) / ri) lhead[j] = ex;
+    }
+    __syncthreads();  // (also orders this pass's psum reads before the next pass's writes)
+    if (live) {
+      const uint64_t roff = ex - bfirst[j];
+      const uint32_t x = head ? ridx : m.sh;
+      P.erec[i] = (uint32_t)min(roff, (uint64_t)0x7FFF) | (head ? kErecHead : 0u) | (min(x, 0xFFFFu) << 16);
+    }
+    carry += ptot;
   }
   __syncthreads();
   if (tid >= nb) return;
   const uint32_t b = b0 + tid, s = bst[tid], e = bst[tid + 1];
   bool bad = !mono || e <= s || badf[tid];
   const uint32_t n = bad ? 0 : e - s;
-  const uint64_t carry = recs[tid], last_head = carry - tail[tid];
+  const uint64_t recs = bad ? 0 : bend[tid] - bfirst[tid], last_head = bad ? 0 : lhead[tid] - bfirst[tid];
   const uint32_t bin_len = n ? (n + ri - 1) / ri : 0;
   const uint32_t step = last_head <= 0xFFFF ? 2 : 4;
   const uint32_t buckets = is_index(P) ? 0 : bucket_count(n, P.ratio);
   const uint32_t hash_w = (buckets > 0 && bin_len <= kHashMaxPointers) ? buckets : 0;
-  const uint64_t total = kHdrLen + carry + 1 + (uint64_t)bin_len * step + hash_w + kTrailerLen;
-  if (carry > 0xFFFFFFF0ULL || total > 0xFFFFFF00ULL) bad = true;
+  const uint64_t total = kHdrLen + recs + 1 + (uint64_t)bin_len * step + hash_w + kTrailerLen;
+  if (recs > 0xFFFFFFF0ULL || total > 0xFFFFFF00ULL) bad = true;
   const uint64_t ks = P.it.key_off[s], ke = P.it.key_off[e];
   const uint64_t vs = is_index(P) ? 0 : P.it.val_off[s], ve = is_index(P) ? 0 : P.it.val_off[e];
   uint32_t flags = 0;
@@ -600,7 +642,7 @@ __global__ __launch_bounds__(256) void encode_plan_kernel(EncodeParams P) {
     const uint64_t need = e2_need(total, hash_w);
     flags = need <= kImgMedium ? kPlanMedium : need <= kImgBig ? kPlanBig : kPlanHuge;
   }
-  P.plans[b] = BlockPlan{(uint32_t)carry, bin_len, hash_w, step | (flags << 8)};
+  P.plans[b] = BlockPlan{(uint32_t)recs, bin_len, hash_w, step | (flags << 8)};
   // bits 40.. count the listed (not group) blocks: the size scan numbers them
   P.sizes[b] = (bad ? 0 : total) | ((flags & (kPlanMedium | kPlanBig | kPlanHuge)) ? kListedOne : 0);
   P.kspan[b] = ks;
@@ -638,7 +680,7 @@ struct GBlk {
   uint32_t recs, bin_len;  // record bytes, restart heads
   uint32_t step, hash_w;   // binary-index step, hash-index buckets
   uint32_t hash_base, u0;  // first vote pair, first hash unit
-  uint32_t nbk, rbase;     // full KiB units of the payload, group record bytes before
+  uint32_t nbk, spare;     // full KiB units of the payload
   uint64_t ck_lo, ck_hi;   // payload xxh3_128
 };
 static_assert(sizeof(GBlk) == 64, "GBlk");
@@ -650,38 +692,59 @@ struct GroupLds {
   uint32_t uni[kGUnion / 4];
   GBlk blk[kGBlocks];
   LongSecret secret;
-  uint32_t wsum[kGWaves];
 };
 
 
 // n bytes src[s ..) (LDS) -> dst[d ..) (LDS): byte stores for the dst bytes
 // that share a dword with a neighbour record, aligned dword stores inside
 // (each from two source dwords and v_alignbyte); reads up to 8 bytes past.
-__device__ __forceinline__ void lds_copy(uint8_t* dst, uint32_t d, const uint8_t* src, uint32_t s, uint32_t n) {
+// Lane `rot` starts its dword loop at a lane-dependent point of the span and
+// wraps: records with a power-of-two source stride (64 B values: every lane
+// of a 32-lane group on 2 banks) then read and write conflict-free.
+__device__ __forceinline__ void lds_copy(uint8_t* dst, uint32_t d, const uint8_t* src, uint32_t s, uint32_t n,
+                                         uint32_t rot) {
   if (!n) return;
+  // (every read of a step is issued before its writes: one LDS round trip per step)
   const uint32_t h = min(n, (4u - (d & 3u)) & 3u);
-  for (uint32_t k = 0; k < h; ++k) dst[d + k] = src[s + k];
+  uint32_t hb[3];
+#pragma unroll
+  for (uint32_t k = 0; k < 3; ++k)
+    if (k < h) hb[k] = src[s + k];
+#pragma unroll
+  for (uint32_t k = 0; k < 3; ++k)
+    if (k < h) dst[d + k] = (uint8_t)hb[k];
   if (n == h) return;
   const uint32_t d1 = d + h, e = d + n, body = ((e & ~3u) - d1) >> 2;
   const uint32_t sp = s + h, sh = sp & 3u;
   const uint32_t* s32 = reinterpret_cast<const uint32_t*>(src + (sp & ~3u));
   uint32_t* d32 = reinterpret_cast<uint32_t*>(dst + d1);
-  uint32_t prev = s32[0];
-  uint32_t q = 0;
-  for (; q + 4 <= body; q += 4) {
-    const uint32_t a = s32[q + 1], b = s32[q + 2], c = s32[q + 3], x = s32[q + 4];
-    d32[q] = alignbyte(a, prev, sh);
-    d32[q + 1] = alignbyte(b, a, sh);
-    d32[q + 2] = alignbyte(c, b, sh);
-    d32[q + 3] = alignbyte(x, c, sh);
-    prev = x;
+  uint32_t q = ((rot & 15u) * body) >> 4;  // 0 <= q < body
+  for (uint32_t j0 = 0; j0 < body; j0 += 8) {
+    uint32_t lo[8], hi[8], at[8];
+#pragma unroll
+    for (uint32_t t = 0; t < 8; ++t) {
+      uint32_t p = q + t;
+      p = p >= body ? p - body : p;
+      at[t] = p;
+      if (j0 + t < body) {
+        lo[t] = s32[p];
+        hi[t] = s32[p + 1];
+      }
+    }
+#pragma unroll
+    for (uint32_t t = 0; t < 8; ++t)
+      if (j0 + t < body) d32[at[t]] = alignbyte(hi[t], lo[t], sh);
+    q += 8;
+    q = q >= body ? q - body : q;
   }
-  for (; q < body; ++q) {
-    const uint32_t a = s32[q + 1];
-    d32[q] = alignbyte(a, prev, sh);
-    prev = a;
-  }
-  for (uint32_t k = d1 + 4 * body; k < e; ++k) dst[k] = src[s + (k - d)];
+  const uint32_t t0 = d1 + 4 * body;  // 0..3 tail bytes
+  uint32_t tb[3];
+#pragma unroll
+  for (uint32_t k = 0; k < 3; ++k)
+    if (t0 + k < e) tb[k] = src[s + (t0 + k - d)];
+#pragma unroll
+  for (uint32_t k = 0; k < 3; ++k)
+    if (t0 + k < e) dst[t0 + k] = (uint8_t)tb[k];
 }
 
 __device__ __forceinline__ uint32_t lds_put_leb(uint8_t* dst, uint32_t pos, uint64_t v) {
@@ -691,17 +754,6 @@ __device__ __forceinline__ uint32_t lds_put_leb(uint8_t* dst, uint32_t pos, uint
   }
   dst[pos++] = (uint8_t)v;
   return pos;
-}
-
-// longest_shared_prefix_length (util.rs:125-130) of two staged keys.
-__device__ __forceinline__ uint32_t lcp_lds(const uint8_t* keys, uint32_t a, uint32_t b, uint32_t n) {
-  for (uint32_t k = 0; k < n; k += 16) {
-    const Win16 wa = read_win16(keys, a + k), wb = read_win16(keys, b + k);
-    const uint64_t x0 = wa.lo ^ wb.lo, x1 = wa.hi ^ wb.hi;
-    if (x0) return min(n, k + (uint32_t)(__builtin_ctzll(x0) >> 3));
-    if (x1) return min(n, k + 8 + (uint32_t)(__builtin_ctzll(x1) >> 3));
-  }
-  return n;
 }
 
 __device__ __forceinline__ void group_barrier() {
@@ -794,8 +846,7 @@ __global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(4))) 
       if (i * kWave + lane < vc)
         __builtin_amdgcn_global_load_lds((gbl_void_t*)(vs + 1024 * i), (lds_void_t*)(L.vals + 1024 * i), 16, 0, 0);
   };
-  uint32_t* kofs = L.uni;                          // [kGItems + 1] key offsets in the stage
-  uint32_t* hlo = L.uni + kGItems + 4;             // [kGHash] vote min
+  uint32_t* hlo = L.uni;                           // [kGHash] vote min
   uint32_t* hhi = hlo + kGHash;                    // [kGHash] vote max
   uint64_t* contrib = reinterpret_cast<uint64_t*>(L.uni);  // [kGUnits][4][2] (after the records)
 
@@ -805,7 +856,10 @@ __global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(4))) 
     const uint32_t r0 = g.b - b_begin;
     const uint32_t i0 = rl32(r_start, r0), n = rl32(r_start, r0 + g.k) - i0;
     bool bad = false;
-    if (tid < n) m = load_item(P, (uint64_t)i0 + tid, bad);
+    if (tid < n) {
+      m = load_item(P, (uint64_t)i0 + tid, bad);
+      m.e = P.erec[(uint64_t)i0 + tid];
+    }
   };
 
   // Software pipeline: group G's stage DMA and item fields are issued one
@@ -851,8 +905,6 @@ __global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(4))) 
       const uint32_t nbk = plen > 240 ? (plen - 1) / 1024 : 0;
       const uint32_t units = plen > 240 ? nbk + 1 : 0;
       const uint32_t u0 = wave_incl_scan_u32(units) - units;
-      const uint32_t rin = in ? recs : 0;
-      const uint32_t rbase = wave_incl_scan_u32(rin) - rin;
       if (in) {
         GBlk B;
         B.it0 = st - i0;
@@ -866,14 +918,10 @@ __global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(4))) 
         B.hash_base = hb;
         B.u0 = u0;
         B.nbk = nbk;
-        B.rbase = rbase;
+        B.spare = 0;
         B.ck_lo = B.ck_hi = 0;
         L.blk[lane] = B;
       }
-    }
-    if (live) {
-      kofs[tid] = (uint32_t)(m.ko - kbase);
-      if (tid + 1 == n_items) kofs[tid + 1] = (uint32_t)(m.ko + m.klen - kbase);
     }
     // (shuffles only with every lane active: a bpermute from an inactive lane is undefined)
     const uint32_t hsum = rl32(r_hpre, r0 + k) - rl32(r_hpre, r0);
@@ -883,7 +931,7 @@ __global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(4))) 
     }
     group_barrier();
     ENC_PHASE(1);
-    // ---- item t: block, shared prefix, record length
+    // ---- item t: its block (record offset and shared prefix from E1)
     uint32_t j = 0;
     if (live) {
       uint32_t lo = 0, hi = k;
@@ -894,58 +942,45 @@ __global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(4))) 
       }
       j = lo;
     }
-    const uint32_t it0 = L.blk[j].it0;
-    const uint32_t jj = tid - it0;
-    const bool head = jj % ri == 0;
-    if (live && !index && !head && !(kDiagBuild && (P.diag & 8))) {
-      const uint32_t ht = it0 + (jj / ri) * ri;
-      const uint32_t hk = kofs[ht], hkl = kofs[ht + 1] - hk;
-      m.sh = lcp_lds(L.keys, hk, kofs[tid], min(hkl, m.klen));
-    }
-    const uint32_t rec = live ? (uint32_t)item_record_len(P, m, head) : 0;
-    const uint32_t incl = wave_incl_scan_u32(rec);
-    if (lane == 63) L.wsum[wave] = incl;
-    group_barrier();
-    ENC_PHASE(2);
-    uint32_t wbase = 0;
-    for (uint32_t w = 0; w < wave; ++w) wbase += L.wsum[w];
-    const uint32_t ex = wbase + incl - rec;
+    const bool head = (m.e & kErecHead) != 0;
+    m.sh = head ? 0u : m.e >> 16;
     // ---- item t: its record into the image
     if (live && !(kDiagBuild && (P.diag & 9))) {
       const GBlk& B = L.blk[j];
-      const uint32_t roff = ex - B.rbase;
+      const uint32_t roff = m.e & 0x7FFFu;
       const uint32_t p0 = B.img + kHdrLen;
       uint32_t pos = p0 + roff;
-      const uint32_t kst = kofs[tid];
+      const uint32_t kst = (uint32_t)(m.ko - kbase);
       if (index) {
         L.img[pos++] = 0;
         pos = lds_put_leb(L.img, pos, m.vo);
         pos = lds_put_leb(L.img, pos, m.vl);
         pos = lds_put_leb(L.img, pos, m.seq);
         pos = lds_put_leb(L.img, pos, m.klen);
-        lds_copy(L.img, pos, L.keys, kst, m.klen);
+        lds_copy(L.img, pos, L.keys, kst, m.klen, lane);
       } else {
         L.img[pos++] = (uint8_t)m.vt;
         pos = lds_put_leb(L.img, pos, m.seq);
         const uint32_t from = head ? 0 : m.sh;
         if (!head) pos = lds_put_leb(L.img, pos, m.sh);
         pos = lds_put_leb(L.img, pos, m.klen - from);
-        lds_copy(L.img, pos, L.keys, kst + from, m.klen - from);
+        lds_copy(L.img, pos, L.keys, kst + from, m.klen - from, lane);
         pos += m.klen - from;
         if (!is_tombstone(m.vt)) {
           pos = lds_put_leb(L.img, pos, m.vl);
-          lds_copy(L.img, pos, L.vals, (uint32_t)(m.vo - vbase), m.vl);
+          lds_copy(L.img, pos, L.vals, (uint32_t)(m.vo - vbase), m.vl, lane);
         }
       }
       if (head) {
-        const uint32_t bp = p0 + B.recs + 1 + (jj / ri) * B.step;
+        const uint32_t bp = p0 + B.recs + 1 + (m.e >> 16) * B.step;
         for (uint32_t q = 0; q < B.step; ++q) L.img[bp + q] = (uint8_t)(roff >> (8 * q));
       }
       if (B.hash_w) {
+        const uint32_t ridx = (tid - B.it0) / ri;
         const uint64_t hv = xxh3_64_any(m.klen, BaseReader8{L.keys, kst}, BaseReader64{L.keys, kst});
         const uint32_t bk = B.hash_base + (uint32_t)(hv % B.hash_w);
-        atomicMin(&hlo[bk], jj / ri);
-        atomicMax(&hhi[bk], jj / ri);
+        atomicMin(&hlo[bk], ridx);
+        atomicMax(&hhi[bk], ridx);
       }
     }
     group_barrier();
@@ -1182,9 +1217,9 @@ static unsigned long long* diag_phase_buffer() {
 static size_t al256(size_t x) { return (x + 255) / 256 * 256; }
 
 size_t encode_workspace_size(uint64_t n_items, uint32_t n_blocks) {
-  (void)n_items;
   return 2 * al256(((size_t)n_blocks + 1) * 8) + al256((size_t)n_blocks * 8) +
-         al256((size_t)n_blocks * sizeof(BlockPlan)) + al256((size_t)n_blocks * 4) + 256 + al256(scan_tiles(n_blocks) * 8);
+         al256((size_t)n_blocks * sizeof(BlockPlan)) + al256((size_t)n_blocks * 4) + 256 +
+         al256(scan_tiles(n_blocks) * 8) + al256((size_t)n_items * 4);
 }
 
 uint64_t encode_bound(uint64_t n_items, uint32_t n_blocks, uint64_t key_bytes, uint64_t val_bytes,
@@ -1223,7 +1258,8 @@ hipError_t launch_encode(const lsm_items& items, const uint32_t* starts, uint32_
   P.plans = (BlockPlan*)w; w += al256((size_t)n_blocks * sizeof(BlockPlan));
   P.lists = (uint32_t*)w; w += al256((size_t)n_blocks * 4);
   P.list_count = (uint32_t*)w; w += 256;
-  uint64_t* tiles = (uint64_t*)w;
+  uint64_t* tiles = (uint64_t*)w; w += al256(scan_tiles(n_blocks) * 8);
+  P.erec = (uint32_t*)w;
   hipError_t e;
   hipLaunchKernelGGL(encode_plan_kernel, dim3((n_blocks + kPlanBlocks - 1) / kPlanBlocks), dim3(256), 0, st, P);
   if ((e = launch_excl_scan(P.sizes, n_blocks, tiles,

@@ -19,6 +19,7 @@ def main():
     ap.add_argument("--blocks", type=int, default=1 << 20)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--workload", default="counter", choices=["counter", "prefix16k"])
+    ap.add_argument("--diag-bits", type=int, default=0, help="lsm_block_params.reserved for the timed loop (diagnostic build)")
     ap.add_argument("--phases", action="store_true", help="per-phase cycles of the group kernel (diagnostic build)")
     ap.add_argument("--ablate", action="store_true", help="diagnostic ablations (lsm_block_params.reserved bits)")
     args = ap.parse_args()
@@ -28,6 +29,10 @@ def main():
         items, starts, n_items = bench.make_workload(torch, lsmgpu, nb)
     else:
         items, starts, n_items = bench.make_workload(torch, lsmgpu, nb, items_per_block=56, key_len=40, val_len=256)
+    if args.diag_bits:
+        lsmgpu.lib()
+        orig_p = lsmgpu.LsmBlockParams
+        lsmgpu.LsmBlockParams = lambda ri, bt, c, r, hr: orig_p(ri, bt, c, args.diag_bits, hr)
     enc_ctx = lsmgpu.Encoder()
     enc = enc_ctx.encode(items, starts, nb)
     torch.cuda.synchronize()
