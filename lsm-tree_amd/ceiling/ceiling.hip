@@ -1,8 +1,11 @@
 // ceiling.hip — measurement-only kernels (liblsmceiling.so, NOT part of the
 // product library or its header): the practical HBM ceilings the bench
 // reports next to the 8 TB/s spec peak.
-//   lsm_ceiling_copy   16 B/lane streaming copy (read + write), grid-stride,
-//                      four loads in flight per lane: the R+W ceiling.
+//   lsm_ceiling_copy   16 B/lane streaming copy (read + write): one 8 KiB tile
+//                      per workgroup, 2 loads per lane then 2 stores (the
+//                      fastest of the variants in scripts/copy_ceiling_sweep.py:
+//                      5.88 TB/s vs 4.77 for a 4-deep grid-stride loop and
+//                      4.1 for 8 per lane): the R+W ceiling.
 //   lsm_ceiling_read   the decode kernel's read shape alone: 4-wave
 //                      workgroups (four per CU) stage consecutive 32 KiB spans
 //                      into LDS by LDS-DMA, nothing computed: the read ceiling.
@@ -27,6 +30,25 @@ __global__ __launch_bounds__(256) void copy_kernel(const u32x4* __restrict__ src
     dst[i + 3 * stride] = d;
   }
   for (; i < n16; i += stride) dst[i] = src[i];
+}
+
+// One tile of K x 4 KiB per workgroup (K x 16 B per lane, all loads then all
+// stores), grid = the whole buffer: no grid-stride loop.  mode bit 0:
+// non-temporal loads, bit 1: non-temporal stores.
+template <int K>
+__global__ __launch_bounds__(256) void copy_tile_kernel(const u32x4* __restrict__ src, u32x4* __restrict__ dst,
+                                                        uint64_t n16, int mode) {
+  const uint64_t base = (uint64_t)blockIdx.x * (256 * K) + threadIdx.x;
+  u32x4 v[K];
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+    if (base + 256 * k < n16) v[k] = (mode & 1) ? __builtin_nontemporal_load(src + base + 256 * k) : src[base + 256 * k];
+#pragma unroll
+  for (int k = 0; k < K; ++k)
+    if (base + 256 * k < n16) {
+      if (mode & 2) __builtin_nontemporal_store(v[k], dst + base + 256 * k);
+      else dst[base + 256 * k] = v[k];
+    }
 }
 
 constexpr uint32_t kSpan = 32768;
@@ -55,12 +77,26 @@ __global__ __launch_bounds__(256) void read_kernel(const uint8_t* __restrict__ s
 
 }  // namespace
 
-extern "C" int lsm_ceiling_copy(const void* src, void* dst, uint64_t bytes, void* stream) {
+extern "C" int lsm_ceiling_copy_variant(const void* src, void* dst, uint64_t bytes, int variant, void* stream) {
   if (((uintptr_t)src | (uintptr_t)dst | bytes) & 15) return 10;
   const uint64_t n16 = bytes / 16;
-  hipLaunchKernelGGL(copy_kernel, dim3(256 * 8), dim3(256), 0, (hipStream_t)stream, (const u32x4*)src, (u32x4*)dst,
-                     n16);
+  if (variant == 0)
+    hipLaunchKernelGGL(copy_kernel, dim3(256 * 8), dim3(256), 0, (hipStream_t)stream, (const u32x4*)src,
+                       (u32x4*)dst, n16);
+  else if (variant <= 4)  // 1..4: mode = variant - 1, 4 per lane
+    hipLaunchKernelGGL(copy_tile_kernel<4>, dim3((unsigned)((n16 + 1023) / 1024)), dim3(256), 0, (hipStream_t)stream,
+                       (const u32x4*)src, (u32x4*)dst, n16, variant - 1);
+  else if (variant <= 8)  // 5..8: mode = variant - 5, 8 per lane
+    hipLaunchKernelGGL(copy_tile_kernel<8>, dim3((unsigned)((n16 + 2047) / 2048)), dim3(256), 0, (hipStream_t)stream,
+                       (const u32x4*)src, (u32x4*)dst, n16, variant - 5);
+  else  // 9..12: 2 per lane
+    hipLaunchKernelGGL(copy_tile_kernel<2>, dim3((unsigned)((n16 + 511) / 512)), dim3(256), 0, (hipStream_t)stream,
+                       (const u32x4*)src, (u32x4*)dst, n16, variant - 9);
   return hipGetLastError() == hipSuccess ? 0 : 11;
+}
+
+extern "C" int lsm_ceiling_copy(const void* src, void* dst, uint64_t bytes, void* stream) {
+  return lsm_ceiling_copy_variant(src, dst, bytes, 9, stream);  // the fastest of scripts/copy_ceiling_sweep.py
 }
 
 extern "C" int lsm_ceiling_read(const void* src, uint64_t bytes, uint32_t* sink, void* stream) {
