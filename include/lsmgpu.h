@@ -27,6 +27,11 @@
  *   lsm_xxh3_128_file  <- ChecksummedWriter         src/checksum.rs:59-96 (whole-file checksum)
  *   lsm_lz4_decompress_blocks <- Block::from_reader/from_file, CompressionType::Lz4  block/mod.rs:87-182
  *   lsm_lz4_plan_output <- the builder_unzeroed(uncompressed_length) sizing of the same  block/mod.rs:104-112
+ *   lsm_lz4_plan_framed / lsm_lz4_decompress_framed + lsm_decode_blocks_tuned(LSM_DECODE_PAYLOAD_VERIFIED)
+ *                      <- Block::from_reader(Lz4) then DataBlock::new + iter   block/mod.rs:104-118, data_block/mod.rs:335,476
+ *   lsm_scan_table     <- Scanner::new / next      src/table/scanner.rs:24-92 (block handles from the
+ *                         block index: FullBlockIndex / TwoLevelBlockIndex, src/table/block_index/,
+ *                         regions from the TOC, src/table/regions.rs:55-76)
  *   lsm_bloom_shape    <- BloomConstructionPolicy::init  src/table/filter/mod.rs:25-34
  *   lsm_hash64_keys    <- FullFilterWriter::register_key src/table/writer/filter/full.rs:47-50
  *   lsm_bloom_build    <- standard_bloom Builder set_with_hash + build  builder.rs:33-53,154-170
@@ -42,7 +47,7 @@
 extern "C" {
 #endif
 
-#define LSM_ABI_VERSION 2
+#define LSM_ABI_VERSION 3
 #define LSM_HEADER_LEN 33  /* Header::serialized_len(), header.rs:64-76 */
 #define LSM_TRAILER_LEN 31 /* TRAILER_SIZE, trailer.rs:14-23 */
 /* d_blocks must be 16-byte aligned and readable for LSM_INPUT_PADDING bytes
@@ -118,7 +123,8 @@ typedef struct lsm_block_params {
 } lsm_block_params;
 
 /* Tuning knobs for the decode kernel (0 = library default).  Any flag bit
- * other than LSM_DECODE_ITEM_START_VALID is rejected with LSM_BAD_ARG. */
+ * other than LSM_DECODE_ITEM_START_VALID / LSM_DECODE_PAYLOAD_VERIFIED is
+ * rejected with LSM_BAD_ARG. */
 typedef struct lsm_decode_tuning {
     uint32_t blocks_per_wave;  /* consecutive blocks one workgroup owns (1..63, default 48) */
     uint32_t stage_bytes;      /* LDS stage bytes (256..65536, default 32768); larger blocks take the general path */
@@ -127,6 +133,12 @@ typedef struct lsm_decode_tuning {
                                   prefix sum of this batch (skip the count + scan pass) */
 } lsm_decode_tuning;
 #define LSM_DECODE_ITEM_START_VALID 1u
+/* The payload checksums were verified upstream: skip the xxh3_128 of every
+ * payload (header fields, data_length, type, trailer and records are still
+ * checked).  For LZ4 blocks decompressed by lsm_lz4_decompress_framed, whose
+ * stored bytes Block::from_reader verified before decompressing
+ * (block/mod.rs:94-118); their frame headers carry the STORED checksum. */
+#define LSM_DECODE_PAYLOAD_VERIFIED 2u
 
 /* Point-read results (DataBlock::point_read -> Option<InternalValue>,
  * data_block/mod.rs:412-472), one row per query; NULL fields other than item
@@ -304,6 +316,58 @@ int lsm_lz4_plan_output(const uint8_t* d_blocks, const uint64_t* d_block_off, ui
 int lsm_lz4_decompress_blocks(const uint8_t* d_blocks, const uint64_t* d_block_off, uint32_t n_blocks,
                               uint8_t* d_out, const uint64_t* d_out_off, int32_t* d_status,
                               void* d_workspace, size_t workspace_bytes, void* stream);
+
+/* LZ4 -> parse chaining.  lsm_lz4_plan_framed is lsm_lz4_plan_output with 33
+ * more bytes per verified block; lsm_lz4_decompress_framed writes each block
+ * as a frame d_out[d_out_off[b] ..) = Header' || decompressed payload, where
+ * Header' = the stored header with data_length = uncompressed_length and its
+ * header checksum recomputed (the payload checksum field stays the STORED
+ * bytes' checksum).  The frames are then decoded in place with
+ * lsm_decode_blocks_tuned(d_out, d_out_off, ..., flags LSM_DECODE_PAYLOAD_VERIFIED);
+ * a block's final status is its lsm_lz4_decompress_framed status if that is
+ * not LSM_OK, else its decode status. */
+int lsm_lz4_plan_framed(const uint8_t* d_blocks, const uint64_t* d_block_off, uint32_t n_blocks,
+                        uint64_t max_block_bytes, uint64_t* d_out_off, void* d_workspace, size_t workspace_bytes,
+                        void* stream);
+int lsm_lz4_decompress_framed(const uint8_t* d_blocks, const uint64_t* d_block_off, uint32_t n_blocks,
+                              uint8_t* d_out, const uint64_t* d_out_off, int32_t* d_status,
+                              void* d_workspace, size_t workspace_bytes, void* stream);
+
+/* ---- whole-table scan (Scanner, src/table/scanner.rs:24-92) -----------------
+ * Decodes every data block of one table file image d_file[0 .. file_len) (16-byte
+ * aligned, LSM_INPUT_PADDING readable bytes past file_len), in file order, as the
+ * compaction read side does.  The block handles come from the table's block
+ * index on the device: the TLI block (an index block at table->tli_off, size
+ * table->tli_size: the "tli" TOC section, regions.rs:55-76) lists the data
+ * blocks (FullBlockIndex, writer/index/full.rs:55-69) or, with
+ * table->two_level (the TOC has an "index" section), index partitions that list
+ * them (TwoLevelBlockIndex, writer/index/partitioned.rs:54-125).  The data
+ * blocks must be contiguous from file offset 0 (the layout Scanner reads back to
+ * back) and end inside the file.  Every item's seqno gets table->global_seqno
+ * added (scanner.rs:84, wrapping).
+ * Outputs: d_block_off (cap_blocks+1 u64: the data blocks, as lsm_decode_blocks
+ * takes them), parsed items / d_item_start / d_status as lsm_decode_blocks
+ * (block type Data expected, fetch_next_block scanner.rs:54-72),
+ * *n_blocks (host) = number of data blocks, *table_status (host) = LSM_OK, or the
+ * status of the first failing index block, LSM_OVERFLOW (more than cap_blocks
+ * blocks or index entries), LSM_TRUNCATED (handles not contiguous from 0 or past
+ * file_len) or LSM_PARSE (block count != table->block_count when non-zero,
+ * the metadata's data_block_count).
+ * Synchronises `stream` once per index level (the block count sizes the data
+ * decode); the data decode itself is left enqueued on `stream`.
+ * Workspace: lsm_scan_workspace_size(cap_blocks) bytes. */
+typedef struct lsm_table_scan {
+    uint64_t tli_off;       /* TLI region handle (TOC "tli" section) */
+    uint32_t tli_size;
+    uint32_t two_level;     /* 1: TLI entries are index partitions (TOC "index" section present) */
+    uint64_t global_seqno;  /* Table::global_seqno, added to every item's seqno */
+    uint64_t block_count;   /* ParsedMeta data_block_count (0 = not checked) */
+} lsm_table_scan;
+size_t lsm_scan_workspace_size(uint32_t cap_blocks);
+int lsm_scan_table(const uint8_t* d_file, uint64_t file_len, const lsm_table_scan* table,
+                   uint64_t* d_block_off, uint32_t cap_blocks, const lsm_parsed_items* d_out, uint64_t item_cap,
+                   uint32_t* d_item_start, int32_t* d_status, uint32_t* n_blocks, int32_t* table_status,
+                   void* d_workspace, size_t workspace_bytes, void* stream);
 
 #ifdef __cplusplus
 }

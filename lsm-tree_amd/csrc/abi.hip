@@ -23,10 +23,6 @@ int lsmgpu::hip_status(hipError_t e, const char* where) {
 namespace {
 int set_hip_error(hipError_t e, const char* where) { return lsmgpu::hip_status(e, where); }
 
-constexpr uint32_t kDefaultBlocksPerWave = 48;  // per workgroup
-constexpr uint32_t kDefaultStageBytes = 32768;  // four 4-wave workgroups per CU (LDS ~40 KiB each)
-constexpr uint32_t kDefaultTileItems = 448;
-
 }  // namespace
 
 extern "C" {
@@ -88,12 +84,14 @@ int lsm_decode_blocks_tuned(const uint8_t* d_blocks, const uint64_t* d_block_off
   P.item_start_w = d_item_start;
   P.status = d_status;
   P.flags = tuning ? tuning->flags : 0;
-  const uint32_t allowed = LSM_DECODE_ITEM_START_VALID | (lsmgpu::kDiagBuild ? lsmgpu::kDecodeDiagMask : 0u);
+  const uint32_t allowed = LSM_DECODE_ITEM_START_VALID | LSM_DECODE_PAYLOAD_VERIFIED |
+                           (lsmgpu::kDiagBuild ? lsmgpu::kDecodeDiagMask : 0u);
   if (P.flags & ~allowed) return LSM_BAD_ARG;
   auto pick = [&](uint32_t v, uint32_t dflt) { return v ? v : dflt; };
-  P.blocks_per_wave = pick(tuning ? tuning->blocks_per_wave : 0, kDefaultBlocksPerWave);
-  P.stage_bytes = pick(tuning ? tuning->stage_bytes : 0, kDefaultStageBytes);
-  P.tile_items = pick(tuning ? tuning->tile_items : 0, kDefaultTileItems);
+  P.blocks_per_wave = pick(tuning ? tuning->blocks_per_wave : 0, lsmgpu::kDefaultBlocksPerWave);
+  P.stage_bytes = pick(tuning ? tuning->stage_bytes : 0, lsmgpu::kDefaultStageBytes);
+  P.tile_items = pick(tuning ? tuning->tile_items : 0, lsmgpu::kDefaultTileItems);
+  P.seqno_add = 0;
   if (P.tile_items > 8192 || P.stage_bytes < 256 || P.stage_bytes > 65536 || P.blocks_per_wave > 63)
     return LSM_BAD_ARG;
   P.stage_bytes = (P.stage_bytes + 15) & ~15u;

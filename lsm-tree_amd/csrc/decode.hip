@@ -5,21 +5,21 @@
 // (src/table/util.rs:79-86) and the full forward DataBlock::iter() /
 // IndexBlock::iter() (src/table/block/decoder.rs:442-483) over a whole batch.
 //
-// Launch shape (DESIGN.md "Decode kernel"): one 64-lane wave per workgroup,
-// wave w owns blocks [w*BPW, (w+1)*BPW) and walks them in GROUPS — the longest
-// run of consecutive blocks that fits the LDS stage (consecutive blocks are
+// Launch shape: 4-wave workgroups, four per CU.  Workgroup w
+// owns blocks [w*BPW, (w+1)*BPW) and walks them in GROUPS — the longest run of
+// consecutive blocks that fits the 32 KiB LDS stage (consecutive blocks are
 // contiguous on disk, so a group is one contiguous span):
-//   1. lane j holds block j's handle and item range in registers;
-//   2. the span is copied HBM -> LDS with global_load_lds_dwordx4 (1 KiB per
-//      wave instruction), one wait per group;
-//   3. lane j checks block j's header (magic, type, 29-byte xxh3 checksum);
-//   4. the four 16-lane DPP rows hash four payloads at a time (xxh3_128);
-//   5. lane j reads block j's trailer, a wave scan numbers the restart
-//      intervals of the group;
-//   6. phase A: lane = restart interval, walks record boundaries only;
-//   7. phase B: lane = record, parses and validates every field and stores
-//      the parsed-item SoA with coalesced global stores.
-// Blocks larger than the stage take decode_block_direct (same parsers on HBM).
+//   1. lane j of every wave holds block j's handle and item range;
+//   2. all waves copy the span HBM -> LDS with global_load_lds_dwordx4;
+//   3. wave 0: lane j checks block j's header fields and trailer, a wave scan
+//      numbers the restart intervals of the group;
+//   4. phase A on one wave (lane = restart interval) walks record boundaries
+//      only, while the other waves verify the payload xxh3_128 (16-lane DPP
+//      rows) and the header checksums;
+//   5. phase B on all waves (thread = record) parses and validates every
+//      field and stores the parsed-item SoA with coalesced global stores.
+// Blocks larger than the stage, index blocks and rare record shapes go to
+// decode_deferred_staged_kernel (one block per 4-wave workgroup, LEB cursor).
 #include <hip/hip_runtime.h>
 
 #include "block_format.hpp"
@@ -98,8 +98,9 @@ __device__ __forceinline__ void lds_barrier() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
-__device__ __forceinline__ void emit_global(const lsm_parsed_items& o, uint64_t i, const ItemFields& f) {
-  if (o.seqno) gstore(o.seqno, i, f.seqno);
+__device__ __forceinline__ void emit_global(const lsm_parsed_items& o, uint64_t i, const ItemFields& f,
+                                            uint64_t seqno_add) {
+  if (o.seqno) gstore(o.seqno, i, f.seqno + seqno_add);
   if (o.key_off) gstore(o.key_off, i, f.key_off);
   if (o.val_off) gstore(o.val_off, i, f.val_off);
   if (o.val_len) gstore(o.val_len, i, f.val_len);
@@ -386,7 +387,7 @@ __host__ __device__ __forceinline__ bool all_fields(const lsm_parsed_items& o) {
 __device__ __forceinline__ void store_fields(const DecodeParams& P, bool all_fields, uint64_t gi,
                                              const ItemFields& f) {
   if (all_fields) {  // every output array present: no per-field null checks
-    gstore(P.out.seqno, gi, f.seqno);
+    gstore(P.out.seqno, gi, f.seqno + P.seqno_add);
     gstore(P.out.key_off, gi, f.key_off);
     gstore(P.out.val_off, gi, f.val_off);
     gstore(P.out.val_len, gi, f.val_len);
@@ -395,7 +396,7 @@ __device__ __forceinline__ void store_fields(const DecodeParams& P, bool all_fie
     gstore(P.out.vtype, gi, f.vtype);
     if (P.out.handle_off) gstore(P.out.handle_off, gi, f.handle_off);
   } else {
-    emit_global(P.out, gi, f);
+    emit_global(P.out, gi, f, P.seqno_add);
   }
 }
 
@@ -466,7 +467,7 @@ __device__ __forceinline__ void decode_block_direct(const DecodeParams& P, uint3
   const uint32_t cap = gload(P.item_start, b + 1) - gload(P.item_start, b);
   if (lane == 0) meta_header(base, hb, len, meta[0]);
   wave_sync();
-  if (meta[0].st == ST_OK) {
+  if (meta[0].st == ST_OK && !(P.flags & LSM_DECODE_PAYLOAD_VERIFIED)) {
     uint64_t lo, hi;
     xxh3_128_wave(base, hb + kHdrLen, meta[0].len - kHdrLen, &kLongSecret, lo, hi);
     if (lane == 0 && (lo != meta[0].ck_lo || hi != meta[0].ck_hi)) meta[0].st = ST_CKSUM;
@@ -479,7 +480,7 @@ __device__ __forceinline__ void decode_block_direct(const DecodeParams& P, uint3
     bool ok = true;
     for (uint32_t r = lane; r < m.bin_len; r += kWave) {
       ok &= walk_interval(base, hb + kHdrLen, m, r,
-                          [&](uint32_t j, const ItemFields& f) { emit_global(P.out, item_base + j, f); });
+                          [&](uint32_t j, const ItemFields& f) { emit_global(P.out, item_base + j, f, P.seqno_add); });
     }
     if (!ok) atomicCAS(&meta[0].st, ST_OK, ST_PARSE);
   }
@@ -605,7 +606,7 @@ __global__ __launch_bounds__(kBigWaves * kWave) void decode_deferred_staged_kern
     }
     lds_barrier();
     // payload checksum: per-KiB contributions on all waves, then the chain on wave 0
-    const bool hdr_ok = meta[0].st == ST_OK;
+    const bool hdr_ok = meta[0].st == ST_OK && !(P.flags & LSM_DECODE_PAYLOAD_VERIFIED);
     const uint32_t plen = meta[0].len - kHdrLen;
     if (hdr_ok && plen > 240) xxh3_kib_contribs(stage, hb + kHdrLen, plen, &kLongSecret, contrib, wave, kBigWaves);
     lds_barrier();
@@ -622,7 +623,7 @@ __global__ __launch_bounds__(kBigWaves * kWave) void decode_deferred_staged_kern
         bool ok = true;
         for (uint32_t r = tid - kWave; r < m.bin_len; r += (kBigWaves - 1) * kWave) {
           ok &= walk_interval(stage, hb + kHdrLen, m, r,
-                              [&](uint32_t j, const ItemFields& f) { emit_global(P.out, item_base + j, f); });
+                              [&](uint32_t j, const ItemFields& f) { emit_global(P.out, item_base + j, f, P.seqno_add); });
         }
         if (!ok) atomicCAS(&meta[1].st, ST_OK, ST_PARSE);
       }
@@ -753,7 +754,8 @@ __global__ __launch_bounds__(kGroupWaves * kWave) __attribute__((amdgpu_waves_pe
                              : meta[k - 1].chain0 + (meta[k - 1].st == ST_OK ? meta[k - 1].bin_len : 0);
       const uint32_t nA = min((total + kWave - 1) / kWave, kGroupWaves - 1);
       const uint32_t role = (wave + kGroupWaves - iter % kGroupWaves) % kGroupWaves;  // rotates per group
-      const bool hash = !(kDiagBuild && (P.flags & kDiagSkipHash));
+      // payload checksums (not when verified upstream: the LZ4 path checks the stored bytes)
+      const bool hash = !(kDiagBuild && (P.flags & kDiagSkipHash)) && !(P.flags & LSM_DECODE_PAYLOAD_VERIFIED);
       if (role < nA) {
         phase_a(stage, meta, owner, rec, role * kWave, nA * kWave, total, P.tile_items);
       } else if (hash && k <= kGroupWaves - nA) {

@@ -8,6 +8,12 @@
 
 namespace lsmgpu {
 
+// Default decode tuning (lsm_decode_tuning zeros): 48 blocks per 4-wave
+// workgroup, a 32 KiB LDS stage (four workgroups per CU, ~40 KiB LDS each).
+constexpr uint32_t kDefaultBlocksPerWave = 48;
+constexpr uint32_t kDefaultStageBytes = 32768;
+constexpr uint32_t kDefaultTileItems = 448;
+
 struct DecodeParams {
   const uint8_t* blocks;
   const uint64_t* block_off;
@@ -24,6 +30,7 @@ struct DecodeParams {
   uint32_t flags;
   uint32_t* defer_count;  // workspace: blocks handed to the general path
   uint32_t* defer_list;
+  uint64_t seqno_add;     // added to every decoded seqno (Scanner's global_seqno, scanner.rs:84)
 };
 
 // Diagnostic builds (-DLSM_DIAG, `make variant`) honour ablation bits in

@@ -147,8 +147,10 @@ struct Lz4Block {
 };
 
 // Header + payload checksum (Block::from_reader, mod.rs:92-102); wave-uniform.
+// frame = 0 (payload only) or kHdrLen (lsm_lz4_decompress_framed: the payload
+// follows a frame header written by lz4_frame_headers_kernel).
 __device__ __forceinline__ int32_t lz4_check_block(const uint8_t* blocks, const uint64_t* block_off, const uint64_t* out_off,
-                                   uint8_t* out, uint32_t i, Lz4Block& b) {
+                                   uint8_t* out, uint32_t i, uint32_t frame, Lz4Block& b) {
   const uint64_t o = block_off[i], e = block_off[i + 1];
   b.base = blocks + (o & ~15ULL);
   b.hb = (uint32_t)(o & 15);
@@ -158,11 +160,11 @@ __device__ __forceinline__ int32_t lz4_check_block(const uint8_t* blocks, const 
   if ((uint64_t)h.data_length != e - o - kHdrLen) return ST_TRUNCATED;
   b.data_len = __builtin_amdgcn_readfirstlane(h.data_length);  // wave-uniform: keep the walk scalar
   b.raw_len = __builtin_amdgcn_readfirstlane(read_u32_unaligned(b.base, b.hb + 25));  // uncompressed_length, header.rs:101
-  if ((uint64_t)b.raw_len != out_off[i + 1] - out_off[i]) return ST_OVERFLOW;
+  if ((uint64_t)b.raw_len + frame != out_off[i + 1] - out_off[i]) return ST_OVERFLOW;
   uint64_t lo, hi;
   xxh3_128_wave(b.base, b.hb + kHdrLen, b.data_len, &kLongSecret, lo, hi);
   if (lo != h.ck_lo || hi != h.ck_hi) return ST_CKSUM;
-  b.dst = out + out_off[i];
+  b.dst = out + out_off[i] + frame;
   return ST_OK;
 }
 
@@ -207,14 +209,14 @@ constexpr uint32_t kLargeIn = 72 * 1024, kLargeOut = 80 * 1024;
 __global__ __launch_bounds__(256) void lz4_small_kernel(const uint8_t* __restrict__ blocks,
                                                         const uint64_t* __restrict__ block_off, uint32_t n,
                                                         uint8_t* __restrict__ out, const uint64_t* __restrict__ out_off,
-                                                        int32_t* __restrict__ status) {
+                                                        int32_t* __restrict__ status, uint32_t frame) {
   __shared__ uint32_t s_in[4][kSmallIn / 4];
   __shared__ uint8_t s_out[4][kSmallOut];
   const int wv = threadIdx.x >> 6, lane = threadIdx.x & 63;
   const uint32_t i = blockIdx.x * 4 + wv;
   if (i >= n) return;
   Lz4Block b;
-  int32_t st = lz4_check_block(blocks, block_off, out_off, out, i, b);
+  int32_t st = lz4_check_block(blocks, block_off, out_off, out, i, frame, b);
   if (st == ST_OK) {
     const uint32_t sh = (b.hb + kHdrLen) & 3u;
     if (b.data_len + sh + 12 > kSmallIn || b.raw_len > kSmallOut)  // +12: dword window + 8-byte reads
@@ -229,14 +231,14 @@ __global__ __launch_bounds__(64) void lz4_large_kernel(const uint8_t* __restrict
                                                        const uint64_t* __restrict__ block_off, uint32_t n,
                                                        uint8_t* __restrict__ out, const uint64_t* __restrict__ out_off,
                                                        int32_t* __restrict__ status, const uint32_t* __restrict__ list,
-                                                       const uint32_t* __restrict__ count) {
+                                                       const uint32_t* __restrict__ count, uint32_t frame) {
   extern __shared__ uint32_t s_dyn[];
   const int lane = threadIdx.x;
   const uint32_t total = *count;
   for (uint32_t li = blockIdx.x; li < total; li += gridDim.x) {
     const uint32_t i = list[li];
     Lz4Block b;
-    int32_t st = lz4_check_block(blocks, block_off, out_off, out, i, b);
+    int32_t st = lz4_check_block(blocks, block_off, out_off, out, i, frame, b);
     if (st == ST_OK) {
       const uint32_t sh = (b.hb + kHdrLen) & 3u;
       if (b.data_len + sh + 12 <= kLargeIn && b.raw_len <= kLargeOut) {
@@ -265,7 +267,7 @@ __global__ __launch_bounds__(256) void lz4_collect_deferred(int32_t* __restrict_
 // caller's cap (that block then reports its header status, or OVERFLOW).
 __global__ __launch_bounds__(256) void lz4_plan_kernel(const uint8_t* __restrict__ blocks,
                                                        const uint64_t* __restrict__ block_off, uint32_t n,
-                                                       uint64_t max_raw, uint64_t* __restrict__ raw) {
+                                                       uint64_t max_raw, uint32_t frame, uint64_t* __restrict__ raw) {
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
   if (i >= n) return;
   const uint64_t o = block_off[i], e = block_off[i + 1];
@@ -275,9 +277,37 @@ __global__ __launch_bounds__(256) void lz4_plan_kernel(const uint8_t* __restrict
   uint64_t len = 0;
   if (e >= o && check_header(base, hb, e - o, h) == ST_OK && (uint64_t)h.data_length == e - o - kHdrLen) {
     len = read_u32_unaligned(base, hb + 25);  // uncompressed_length, header.rs:101
-    if (len > max_raw) len = 0;
+    len = len > max_raw ? 0 : len + frame;
   }
   raw[i] = len;
+}
+
+// Frame headers of lsm_lz4_decompress_framed (lane per block): the stored
+// header with data_length = uncompressed_length and the header checksum
+// recomputed over the new first 29 bytes (header.rs:83-109), so the frame is a
+// well-formed uncompressed block whose payload checksum field still names the
+// stored bytes (decoded with LSM_DECODE_PAYLOAD_VERIFIED).  Blocks whose plan
+// gave no frame (failed header) are skipped.
+__global__ __launch_bounds__(256) void lz4_frame_headers_kernel(const uint8_t* __restrict__ blocks,
+                                                                const uint64_t* __restrict__ block_off, uint32_t n,
+                                                                uint8_t* __restrict__ out,
+                                                                const uint64_t* __restrict__ out_off) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i >= n) return;
+  const uint64_t fo = out_off[i];
+  if (out_off[i + 1] - fo < kHdrLen) return;
+  const uint64_t o = block_off[i];
+  const uint8_t* base = blocks + (o & ~15ULL);
+  const uint32_t hb = (uint32_t)(o & 15);
+  uint32_t h[12] = {0};  // 29 header bytes + the readers' 12-byte over-read
+  uint8_t* hp = reinterpret_cast<uint8_t*>(h);
+  for (uint32_t j = 0; j < 21; ++j) hp[j] = base[hb + j];           // magic, type, stored checksum
+  const uint32_t ul = read_u32_unaligned(base, hb + 25);
+  for (uint32_t j = 0; j < 4; ++j) hp[21 + j] = hp[25 + j] = (uint8_t)(ul >> (8 * j));
+  uint64_t lo, hi;
+  xxh3_128_short(29, BaseReader8{hp, 0}, BaseReader64{hp, 0}, lo, hi);
+  for (uint32_t j = 0; j < 4; ++j) hp[29 + j] = (uint8_t)(lo >> (8 * j));
+  for (uint32_t j = 0; j < kHdrLen; ++j) out[fo + j] = hp[j];
 }
 
 struct Lz4OffOut {
@@ -293,9 +323,8 @@ extern "C" size_t lsm_lz4_plan_workspace_size(uint32_t n_blocks) {
   return ((size_t)n_blocks * 8 + 255) / 256 * 256 + (scan_tiles(n_blocks ? n_blocks : 1) * 8 + 255) / 256 * 256;
 }
 
-extern "C" int lsm_lz4_plan_output(const uint8_t* d_blocks, const uint64_t* d_block_off, uint32_t n_blocks,
-                                   uint64_t max_block_bytes, uint64_t* d_out_off, void* d_workspace,
-                                   size_t workspace_bytes, void* stream) {
+static int lz4_plan(const uint8_t* d_blocks, const uint64_t* d_block_off, uint32_t n_blocks, uint64_t max_block_bytes,
+                    uint64_t* d_out_off, void* d_workspace, size_t workspace_bytes, void* stream, uint32_t frame) {
   if (n_blocks == 0) return LSM_OK;
   if (!d_blocks || !d_block_off || !d_out_off || !d_workspace || ((uintptr_t)d_blocks & 15) ||
       workspace_bytes < lsm_lz4_plan_workspace_size(n_blocks))
@@ -304,16 +333,29 @@ extern "C" int lsm_lz4_plan_output(const uint8_t* d_blocks, const uint64_t* d_bl
   uint64_t* raw = (uint64_t*)d_workspace;
   uint64_t* tiles = (uint64_t*)((uint8_t*)d_workspace + ((size_t)n_blocks * 8 + 255) / 256 * 256);
   hipLaunchKernelGGL(lz4_plan_kernel, dim3((n_blocks + 255) / 256), dim3(256), 0, st, d_blocks, d_block_off, n_blocks,
-                     max_block_bytes, raw);
+                     max_block_bytes, frame, raw);
   hipError_t e = launch_excl_scan(raw, n_blocks, tiles, Lz4OffOut{d_out_off}, st);
   return hip_status(e != hipSuccess ? e : hipGetLastError(), "lsm_lz4_plan_output");
 }
 
 extern "C" size_t lsm_lz4_workspace_size(uint32_t n_blocks) { return 16 + (size_t)n_blocks * 4; }
 
-extern "C" int lsm_lz4_decompress_blocks(const uint8_t* d_blocks, const uint64_t* d_block_off, uint32_t n_blocks,
-                                         uint8_t* d_out, const uint64_t* d_out_off, int32_t* d_status,
-                                         void* d_workspace, size_t workspace_bytes, void* stream) {
+extern "C" int lsm_lz4_plan_output(const uint8_t* d_blocks, const uint64_t* d_block_off, uint32_t n_blocks,
+                                   uint64_t max_block_bytes, uint64_t* d_out_off, void* d_workspace,
+                                   size_t workspace_bytes, void* stream) {
+  return lz4_plan(d_blocks, d_block_off, n_blocks, max_block_bytes, d_out_off, d_workspace, workspace_bytes, stream, 0);
+}
+
+extern "C" int lsm_lz4_plan_framed(const uint8_t* d_blocks, const uint64_t* d_block_off, uint32_t n_blocks,
+                                   uint64_t max_block_bytes, uint64_t* d_out_off, void* d_workspace,
+                                   size_t workspace_bytes, void* stream) {
+  return lz4_plan(d_blocks, d_block_off, n_blocks, max_block_bytes, d_out_off, d_workspace, workspace_bytes, stream,
+                  kHdrLen);
+}
+
+static int lz4_decompress(const uint8_t* d_blocks, const uint64_t* d_block_off, uint32_t n_blocks, uint8_t* d_out,
+                          const uint64_t* d_out_off, int32_t* d_status, void* d_workspace, size_t workspace_bytes,
+                          void* stream, uint32_t frame) {
   if (n_blocks == 0) return LSM_OK;
   if (!d_blocks || !d_block_off || !d_out || !d_out_off || !d_status || !d_workspace ||
       ((uintptr_t)d_blocks & 15) || workspace_bytes < lsm_lz4_workspace_size(n_blocks))
@@ -323,8 +365,11 @@ extern "C" int lsm_lz4_decompress_blocks(const uint8_t* d_blocks, const uint64_t
   uint32_t* list = count + 4;
   hipError_t e = hipMemsetAsync(count, 0, 4, st);
   if (e != hipSuccess) return hip_status(e, "lsm_lz4_decompress_blocks");
+  if (frame)
+    hipLaunchKernelGGL(lz4_frame_headers_kernel, dim3((n_blocks + 255) / 256), dim3(256), 0, st, d_blocks, d_block_off,
+                       n_blocks, d_out, d_out_off);
   hipLaunchKernelGGL(lz4_small_kernel, dim3((n_blocks + 3) / 4), dim3(256), 0, st, d_blocks, d_block_off, n_blocks,
-                     d_out, d_out_off, d_status);
+                     d_out, d_out_off, d_status, frame);
   hipLaunchKernelGGL(lz4_collect_deferred, dim3((n_blocks + 255) / 256), dim3(256), 0, st, d_status, n_blocks, list,
                      count);
   static uint64_t attr_done = 0;
@@ -332,6 +377,20 @@ extern "C" int lsm_lz4_decompress_blocks(const uint8_t* d_blocks, const uint64_t
     return hip_status(e, "lsm_lz4_decompress_blocks");
   const uint32_t grid = n_blocks < 1024 ? n_blocks : 1024;
   hipLaunchKernelGGL(lz4_large_kernel, dim3(grid), dim3(64), kLargeIn + kLargeOut, st, d_blocks, d_block_off,
-                     n_blocks, d_out, d_out_off, d_status, list, count);
+                     n_blocks, d_out, d_out_off, d_status, list, count, frame);
   return hip_status(hipGetLastError(), "lsm_lz4_decompress_blocks");
+}
+
+extern "C" int lsm_lz4_decompress_blocks(const uint8_t* d_blocks, const uint64_t* d_block_off, uint32_t n_blocks,
+                                         uint8_t* d_out, const uint64_t* d_out_off, int32_t* d_status,
+                                         void* d_workspace, size_t workspace_bytes, void* stream) {
+  return lz4_decompress(d_blocks, d_block_off, n_blocks, d_out, d_out_off, d_status, d_workspace, workspace_bytes,
+                        stream, 0);
+}
+
+extern "C" int lsm_lz4_decompress_framed(const uint8_t* d_blocks, const uint64_t* d_block_off, uint32_t n_blocks,
+                                         uint8_t* d_out, const uint64_t* d_out_off, int32_t* d_status,
+                                         void* d_workspace, size_t workspace_bytes, void* stream) {
+  return lz4_decompress(d_blocks, d_block_off, n_blocks, d_out, d_out_off, d_status, d_workspace, workspace_bytes,
+                        stream, kHdrLen);
 }

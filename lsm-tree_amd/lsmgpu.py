@@ -51,8 +51,14 @@ class LsmDecodeTuning(C.Structure):
                 ("flags", C.c_uint32)]
 
 
-ABI_VERSION = 2
+class LsmTableScan(C.Structure):
+    _fields_ = [("tli_off", C.c_uint64), ("tli_size", C.c_uint32), ("two_level", C.c_uint32),
+                ("global_seqno", C.c_uint64), ("block_count", C.c_uint64)]
+
+
+ABI_VERSION = 3
 DECODE_ITEM_START_VALID = 1
+DECODE_PAYLOAD_VERIFIED = 2
 
 
 class LsmError(RuntimeError):
@@ -136,6 +142,17 @@ def lib():
         L.lsm_lz4_plan_output.restype = C.c_int
         L.lsm_lz4_plan_output.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint64, C.c_void_p, C.c_void_p,
                                           C.c_size_t, C.c_void_p]
+        for fn in (L.lsm_lz4_plan_framed,):
+            fn.restype = C.c_int
+            fn.argtypes = L.lsm_lz4_plan_output.argtypes
+        L.lsm_lz4_decompress_framed.restype = C.c_int
+        L.lsm_lz4_decompress_framed.argtypes = L.lsm_lz4_decompress_blocks.argtypes
+        L.lsm_scan_workspace_size.restype = C.c_size_t
+        L.lsm_scan_workspace_size.argtypes = [C.c_uint32]
+        L.lsm_scan_table.restype = C.c_int
+        L.lsm_scan_table.argtypes = [C.c_void_p, C.c_uint64, C.POINTER(LsmTableScan), C.c_void_p, C.c_uint32,
+                                     C.POINTER(LsmParsed), C.c_uint64, C.c_void_p, C.c_void_p,
+                                     C.POINTER(C.c_uint32), C.POINTER(C.c_int32), C.c_void_p, C.c_size_t, C.c_void_p]
         _lib = L
     return _lib
 
@@ -146,7 +163,8 @@ EXPORTED_SYMBOLS = ["lsm_abi_version", "lsm_status_name", "lsm_last_error", "lsm
                     "lsm_point_read_blocks", "lsm_xxh3_128_file_workspace_size", "lsm_xxh3_128_file",
                     "lsm_bloom_calculate_m", "lsm_bloom_shape", "lsm_bloom_filter_size", "lsm_hash64_keys",
                     "lsm_bloom_build", "lsm_bloom_contains", "lsm_lz4_workspace_size", "lsm_lz4_decompress_blocks",
-                    "lsm_lz4_plan_workspace_size", "lsm_lz4_plan_output", "lsm_seek_blocks"]
+                    "lsm_lz4_plan_workspace_size", "lsm_lz4_plan_output", "lsm_seek_blocks", "lsm_lz4_plan_framed",
+                    "lsm_lz4_decompress_framed", "lsm_scan_workspace_size", "lsm_scan_table"]
 
 
 def _check(rc, what):
@@ -420,6 +438,71 @@ def lz4_decompress_blocks(blocks, block_off, n_blocks=None, max_block_bytes=LZ4_
                                            _ptr(status), _ptr(ws), ws.numel(), _stream(stream)),
            "lsm_lz4_decompress_blocks")
     return out, out_off, status[:n]
+
+
+def decode_lz4_blocks(blocks, block_off, n_blocks=None, expect_type=-1, item_cap=None, fields=None,
+                      max_block_bytes=LZ4_MAX_BLOCK, stream=None):
+    """LZ4 blocks end to end: Block::from_reader(Lz4) then DataBlock::new + iter
+    (block/mod.rs:104-118, data_block/mod.rs:335,476).  lsm_lz4_plan_framed ->
+    lsm_lz4_decompress_framed (frames = Header' || decompressed payload) ->
+    lsm_decode_blocks_tuned(frames, LSM_DECODE_PAYLOAD_VERIFIED).  Returns the decode
+    output dict (payload-relative offsets into each frame's payload) plus "frames",
+    "frame_off" and "status" = the decompress status where it is not OK, else the
+    decode status."""
+    torch = _torch()
+    n = block_off.numel() - 1 if n_blocks is None else n_blocks
+    dev = blocks.device
+    frame_off = torch.zeros(n + 1, dtype=torch.int64, device=dev)
+    if n:
+        pws = torch.empty(lib().lsm_lz4_plan_workspace_size(n), dtype=torch.uint8, device=dev)
+        _check(lib().lsm_lz4_plan_framed(_ptr(blocks), _ptr(block_off), n, max_block_bytes, _ptr(frame_off),
+                                         _ptr(pws), pws.numel(), _stream(stream)), "lsm_lz4_plan_framed")
+    total = int(frame_off[-1].item()) if n else 0
+    frames = padded_bytes(total, dev)
+    zst = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
+    ws = torch.empty(lib().lsm_lz4_workspace_size(n), dtype=torch.uint8, device=dev)
+    _check(lib().lsm_lz4_decompress_framed(_ptr(blocks), _ptr(block_off), n, _ptr(frames), _ptr(frame_off),
+                                           _ptr(zst), _ptr(ws), ws.numel(), _stream(stream)),
+           "lsm_lz4_decompress_framed")
+    if item_cap is None:
+        item_cap = total // 3 + 1
+    d = Decoder(dev)
+    out = d.alloc_outputs(item_cap, n, fields)
+    d.decode(frames, frame_off, n, out, item_cap, expect_type,
+             tuning=(0, 0, 0, DECODE_PAYLOAD_VERIFIED), stream=stream)
+    out["status"] = torch.where(zst[:max(n, 1)] != 0, zst[:max(n, 1)], out["status"])
+    out["frames"], out["frame_off"] = frames, frame_off
+    return out
+
+
+SCAN_STATUS_OK = 0
+
+
+def scan_table(file, file_len, tli_off, tli_size, two_level=False, global_seqno=0, block_count=0, cap_blocks=None,
+               item_cap=None, fields=None, stream=None):
+    """Scanner over a table file image (scanner.rs:24-92): file = padded uint8 cuda tensor.
+    Returns dict: table_status (int), n_blocks (int), block_off (int64 cuda [n+1]),
+    the parsed fields, item_start and status (as decode_blocks)."""
+    torch = _torch()
+    dev = file.device
+    if cap_blocks is None:
+        cap_blocks = max(1, file_len // 33)
+    if item_cap is None:
+        item_cap = file_len // 3 + 1
+    out = Decoder(dev).alloc_outputs(item_cap, cap_blocks, fields)
+    block_off = torch.zeros(cap_blocks + 1, dtype=torch.int64, device=dev)
+    ws = torch.empty(lib().lsm_scan_workspace_size(cap_blocks), dtype=torch.uint8, device=dev)
+    ps = LsmParsed()
+    for f, _ in PARSED_FIELDS:
+        setattr(ps, f, out[f].data_ptr() if f in out else None)
+    t = LsmTableScan(tli_off, tli_size, int(bool(two_level)), global_seqno & (2 ** 64 - 1), block_count)
+    nb, tst = C.c_uint32(), C.c_int32()
+    _check(lib().lsm_scan_table(_ptr(file), file_len, C.byref(t), _ptr(block_off), cap_blocks, C.byref(ps), item_cap,
+                                _ptr(out["item_start"]), _ptr(out["status"]), C.byref(nb), C.byref(tst), _ptr(ws),
+                                ws.numel(), _stream(stream)), "lsm_scan_table")
+    out["table_status"], out["n_blocks"] = int(tst.value), int(nb.value)
+    out["block_off"] = block_off[:nb.value + 1]
+    return out
 
 
 def cut_blocks(key_off, val_off, block_size):

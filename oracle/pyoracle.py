@@ -409,3 +409,98 @@ def decode_materialize_blocks(blocks: np.ndarray, block_off: np.ndarray, nthread
     n = lib().orc_decode_materialize_blocks(_ptr(np.ascontiguousarray(blocks)), _ptr(np.ascontiguousarray(block_off, dtype=np.uint64)),
                                             len(block_off) - 1, nthreads, C.byref(fold))
     return int(n), fold.value
+
+
+# ---- table file image + Scanner ------------------------------------
+
+def table_write(items: Items, block_size=4096, restart_interval=16, hash_ratio=0.0, two_level=False,
+                partition_size=4096):
+    """Data and block-index regions of a table file (test fixture builder; the sfa TOC,
+    meta, filter and trailer sections are not written — the caller gets the TLI handle
+    the TOC would hold, regions.rs:55-76).
+      Writer::write / spill_block (src/table/writer/mod.rs:243-343): items cut by
+        cut_blocks, data blocks back to back from offset 0, each registered as
+        KeyedBlockHandle(last key, last seqno, (file_pos, 33 + data_length));
+      FullIndexWriter::finish (writer/index/full.rs:55-69): one TLI index block of all
+        data-block handles;
+      PartitionedIndexWriter (writer/index/partitioned.rs:54-125,158-235): handles are
+        buffered and a partition index block is cut once the buffered size reaches
+        partition_size (buffered size per handle = end_key length + 48, standing in for
+        size_of::<KeyedBlockHandle>(), which is not pinned; the scan does not depend on
+        where partitions are cut), partitions are concatenated as the "index" region
+        after the data, and the TLI lists the partitions with handles shifted to file
+        offsets (partitioned.rs:136-140).
+    Returns dict(file bytes, tli_off, tli_size, index_off, data_len, block_count,
+    block_off (data blocks), starts)."""
+    starts = cut_blocks(items, block_size)
+    data, off = encode_blocks(items, starts, restart_interval=restart_interval, hash_ratio=hash_ratio)
+    nb = len(starts) - 1
+    last = starts[1:] - 1
+    ko = items.key_off
+
+    def end_key(i):
+        return items.keys[int(ko[i]):int(ko[i + 1])].tobytes()
+
+    handles = [(end_key(int(j)), int(items.seqno[int(j)]), int(off[b]), int(off[b + 1] - off[b]))
+               for b, j in enumerate(last)]
+
+    def index_block(entries):
+        it = Items(np.frombuffer(b"".join(k for k, *_ in entries), np.uint8),
+                   np.concatenate([[0], np.cumsum([len(k) for k, *_ in entries])]).astype(np.uint64),
+                   np.zeros(0, np.uint8), np.zeros(len(entries) + 1, np.uint64),
+                   [s for _, s, _, _ in entries], np.zeros(len(entries), np.uint8),
+                   [o for _, _, o, _ in entries], [z for _, _, _, z in entries])
+        return block_write(index_block_encode(it), block_type=1)
+
+    body = data.tobytes()
+    index_off = len(body)
+    if two_level:
+        parts, buf, size, rel = [], [], 0, 0
+        region = b""
+        for h in handles:
+            buf.append(h)
+            size += len(h[0]) + 48
+            if size >= partition_size:
+                blk = index_block(buf)
+                parts.append((buf[-1][0], buf[-1][1], index_off + rel, len(blk)))
+                region += blk
+                rel += len(blk)
+                buf, size = [], 0
+        if buf:
+            blk = index_block(buf)
+            parts.append((buf[-1][0], buf[-1][1], index_off + rel, len(blk)))
+            region += blk
+        body += region
+        tli = index_block(parts)
+    else:
+        tli = index_block(handles)
+    tli_off = len(body)
+    body += tli
+    return {"file": body, "tli_off": tli_off, "tli_size": len(tli), "index_off": index_off,
+            "data_len": index_off, "block_count": nb, "block_off": off, "starts": starts}
+
+
+def scanner(file: bytes, block_count: int, global_seqno: int = 0):
+    """Scanner::new / next (src/table/scanner.rs:24-92): block_count blocks read back to
+    back from offset 0 with Block::from_reader (header, then data_length payload bytes,
+    xxh3 verify), each must be a Data block (fetch_next_block :54-72), every item's seqno
+    += global_seqno (:84, wrapping as in release builds).  Iteration stops at the first
+    error.  Returns (blocks, status): blocks = list of (offset, size, parsed dict) read
+    before the error; status = 0 or the failing block's status."""
+    pos, out = 0, []
+    buf = np.frombuffer(file, np.uint8)
+    for _ in range(block_count):
+        st, h = header_decode(file[pos:pos + 33])
+        if st:
+            return out, st
+        size = 33 + int(h.data_length)
+        if pos + size > len(file):
+            return out, 8  # Error::Io (UnexpectedEof): TRUNCATED
+        parsed, item_start, status = decode_blocks(buf[pos:pos + size], np.array([0, size], np.uint64),
+                                                   expect_type=0, nthreads=1)
+        if status[0]:
+            return out, int(status[0])
+        parsed["seqno"] = (parsed["seqno"] + np.uint64(global_seqno & (2 ** 64 - 1))).astype(np.uint64)
+        out.append((pos, size, parsed))
+        pos += size
+    return out, 0

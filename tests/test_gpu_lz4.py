@@ -130,3 +130,50 @@ def test_lz4_corrupt_length_cannot_size_the_output(gpu):
     out, out_off, status = gpu.lz4_decompress_blocks(buf, off)
     torch.cuda.synchronize()
     assert status.cpu().tolist()[1] == OK and status.cpu().tolist()[0] != OK and int(out_off[1]) == 0
+
+
+def test_lz4_chained_parse(gpu):
+    """LZ4 -> parse chaining: Block::from_reader(Lz4) then DataBlock::new + iter
+    (block/mod.rs:104-118, data_block/mod.rs:335,476) on the device:
+    lsm_lz4_plan_framed -> lsm_lz4_decompress_framed -> lsm_decode_blocks_tuned with
+    LSM_DECODE_PAYLOAD_VERIFIED.  Every parsed field must equal the oracle's decode of the
+    uncompressed payload; corrupt stored bytes keep their checksum status, a malformed
+    stream its DECOMPRESS status, a bad type its TYPE_MISMATCH."""
+    import torch
+    from helpers import FIELD_VIEW, prefix_items
+    raws = []
+    for n_items, kind, ri in [(52, "counter", 16), (52, "random", 1), (205, "counter", 16), (820, "counter", 16),
+                              (820, "random", 4), (1300, "counter", 16)]:
+        raws.append(_payloads(n_items, ri, kind, n_items))
+    raws += [pyoracle.data_block_encode(prefix_items(56, seed=s)) for s in range(8)]
+    raws += [_payloads(52, 16, "counter", 100 + s) for s in range(40)]
+    blocks = [_frame(lz4_compress(r), len(r)) for r in raws]
+    # corruptions: stored-byte flip (CKSUM), malformed stream (DECOMPRESS), index type (TYPE_MISMATCH)
+    bad_ck = bytearray(blocks[3]); bad_ck[40] ^= 1; blocks[3] = bytes(bad_ck)
+    blocks[7] = _frame(b"\xf0", len(raws[7]))
+    blocks[9] = _frame(lz4_compress(raws[9]), len(raws[9]), block_type=1)
+    off = np.zeros(len(blocks) + 1, np.int64)
+    off[1:] = np.cumsum([len(b) for b in blocks])
+    buf = gpu.to_device_bytes(np.frombuffer(b"".join(blocks), np.uint8))
+    out = gpu.decode_lz4_blocks(buf, torch.from_numpy(off).cuda(), expect_type=0)
+    torch.cuda.synchronize()
+    st = out["status"].cpu().numpy()[:len(blocks)]
+    want = [OK] * len(blocks)
+    want[3], want[7], want[9] = CKSUM, DECOMPRESS, 7
+    assert st.tolist() == want
+    starts = out["item_start"].cpu().numpy().view(np.uint32)
+    frames = out["frames"].cpu().numpy()
+    foff = out["frame_off"].cpu().numpy()
+    for b, r in enumerate(raws):
+        if want[b] != OK:
+            continue
+        assert frames[foff[b] + 33:foff[b + 1]].tobytes() == r
+        n, parsed = pyoracle.data_block_decode(r)
+        lo, hi = int(starts[b]), int(starts[b + 1])
+        assert hi - lo == n
+        for f, dt in FIELD_VIEW.items():
+            if f != "handle_off":
+                assert (out[f].cpu().numpy().view(dt)[lo:hi] == parsed[f].astype(dt)).all(), (b, f)
+    # the frame header is a well-formed uncompressed-size header of the stored checksum
+    st0, h = pyoracle.header_decode(frames[foff[0]:foff[0] + 33].tobytes())
+    assert st0 == 0 and h.data_length == len(raws[0]) == h.uncompressed_length

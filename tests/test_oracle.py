@@ -235,3 +235,31 @@ def test_oracle_asan():
         r = subprocess.run([str(oracle_dir / "fuzz_asan"), seed, "1500"], capture_output=True, text=True, timeout=300)
         assert r.returncode == 0, r.stderr[-4000:]
         assert "fuzz_driver ok" in r.stdout
+
+
+def test_table_write_and_scanner(oracle):
+    """pyoracle.table_write + scanner (Scanner, src/table/scanner.rs:24-92): the block
+    index (full and two-level) lists exactly the data blocks, and the scanned items
+    are the written items with global_seqno added."""
+    from helpers import counter_items
+    items = counter_items(52 * 30, seed=2)
+    for two_level in (False, True):
+        t = oracle.table_write(items, two_level=two_level, partition_size=600)
+        tli = t["file"][t["tli_off"]:t["tli_off"] + t["tli_size"]]
+        assert oracle.block_verify(tli)[0] == 0
+        n, parsed = oracle.data_block_decode(tli[33:], index=True)
+        handles = list(zip(parsed["handle_off"].tolist(), parsed["val_len"].tolist()))
+        if two_level:
+            assert n > 1 and handles[0][0] == t["index_off"]
+            data_handles = []
+            for o, sz in handles:
+                m, p = oracle.data_block_decode(t["file"][o + 33:o + sz], index=True)
+                data_handles += list(zip(p["handle_off"].tolist(), p["val_len"].tolist()))
+            handles = data_handles
+        assert [o for o, _ in handles] == t["block_off"][:-1].tolist()
+        assert [o + s for o, s in handles] == t["block_off"][1:].tolist()
+        blocks, err = oracle.scanner(t["file"], t["block_count"], 2 ** 64 - 1)
+        assert err == 0 and len(blocks) == t["block_count"]
+        seq = np.concatenate([b[2]["seqno"] for b in blocks])
+        assert (seq == items.seqno - np.uint64(1)).all()  # + (2^64 - 1) wraps
+        assert sum(len(b[2]["seqno"]) for b in blocks) == items.n
