@@ -29,6 +29,7 @@
  *   lsm_lz4_plan_output <- the builder_unzeroed(uncompressed_length) sizing of the same  block/mod.rs:104-112
  *   lsm_lz4_plan_framed / lsm_lz4_decompress_framed + lsm_decode_blocks_tuned(LSM_DECODE_PAYLOAD_VERIFIED)
  *                      <- Block::from_reader(Lz4) then DataBlock::new + iter   block/mod.rs:104-118, data_block/mod.rs:335,476
+ *   lsm_materialize_plan / lsm_materialize_keys <- DataBlockParsedItem::materialize  data_block/mod.rs:296-315
  *   lsm_scan_table     <- Scanner::new / next      src/table/scanner.rs:24-92 (block handles from the
  *                         block index: FullBlockIndex / TwoLevelBlockIndex, src/table/block_index/,
  *                         regions from the TOC, src/table/regions.rs:55-76)
@@ -332,6 +333,27 @@ int lsm_lz4_plan_framed(const uint8_t* d_blocks, const uint64_t* d_block_off, ui
 int lsm_lz4_decompress_framed(const uint8_t* d_blocks, const uint64_t* d_block_off, uint32_t n_blocks,
                               uint8_t* d_out, const uint64_t* d_out_off, int32_t* d_status,
                               void* d_workspace, size_t workspace_bytes, void* stream);
+
+/* ---- materialize (DataBlockParsedItem::materialize, data_block/mod.rs:296-315) --
+ * Owned keys of decoded items: key = Slice::fused(prefix, suffix) =
+ * payload[head.key_off .. + prefix_len] || payload[key_off .. + key_len], head =
+ * the item's restart head (item - item % restart_interval within its block).
+ * Values stay payload sub-slices (val_off, val_len), as in the reference.  Inputs
+ * are lsm_decode_blocks' outputs (key_off, key_len, prefix_len required) over the
+ * same blocks; n_items = d_item_start[n_blocks].  Items of blocks whose
+ * d_status is not LSM_OK get empty keys.
+ * lsm_materialize_plan: d_key_out_off (n_items+1 u64) = exclusive prefix sum of
+ * the key lengths (workspace: lsm_materialize_workspace_size(n_items) bytes);
+ * the caller sizes d_key_out from d_key_out_off[n_items], then
+ * lsm_materialize_keys writes key i to d_key_out[d_key_out_off[i] .. [i+1]). */
+size_t lsm_materialize_workspace_size(uint64_t n_items);
+int lsm_materialize_plan(const uint8_t* d_blocks, const uint64_t* d_block_off, uint32_t n_blocks,
+                         const uint32_t* d_item_start, const int32_t* d_status, const lsm_parsed_items* d_parsed,
+                         uint64_t n_items, uint64_t* d_key_out_off, void* d_workspace, size_t workspace_bytes,
+                         void* stream);
+int lsm_materialize_keys(const uint8_t* d_blocks, const uint64_t* d_block_off, uint32_t n_blocks,
+                         const uint32_t* d_item_start, const int32_t* d_status, const lsm_parsed_items* d_parsed,
+                         uint64_t n_items, const uint64_t* d_key_out_off, uint8_t* d_key_out, void* stream);
 
 /* ---- whole-table scan (Scanner, src/table/scanner.rs:24-92) -----------------
  * Decodes every data block of one table file image d_file[0 .. file_len) (16-byte

@@ -153,6 +153,15 @@ def lib():
         L.lsm_scan_table.argtypes = [C.c_void_p, C.c_uint64, C.POINTER(LsmTableScan), C.c_void_p, C.c_uint32,
                                      C.POINTER(LsmParsed), C.c_uint64, C.c_void_p, C.c_void_p,
                                      C.POINTER(C.c_uint32), C.POINTER(C.c_int32), C.c_void_p, C.c_size_t, C.c_void_p]
+        L.lsm_materialize_workspace_size.restype = C.c_size_t
+        L.lsm_materialize_workspace_size.argtypes = [C.c_uint64]
+        L.lsm_materialize_plan.restype = C.c_int
+        L.lsm_materialize_plan.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p,
+                                           C.POINTER(LsmParsed), C.c_uint64, C.c_void_p, C.c_void_p, C.c_size_t,
+                                           C.c_void_p]
+        L.lsm_materialize_keys.restype = C.c_int
+        L.lsm_materialize_keys.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p,
+                                           C.POINTER(LsmParsed), C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p]
         _lib = L
     return _lib
 
@@ -164,7 +173,8 @@ EXPORTED_SYMBOLS = ["lsm_abi_version", "lsm_status_name", "lsm_last_error", "lsm
                     "lsm_bloom_calculate_m", "lsm_bloom_shape", "lsm_bloom_filter_size", "lsm_hash64_keys",
                     "lsm_bloom_build", "lsm_bloom_contains", "lsm_lz4_workspace_size", "lsm_lz4_decompress_blocks",
                     "lsm_lz4_plan_workspace_size", "lsm_lz4_plan_output", "lsm_seek_blocks", "lsm_lz4_plan_framed",
-                    "lsm_lz4_decompress_framed", "lsm_scan_workspace_size", "lsm_scan_table"]
+                    "lsm_lz4_decompress_framed", "lsm_scan_workspace_size", "lsm_scan_table",
+                    "lsm_materialize_workspace_size", "lsm_materialize_plan", "lsm_materialize_keys"]
 
 
 def _check(rc, what):
@@ -475,7 +485,26 @@ def decode_lz4_blocks(blocks, block_off, n_blocks=None, expect_type=-1, item_cap
     return out
 
 
-SCAN_STATUS_OK = 0
+def materialize_keys(blocks, block_off, n_blocks, out, n_items=None, stream=None):
+    """DataBlockParsedItem::materialize (data_block/mod.rs:296-315) of decode output `out`
+    (dict from decode_blocks / scan_table) -> (keys uint8 cuda arena, key_off int64 cuda
+    [n_items+1]); values stay (val_off, val_len) sub-slices of each payload."""
+    torch = _torch()
+    dev = blocks.device
+    if n_items is None:
+        n_items = int(out["item_start"][n_blocks].item())
+    key_off = torch.zeros(n_items + 1, dtype=torch.int64, device=dev)
+    ps = LsmParsed()
+    for f, _ in PARSED_FIELDS:
+        setattr(ps, f, out[f].data_ptr() if f in out else None)
+    ws = torch.empty(lib().lsm_materialize_workspace_size(n_items), dtype=torch.uint8, device=dev)
+    args = (_ptr(blocks), _ptr(block_off), n_blocks, _ptr(out["item_start"]), _ptr(out["status"]), C.byref(ps), n_items)
+    _check(lib().lsm_materialize_plan(*args, _ptr(key_off), _ptr(ws), ws.numel(), _stream(stream)),
+           "lsm_materialize_plan")
+    total = int(key_off[-1].item()) if n_items else 0
+    keys = padded_bytes(total, dev)
+    _check(lib().lsm_materialize_keys(*args, _ptr(key_off), _ptr(keys), _stream(stream)), "lsm_materialize_keys")
+    return keys, key_off
 
 
 def scan_table(file, file_len, tli_off, tli_size, two_level=False, global_seqno=0, block_count=0, cap_blocks=None,
