@@ -29,7 +29,8 @@ scaling, no data-path collective).
 Also in the same JSON line (not `value`): per-kernel rooflines (decode, encode)
 with the measured copy / LDS-DMA read ceilings, configs[3] (prefix-heavy 16 KiB),
 configs[4] (8 GiB mixed 4/16/64 KiB data + index blocks byte-split across ranks),
-point reads, range seeks, whole-file checksum, Bloom filter, LZ4, the
+point reads, range seeks, whole-file checksum, Bloom filter, LZ4 (and the
+LZ4 -> parse chain), device materialize, a whole-table scan, the
 host-inclusive rates (decode from an mmap'd file, encode from a host write
 buffer) and the CPU baseline (oracle port on the host cores, 1 thread and all).
 """
@@ -542,10 +543,110 @@ def bench_lz4(torch, lsmgpu, enc, n_blocks, reps=5, sample=131072):
     e1.record()
     torch.cuda.synchronize()
     ms = e0.elapsed_time(e1) / reps
+    # LZ4 -> parse chain (Block::from_reader(Lz4) + DataBlock::iter): every field vs the plain decode
+    ch = lsmgpu.decode_lz4_blocks(dbuf, doff, expect_type=0, item_cap=nb * 52, fields=DATA_FIELDS)
+    torch.cuda.synchronize()
+    assert int((ch["status"][:nb] != 0).sum().item()) == 0, "lz4 chain: status"
+    ref = lsmgpu.decode_blocks(enc["buf"], enc["block_off"][:nb + 1], nb, item_cap=nb * 52, fields=DATA_FIELDS)
+    torch.cuda.synchronize()
+    for f in DATA_FIELDS:
+        assert torch.equal(ch[f][:nb * 52], ref[f][:nb * 52]), f"lz4 chain: {f}"
+    del ch, ref
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        lsmgpu.decode_lz4_blocks(dbuf, doff, expect_type=0, item_cap=nb * 52, fields=DATA_FIELDS)
+    torch.cuda.synchronize()
+    ms_chain = (time.perf_counter() - t0) * 1e3 / reps
     return {"blocks": nb, "stored_bytes": int(loff[-1]), "raw_bytes": raw_total, "ms": round(ms, 4),
             "GiB_per_s_raw": round(raw_total / (ms * 1e-3) / 2 ** 30, 1),
             "note": "plan (verified headers -> output offsets) + header / xxh3_128 verify + LZ4 decode, every "
-                    "decompressed byte checked"}
+                    "decompressed byte checked",
+            "chain_ms": round(ms_chain, 4), "chain_GiB_per_s_raw": round(raw_total / (ms_chain * 1e-3) / 2 ** 30, 1),
+            "chain_note": "decode_lz4_blocks: plan_framed (host sync for the arena size) + decompress_framed + "
+                          "decode with LSM_DECODE_PAYLOAD_VERIFIED, host-timed; every parsed field equal to the "
+                          "plain decode of the uncompressed blocks"}
+
+
+def bench_table_scan(torch, lsmgpu, items, enc, nb, n_items, ref_out, reps=3, partition=100):
+    """Scanner over one table whose data region is the whole configs[1] batch
+    (scanner.rs:24-92): a two-level block index is written on the
+    device with lsm_encode_blocks(block_type = Index) (KeyedBlockHandle(last key,
+    seqno, (offset, size)) per data block, partitions of `partition` handles, a TLI
+    of partition handles, writer/index/partitioned.rs), appended after the data;
+    lsm_scan_table then decodes TLI -> partitions -> every data block
+    (global_seqno 1000 added).  Checked: block offsets, statuses and every item's
+    fields equal the plain decode's (seqno + 1000)."""
+    dev = enc["buf"].device
+    data_len = int(enc["block_off"][nb].item())
+    boff = enc["block_off"][:nb + 1]
+    last = (torch.arange(1, nb + 1, device=dev, dtype=torch.int64) * 52 - 1)
+    kl = 16
+
+    def index_blocks(end_items_key, seq, h_off, h_size, per_block, base):
+        n = h_off.numel()
+        nblk = (n + per_block - 1) // per_block
+        it = {"keys": end_items_key, "key_off": torch.arange(n + 1, device=dev, dtype=torch.int64) * kl,
+              "seqno": seq, "handle_off": h_off, "handle_size": h_size.to(torch.int32)}
+        st = torch.clamp(torch.arange(nblk + 1, device=dev, dtype=torch.int64) * per_block, max=n).to(torch.int32)
+        out = lsmgpu.Encoder(dev).encode(it, st, nblk, block_type=lsmgpu.BLOCK_INDEX)
+        torch.cuda.synchronize()
+        assert int((out["status"][:nblk] != 0).sum().item()) == 0
+        ln = int(out["block_off"][nblk].item())
+        return out["buf"][:ln], out["block_off"][:nblk + 1] + base, nblk
+
+    ekeys = items["keys"][:n_items * kl].view(n_items, kl)[last].reshape(-1)
+    ekeys = torch.cat([ekeys, torch.zeros(64, dtype=torch.uint8, device=dev)])
+    seq = items["seqno"][last]
+    parts, poff, npart = index_blocks(ekeys, seq, boff[:nb], (boff[1:] - boff[:nb]), partition, data_len)
+    plast = torch.clamp(torch.arange(1, npart + 1, device=dev) * partition, max=nb) - 1
+    pkeys = torch.cat([ekeys[:nb * kl].view(nb, kl)[plast].reshape(-1), torch.zeros(64, dtype=torch.uint8, device=dev)])
+    tli, toff, _ = index_blocks(pkeys, seq[plast], poff[:npart], poff[1:] - poff[:npart], 1 << 20,
+                                data_len + parts.numel())
+    file_len = data_len + parts.numel() + tli.numel()
+    f = lsmgpu.padded_bytes(file_len, dev)
+    f[:data_len].copy_(enc["buf"][:data_len])
+    f[data_len:data_len + parts.numel()].copy_(parts)
+    f[data_len + parts.numel():file_len].copy_(tli)
+    tli_off = data_len + parts.numel()
+    kw = dict(two_level=True, global_seqno=1000, block_count=nb, cap_blocks=nb + 16, item_cap=n_items,
+              fields=DATA_FIELDS)
+    out = lsmgpu.scan_table(f, file_len, tli_off, tli.numel(), **kw)
+    torch.cuda.synchronize()
+    assert out["table_status"] == 0 and out["n_blocks"] == nb, (out["table_status"], out["n_blocks"])
+    assert torch.equal(out["block_off"], boff)
+    assert int((out["status"][:nb] != 0).sum().item()) == 0
+    assert torch.equal(out["seqno"][:n_items], ref_out["seqno"][:n_items] + 1000)
+    for fld in DATA_FIELDS[1:]:
+        assert torch.equal(out[fld][:n_items], ref_out[fld][:n_items]), fld
+    del out
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        lsmgpu.scan_table(f, file_len, tli_off, tli.numel(), **kw)
+    torch.cuda.synchronize()
+    ms = (time.perf_counter() - t0) * 1e3 / reps
+    return {"data_blocks": nb, "index_partitions": npart, "tli_bytes": int(tli.numel()), "file_bytes": file_len,
+            "ms": round(ms, 4), "GiB_per_s": round(file_len / (ms * 1e-3) / 2 ** 30, 1),
+            "note": "host-timed lsm_scan_table call (2 index levels, one stream sync each, then the data decode); "
+                    "every item equal to the plain decode with global_seqno 1000 added"}
+
+
+def bench_materialize(torch, lsmgpu, enc, nb, out, n_items, reps=5):
+    """DataBlockParsedItem::materialize on the device (data_block/mod.rs:296-315) for
+    every item of the configs[1] decode: keys = restart-head prefix || suffix; checked
+    against the encoder's input keys."""
+    keys, key_off = lsmgpu.materialize_keys(enc["buf"], enc["block_off"], nb, out, n_items)
+    torch.cuda.synchronize()
+    total = int(key_off[n_items].item())
+    a, b = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    a.record()
+    for _ in range(reps):
+        lsmgpu.materialize_keys(enc["buf"], enc["block_off"], nb, out, n_items)
+    b.record()
+    torch.cuda.synchronize()
+    ms = a.elapsed_time(b) / reps
+    return keys[:total], {"items": n_items, "key_bytes": total, "ms": round(ms, 4),
+                          "GiB_per_s_keys": round(total / (ms * 1e-3) / 2 ** 30, 1),
+                          "note": "plan (lengths + scan) + copy, host-synchronised once for the arena size"}
 
 
 # ----------------------------------------------------------- host-inclusive
@@ -890,7 +991,7 @@ def main():
     r_dec = roofline_entry("decode_blocks_kernel (item_start precomputed)", dec_alg, kdec_ms, ceil,
                            "decode_blocks_kernel", nb)
     r_dec["read_only_frac"] = round(total_bytes / (kdec_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
-    r_enc = roofline_entry("lsm_encode_blocks (encode_sizes_kernel + scan + encode_write_kernel)", enc_alg, enc_ms,
+    r_enc = roofline_entry("lsm_encode_blocks (encode_plan_kernel + scan + encode_group_kernel)", enc_alg, enc_ms,
                            ceil, "lsm_encode_blocks", nb)
     dominant = r_enc if enc_ms >= kdec_ms else r_dec
 
@@ -901,6 +1002,12 @@ def main():
         extra["bloom"] = bench_bloom(torch, lsmgpu, items, n_items)
         if rank == 0:
             extra["lz4"] = bench_lz4(torch, lsmgpu, enc, nb)
+        mkeys, extra["materialize"] = bench_materialize(torch, lsmgpu, enc, nb, out, n_items)
+        assert torch.equal(mkeys, items["keys"][:n_items * 16]), "materialize: keys differ from the encoder input"
+        del mkeys
+        if rank == 0 and world == 1:
+            extra["table_scan"] = bench_table_scan(torch, lsmgpu, items, enc, nb, n_items, out)
+            torch.cuda.empty_cache()
     hostinc = {}
     if rank == 0 and world == 1 and not args.no_host and ref_buf is not None:
         hostinc["decode_from_mmap"] = host_inclusive_decode(torch, lsmgpu, enc, nb)

@@ -24,7 +24,7 @@ VARIANTS = [("full", 0), ("no-parse", 0x200), ("stage-only", 0x700), ("no-hash",
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--blocks", type=int, default=1 << 18)
-    ap.add_argument("--tuning", default="0,32768,512")
+    ap.add_argument("--tuning", default="0,0,0", help="blocks_per_wave,stage_bytes,tile_items (0 = default)")
     ap.add_argument("--reps", type=int, default=2)
     ap.add_argument("--variants", default=",".join(v for v, _ in VARIANTS))
     args = ap.parse_args()
@@ -37,12 +37,12 @@ def main():
     dec.decode(enc["buf"], enc["block_off"], nb, out, n_items)
     torch.cuda.synchronize()
     v = [int(x, 0) for x in args.tuning.split(",")]
-    v = v + [0] * (8 - len(v))
-    base, xf, rest = tuple(v[:3]), v[3], tuple(v[4:8])
+    v = v + [0] * (4 - len(v))
+    base, xf = tuple(v[:3]), v[3]
     chosen = [(v, f) for v, f in VARIANTS if v in args.variants.split(",")]
     for _ in range(args.reps):
         for name, fl in chosen:
-            dec.decode(enc["buf"], enc["block_off"], nb, out, n_items, tuning=base + (1 | xf | fl,) + rest)
+            dec.decode(enc["buf"], enc["block_off"], nb, out, n_items, tuning=base + (1 | xf | fl,))
     torch.cuda.synchronize()
     print("variants:", [v for v, _ in chosen], "reps", args.reps, "blocks", nb, "bytes",
           int(enc["block_off"][nb].item()), "items", n_items)

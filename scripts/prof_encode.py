@@ -85,8 +85,10 @@ def main():
             torch.cuda.synchronize()
             lsmgpu.LsmBlockParams = orig
             print(f"  ablate {name:20s} {e0.elapsed_time(e1) / args.reps:.3f} ms", flush=True)
+    key_val = int(items["key_off"][n_items].item()) + int(items["val_off"][n_items].item())
+    alg = key_val + n_items * bench.ENC_IN_PER_ITEM + 4 * (nb + 1) + total + 8 * (nb + 1) + 4 * nb
     print(f"encode {args.workload}: {nb} blocks {n_items} items {total} bytes  {ms:.3f} ms  "
-          f"{total / ms / 1e6:.1f} GB/s written", flush=True)
+          f"{total / ms / 1e6:.1f} GB/s written  alg_bytes {alg}", flush=True)
 
 
 if __name__ == "__main__":

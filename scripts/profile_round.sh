@@ -15,10 +15,15 @@ timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -
   python3 scripts/prof_decode.py --variants full --reps 4 --blocks $NB > $OUT/fetch.log 2>&1
 timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/write -o pmc -- \
   python3 scripts/prof_decode.py --variants full --reps 4 --blocks $NB > $OUT/write.log 2>&1
+timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/efetch -o pmc -- \
+  python3 scripts/prof_encode.py --reps 4 --blocks $NB > $OUT/efetch.log 2>&1
+timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE --output-format csv -d $OUT/ewrite -o pmc -- \
+  python3 scripts/prof_encode.py --reps 4 --blocks $NB > $OUT/ewrite.log 2>&1
 line=$(grep "^variants:" $OUT/fetch.log)
 BYTES=$(echo "$line" | sed 's/.* bytes \([0-9]*\) items.*/\1/')
 ITEMS=$(echo "$line" | sed 's/.* items \([0-9]*\).*/\1/')
-python3 scripts/traffic_summary.py $OUT/fetch $OUT/write $NB $BYTES $ITEMS > $OUT/traffic.json
+EALG=$(grep "alg_bytes" $OUT/efetch.log | sed 's/.*alg_bytes \([0-9]*\).*/\1/')
+python3 scripts/traffic_summary.py $OUT/fetch $OUT/write $NB $BYTES $ITEMS $OUT/efetch $OUT/ewrite $EALG > $OUT/traffic.json
 cat $OUT/traffic.json
 find $OUT/kt -name "*kernel_stats.csv" -exec cp {} $OUT/kernel_stats.csv \;
 head -20 $OUT/kernel_stats.csv
