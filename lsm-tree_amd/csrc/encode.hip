@@ -255,6 +255,57 @@ struct ItemMeta {
   uint32_t e;  // E2 only: the plan's erec word
 };
 
+// An item's fields exactly as loaded (E2's one-group-ahead prefetch).
+struct RawItem {
+  uint64_t ko, ko1, vo, vo1, seq;
+  uint32_t vt, e;
+};
+
+// Plain loads of item i's fields (no arithmetic, so no wait is forced here).
+template <bool kIndex>
+__device__ __forceinline__ RawItem load_raw(const EncodeParams& P, uint64_t i) {
+  RawItem r;
+  r.ko = P.it.key_off[i];
+  r.ko1 = P.it.key_off[i + 1];
+  r.seq = P.it.seqno[i];
+  r.e = 0;
+  if (kIndex) {
+    r.vo = P.it.handle_off[i];
+    r.vo1 = P.it.handle_size[i];
+    r.vt = 0;
+  } else {
+    r.vo = P.it.val_off[i];
+    r.vo1 = P.it.val_off[i + 1];
+    r.vt = P.it.vtype[i];
+  }
+  return r;
+}
+
+// Derived fields of a raw item and the writer's argument checks (key length
+// <= u16, a known value type, value length <= u32).
+template <bool kIndex>
+__device__ __forceinline__ ItemMeta cook_item(const RawItem& r, bool& bad) {
+  ItemMeta m;
+  const uint64_t kl = r.ko1 - r.ko;
+  if (kl > 0xFFFF) bad = true;
+  m.ko = r.ko;
+  m.klen = (uint32_t)min(kl, (uint64_t)0xFFFF);
+  m.seq = r.seq;
+  m.vo = r.vo;
+  m.vt = r.vt;
+  m.sh = 0;
+  m.e = r.e;
+  if (kIndex) {
+    m.vl = (uint32_t)r.vo1;
+  } else {
+    const uint64_t vl = r.vo1 - r.vo;
+    if (!valid_vtype(m.vt)) bad = true;
+    if (!is_tombstone(m.vt) && vl > 0xFFFFFFFFULL) bad = true;
+    m.vl = (uint32_t)vl;
+  }
+  return m;
+}
+
 __device__ __forceinline__ ItemMeta load_item(const EncodeParams& P, uint64_t i, bool& bad) {
   ItemMeta m;
   m.ko = P.it.key_off[i];
@@ -540,22 +591,68 @@ __device__ __host__ __forceinline__ bool group_fits(uint64_t n, uint64_t kspan, 
 }
 
 // ---------------------------------------------------------------- E1: plan
-// Flat over items: a 256-thread workgroup owns kPlanBlocks consecutive blocks
-// and walks their items (contiguous) with one thread per item, so every load
-// is coalesced and all of a workgroup's items are in flight together.  Per
-// item: key / value lengths, the shared prefix with its restart head
-// (encoder.rs:140-143, util.rs:125-130, head key read from L1/L2), the record
-// length and (workgroup scan, in item order) the record's offset in its
-// block, kept for E2 in erec.  Per block: size, binary-index step,
-// hash-index size, size class, and the key / value span starts E2 stages.
+// A 256-thread workgroup owns kPlanBlocks consecutive blocks and walks their
+// items (contiguous) in chunks of 1024, four consecutive items per thread, so
+// each wave has four items' loads in flight at once.  Per chunk:
+//   1. item fields (key / value offsets, seqno, type); key offsets to LDS;
+//   2. the shared prefix with the restart head (encoder.rs:140-143,
+//      util.rs:125-130): the head's key offset from LDS (global only for a
+//      head before the chunk), both keys' first 16 bytes as two aligned 16-B
+//      loads each, all four items' loads issued together (longer equal
+//      prefixes continue in lcp_global);
+//   3. record lengths, a workgroup scan in item order -> each record's offset
+//      in its block, kept for E2 in erec.
+// Per block: size, binary-index step, hash-index size, size class, and the
+// key / value span starts E2 stages.
 constexpr uint32_t kPlanBlocks = 16;
+#ifndef LSM_PLAN_PER
+#define LSM_PLAN_PER 2
+#endif
+constexpr uint32_t kPlanPer = LSM_PLAN_PER;          // consecutive items per thread
+constexpr uint32_t kPlanChunk = 256 * kPlanPer;      // items per chunk
 
+// 16 bytes at p (global, any alignment): two aligned 16-B loads and a funnel
+// shift (reads up to 31 bytes past p; the arenas are padded).
+__device__ __forceinline__ Win16 gwin16(const uint8_t* p) {
+  const uint64_t a = (uint64_t)(uintptr_t)p;
+  const u32x4* w = reinterpret_cast<const u32x4*>(a & ~15ULL);
+  const u32x4 x = w[0], y = w[1];
+  uint64_t w0 = (uint64_t)x.x | ((uint64_t)x.y << 32), w1 = (uint64_t)x.z | ((uint64_t)x.w << 32);
+  uint64_t w2 = (uint64_t)y.x | ((uint64_t)y.y << 32);
+  const uint64_t w3 = (uint64_t)y.z | ((uint64_t)y.w << 32);
+  const uint32_t s = (uint32_t)(a & 15);
+  if (s & 8) {
+    w0 = w1;
+    w1 = w2;
+    w2 = w3;
+  }
+  const uint32_t sh = (s & 7) * 8;
+  Win16 r;
+  r.lo = sh ? (w0 >> sh) | (w1 << (64 - sh)) : w0;
+  r.hi = sh ? (w1 >> sh) | (w2 << (64 - sh)) : w1;
+  return r;
+}
+
+// Shared prefix past an equal first 16 bytes: 16 bytes per step (rare: long
+// common key prefixes; kept narrow so the common path's registers stay low).
+__device__ __noinline__ uint32_t lcp_tail(const uint8_t* keys, uint64_t a, uint64_t b, uint32_t n) {
+  for (uint32_t k = 16; k < n; k += 16) {
+    const Win16 wa = gwin16(keys + a + k), wb = gwin16(keys + b + k);
+    const uint64_t x0 = wa.lo ^ wb.lo, x1 = wa.hi ^ wb.hi;
+    if (x0) return min(n, k + (uint32_t)(__builtin_ctzll(x0) >> 3));
+    if (x1) return min(n, k + 8 + (uint32_t)(__builtin_ctzll(x1) >> 3));
+  }
+  return n;
+}
+
+template <bool kIndex>
 __global__ __launch_bounds__(256) void encode_plan_kernel(EncodeParams P) {
   __shared__ uint32_t bst[kPlanBlocks + 1];
   __shared__ unsigned long long bfirst[kPlanBlocks], bend[kPlanBlocks], lhead[kPlanBlocks];
   __shared__ unsigned long long psum[4];
   __shared__ uint32_t badf[kPlanBlocks];
   __shared__ uint32_t mono;
+  __shared__ unsigned long long kos[kPlanChunk + 1];  // key offsets of the chunk's items (+ the next)
   const uint32_t tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
   const uint32_t b0 = blockIdx.x * kPlanBlocks;
   const uint32_t nb = min(kPlanBlocks, P.n_blocks - b0);
@@ -568,34 +665,91 @@ __global__ __launch_bounds__(256) void encode_plan_kernel(EncodeParams P) {
   __syncthreads();
   if (tid < nb && bst[tid + 1] < bst[tid]) mono = 0;  // (benign race: every writer stores 0)
   __syncthreads();
-  const uint32_t ri = is_index(P) ? 1 : P.ri;
+  const uint32_t ri = kIndex ? 1 : P.ri;
+  constexpr bool index = kIndex;
   // a non-monotone item_start run is a caller error: its blocks are rejected below
   const uint64_t i_begin = bst[0], i_end = mono ? bst[nb] : bst[0];
   uint64_t carry = 0;
-  for (uint64_t base = i_begin; base < i_end; base += 256) {
-    const uint64_t i = base + tid;
-    const bool live = i < i_end;
-    uint32_t j = 0, n = 0, jj = 0, ridx = 0;
-    uint64_t rec = 0;
-    ItemMeta m{};
-    if (live) {
-      uint32_t lo = 0, hi = nb;  // block j: bst[j] <= i < bst[j + 1]
+  for (uint64_t base = i_begin; base < i_end; base += kPlanChunk) {
+    const uint64_t i0 = base + kPlanPer * tid;
+    // ---- 1. item fields, block of each item
+    RawItem raw[kPlanPer];
+#pragma unroll
+    for (uint32_t q = 0; q < kPlanPer; ++q) raw[q] = load_raw<kIndex>(P, min(i0 + q, i_end - 1));
+    ItemMeta m[kPlanPer];
+    uint32_t jq[kPlanPer], jjq[kPlanPer];
+    uint32_t j = 0;
+    if (i0 < i_end) {
+      uint32_t lo = 0, hi = nb;  // block j: bst[j] <= i0 < bst[j + 1]
       while (hi - lo > 1) {
         const uint32_t mid = (lo + hi) >> 1;
-        if (bst[mid] <= i) lo = mid;
+        if (bst[mid] <= i0) lo = mid;
         else hi = mid;
       }
       j = lo;
-      const uint32_t s = bst[j];
-      n = bst[j + 1] - s;
-      jj = (uint32_t)(i - s);
-      ridx = jj / ri;
-      bool bad = false;
-      m = load_item_lcp(P, s, jj, ri, bad);
-      rec = item_record_len(P, m, jj == ridx * ri);
-      if (bad) atomicOr(&badf[j], 1u);
     }
-    const uint64_t incl = wave_incl_scan_u64(rec);
+#pragma unroll
+    for (uint32_t q = 0; q < kPlanPer; ++q) {
+      const uint64_t i = i0 + q;
+      jq[q] = jjq[q] = 0;
+      if (i < i_end) {
+        while (j + 1 < nb && bst[j + 1] <= i) ++j;
+        jq[q] = j;
+        jjq[q] = (uint32_t)(i - bst[j]);
+      }
+    }
+#pragma unroll
+    for (uint32_t q = 0; q < kPlanPer; ++q) {
+      bool bad = false;
+      m[q] = cook_item<kIndex>(raw[q], bad);
+      if (i0 + q < i_end) {
+        if (bad) atomicOr(&badf[jq[q]], 1u);
+        kos[kPlanPer * tid + q] = m[q].ko;
+      }
+    }
+    __syncthreads();
+    // ---- 2. shared prefix with the restart head
+    if (!index) {
+      Win16 wa[kPlanPer], wb[kPlanPer];
+      uint32_t nq[kPlanPer];
+      uint64_t hq[kPlanPer];
+#pragma unroll
+      for (uint32_t q = 0; q < kPlanPer; ++q) {
+        const uint64_t i = i0 + q;
+        nq[q] = 0;
+        hq[q] = 0;
+        if (i < i_end && jjq[q] % ri != 0) {
+          const uint64_t h = i - jjq[q] % ri;  // restart head of item i
+          const uint64_t hko = h >= base ? kos[h - base] : P.it.key_off[h];
+          const uint64_t hke = h + 1 >= base ? kos[h + 1 - base] : P.it.key_off[h + 1];
+          const uint32_t hkl = (uint32_t)min(hke - hko, (uint64_t)0xFFFF);
+          nq[q] = min(hkl, m[q].klen);
+          hq[q] = hko;
+          wa[q] = gwin16(P.it.keys + hko);
+          wb[q] = gwin16(P.it.keys + m[q].ko);
+        }
+      }
+#pragma unroll
+      for (uint32_t q = 0; q < kPlanPer; ++q) {
+        if (!nq[q]) continue;
+        const uint64_t x0 = wa[q].lo ^ wb[q].lo, x1 = wa[q].hi ^ wb[q].hi;
+        const uint32_t n = nq[q];
+        uint32_t sh;
+        if (x0) sh = min(n, (uint32_t)(__builtin_ctzll(x0) >> 3));
+        else if (x1) sh = min(n, 8 + (uint32_t)(__builtin_ctzll(x1) >> 3));
+        else sh = n <= 16 ? n : lcp_tail(P.it.keys, hq[q], m[q].ko, n);
+        m[q].sh = sh;
+      }
+    }
+    // ---- 3. record lengths, workgroup scan in item order
+    uint64_t rec[kPlanPer], tsum = 0;
+#pragma unroll
+    for (uint32_t q = 0; q < kPlanPer; ++q) {
+      rec[q] = 0;
+      if (i0 + q < i_end) rec[q] = item_record_len(P, m[q], jjq[q] % ri == 0);
+      tsum += rec[q];
+    }
+    const uint64_t incl = wave_incl_scan_u64(tsum);
     if (lane == kWave - 1) psum[wave] = incl;
     __syncthreads();
     uint64_t wbase = 0, ptot = 0;
@@ -605,18 +759,30 @@ __global__ __launch_bounds__(256) void encode_plan_kernel(EncodeParams P) {
       wbase += w < wave ? v : 0;
       ptot += v;
     }
-    const uint64_t ex = carry + wbase + incl - rec;
-    const bool head = jj == ridx * ri;
-    if (live) {
-      if (jj == 0) bfirst[j] = ex;
-      if (jj + 1 == n) bend[j] = ex + rec;
-      if (head && ridx == (n - 1) / ri) lhead[j] = ex;
+    uint64_t ex = carry + wbase + incl - tsum;
+    uint64_t exq[kPlanPer];
+#pragma unroll
+    for (uint32_t q = 0; q < kPlanPer; ++q) {
+      exq[q] = ex;
+      if (i0 + q < i_end) {
+        const uint32_t jb = jq[q], jj = jjq[q], ridx = jj / ri;
+        const uint32_t n = bst[jb + 1] - bst[jb];
+        if (jj == 0) bfirst[jb] = ex;
+        if (jj + 1 == n) bend[jb] = ex + rec[q];
+        if (jj == ridx * ri && ridx == (n - 1) / ri) lhead[jb] = ex;
+      }
+      ex += rec[q];
     }
-    __syncthreads();  // (also orders this pass's psum reads before the next pass's writes)
-    if (live) {
-      const uint64_t roff = ex - bfirst[j];
-      const uint32_t x = head ? ridx : m.sh;
-      P.erec[i] = (uint32_t)min(roff, (uint64_t)0x7FFF) | (head ? kErecHead : 0u) | (min(x, 0xFFFFu) << 16);
+    __syncthreads();  // (also orders this chunk's psum / kos reads before the next chunk's writes)
+#pragma unroll
+    for (uint32_t q = 0; q < kPlanPer; ++q) {
+      if (i0 + q < i_end) {
+        const uint32_t jj = jjq[q], ridx = jj / ri;
+        const bool head = jj == ridx * ri;
+        const uint64_t roff = exq[q] - bfirst[jq[q]];
+        const uint32_t x = head ? ridx : m[q].sh;
+        P.erec[i0 + q] = (uint32_t)min(roff, (uint64_t)0x7FFF) | (head ? kErecHead : 0u) | (min(x, 0xFFFFu) << 16);
+      }
     }
     carry += ptot;
   }
@@ -628,12 +794,12 @@ __global__ __launch_bounds__(256) void encode_plan_kernel(EncodeParams P) {
   const uint64_t recs = bad ? 0 : bend[tid] - bfirst[tid], last_head = bad ? 0 : lhead[tid] - bfirst[tid];
   const uint32_t bin_len = n ? (n + ri - 1) / ri : 0;
   const uint32_t step = last_head <= 0xFFFF ? 2 : 4;
-  const uint32_t buckets = is_index(P) ? 0 : bucket_count(n, P.ratio);
+  const uint32_t buckets = kIndex ? 0 : bucket_count(n, P.ratio);
   const uint32_t hash_w = (buckets > 0 && bin_len <= kHashMaxPointers) ? buckets : 0;
   const uint64_t total = kHdrLen + recs + 1 + (uint64_t)bin_len * step + hash_w + kTrailerLen;
   if (recs > 0xFFFFFFF0ULL || total > 0xFFFFFF00ULL) bad = true;
   const uint64_t ks = P.it.key_off[s], ke = P.it.key_off[e];
-  const uint64_t vs = is_index(P) ? 0 : P.it.val_off[s], ve = is_index(P) ? 0 : P.it.val_off[e];
+  const uint64_t vs = kIndex ? 0 : P.it.val_off[s], ve = kIndex ? 0 : P.it.val_off[e];
   uint32_t flags = 0;
   if (bad) {
     flags = kPlanBad;
@@ -719,10 +885,14 @@ __device__ __forceinline__ void lds_copy(uint8_t* dst, uint32_t d, const uint8_t
   const uint32_t* s32 = reinterpret_cast<const uint32_t*>(src + (sp & ~3u));
   uint32_t* d32 = reinterpret_cast<uint32_t*>(dst + d1);
   uint32_t q = ((rot & 15u) * body) >> 4;  // 0 <= q < body
-  for (uint32_t j0 = 0; j0 < body; j0 += 8) {
-    uint32_t lo[8], hi[8], at[8];
+#ifndef LSM_COPY_UNROLL
+#define LSM_COPY_UNROLL 4
+#endif
+  constexpr uint32_t U = LSM_COPY_UNROLL;  // dwords per step (all reads before the writes)
+  for (uint32_t j0 = 0; j0 < body; j0 += U) {
+    uint32_t lo[U], hi[U], at[U];
 #pragma unroll
-    for (uint32_t t = 0; t < 8; ++t) {
+    for (uint32_t t = 0; t < U; ++t) {
       uint32_t p = q + t;
       p = p >= body ? p - body : p;
       at[t] = p;
@@ -732,9 +902,9 @@ __device__ __forceinline__ void lds_copy(uint8_t* dst, uint32_t d, const uint8_t
       }
     }
 #pragma unroll
-    for (uint32_t t = 0; t < 8; ++t)
+    for (uint32_t t = 0; t < U; ++t)
       if (j0 + t < body) d32[at[t]] = alignbyte(hi[t], lo[t], sh);
-    q += 8;
+    q += U;
     q = q >= body ? q - body : q;
   }
   const uint32_t t0 = d1 + 4 * body;  // 0..3 tail bytes
@@ -762,6 +932,19 @@ __device__ __forceinline__ void group_barrier() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
+// The group kernel's barrier: a release fence on LDS counts in-flight LDS-DMA
+// as LDS stores and waits for it and for every other outstanding load
+// (vmcnt(0)), which would expose the next group's stage DMA and item loads at
+// the first barrier after they are issued.  Only this wave's own LDS
+// operations are completed here (lgkmcnt(0)); the asm's memory clobber keeps
+// the compiler from moving memory operations across it.  The stage and the
+// prefetched item fields are waited for explicitly (vmcnt(0)) before the
+// copy-out, and the next iteration's first barrier orders every wave's wait
+// before any read of the stage.
+__device__ __forceinline__ void group_barrier_lds() {
+  asm volatile("s_waitcnt lgkmcnt(0)\n\ts_barrier" ::: "memory");
+}
+
 #ifdef LSM_DIAG
 // Diagnostic per-phase cycle totals of wave 0 of every group workgroup
 // (lsm_block_params.reserved bit 0x80; read by lsm_diag_encode_phases).
@@ -775,6 +958,11 @@ __device__ __forceinline__ void group_barrier() {
 #define ENC_PHASE(i)
 #endif
 
+// kIndex: index blocks (restart interval 1, handle fields); kHash: the batch
+// has hash indexes (hash ratio > 0).  Both are batch-wide, so the paths a
+// batch never takes are compiled out (their registers would spill the
+// common path: every scratch reload waits for all outstanding loads).
+template <bool kIndex, bool kHash>
 __global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(4))) void encode_group_kernel(EncodeParams P) {
   __shared__ GroupLds L;
   typedef __attribute__((address_space(3))) void lds_void_t;
@@ -784,8 +972,8 @@ __global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(4))) 
   const int lane = tid & (kWave - 1);
   const uint32_t b_begin = blockIdx.x * kGRun;
   const uint32_t b_end = min(b_begin + kGRun, P.n_blocks);
-  const uint32_t ri = is_index(P) ? 1 : P.ri;
-  const bool index = is_index(P);
+  const uint32_t ri = kIndex ? 1 : P.ri;
+  constexpr bool index = kIndex;
   if (tid < sizeof(LongSecret) / 8)
     reinterpret_cast<uint64_t*>(&L.secret)[tid] = reinterpret_cast<const uint64_t*>(&kLongSecret)[tid];
   // the run's blocks, lane l = block b_begin + l (every wave holds the same registers)
@@ -850,16 +1038,20 @@ __global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(4))) 
   uint32_t* hhi = hlo + kGHash;                    // [kGHash] vote max
   uint64_t* contrib = reinterpret_cast<uint64_t*>(L.uni);  // [kGUnits][4][2] (after the records)
 
-  // item t's fields of group g (loads only; consumed by the next iteration)
-  // (the plan pass has vetted every group-class item: `bad` is not needed here)
-  auto load_items = [&](const Grp& g, ItemMeta& m) {
+  // item t's raw fields of group g: plain loads, no arithmetic and no branch
+  // (threads past the group's items load its last item), so nothing waits
+  // for them until the next iteration cooks them (the plan pass has vetted
+  // every group-class item: no `bad` checks here)
+  auto load_items = [&](const Grp& g, RawItem& r) {
     const uint32_t r0 = g.b - b_begin;
     const uint32_t i0 = rl32(r_start, r0), n = rl32(r_start, r0 + g.k) - i0;
-    bool bad = false;
-    if (tid < n) {
-      m = load_item(P, (uint64_t)i0 + tid, bad);
-      m.e = P.erec[(uint64_t)i0 + tid];
-    }
+    const uint64_t i = (uint64_t)i0 + min(tid, n - 1);
+    r = load_raw<kIndex>(P, i);
+    r.e = P.erec[i];
+  };
+  auto cook = [&](const RawItem& r) {
+    bool bad = false;  // (vetted by the plan pass)
+    return cook_item<kIndex>(r, bad);
   };
 
   // Software pipeline: group G's stage DMA and item fields are issued one
@@ -871,10 +1063,10 @@ __global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(4))) 
   uint32_t ph_n = 0;
 #endif
   Grp G = next_group(b_begin);
-  ItemMeta m{};
+  RawItem raw{};
   if (G.k) {
     issue_dma(G);
-    load_items(G, m);
+    load_items(G, raw);
   }
   __builtin_amdgcn_s_waitcnt(0x0070);
   ENC_PHASE(11);
@@ -889,8 +1081,10 @@ __global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(4))) 
     const bool live = tid < n_items;
     // the next group's item fields: in flight under this whole group
     const Grp Gn = next_group(G.b + k);
-    ItemMeta mn{};
-    if (Gn.k) load_items(Gn, mn);
+    ItemMeta m = cook(raw);
+#ifndef LSM_NO_PREFETCH
+    if (Gn.k) load_items(Gn, raw);
+#endif
     ENC_PHASE(9);
     // ---- wave 0: the group's block table (lane j = group block j; shuffles with every lane active)
     if (wave == 0) {
@@ -929,7 +1123,7 @@ __global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(4))) 
       hlo[h] = 0xFFFFFFFFu;
       hhi[h] = 0;
     }
-    group_barrier();
+    group_barrier_lds();
     ENC_PHASE(1);
     // ---- item t: its block (record offset and shared prefix from E1)
     uint32_t j = 0;
@@ -975,7 +1169,7 @@ __global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(4))) 
         const uint32_t bp = p0 + B.recs + 1 + (m.e >> 16) * B.step;
         for (uint32_t q = 0; q < B.step; ++q) L.img[bp + q] = (uint8_t)(roff >> (8 * q));
       }
-      if (B.hash_w) {
+      if (kHash && B.hash_w) {
         const uint32_t ridx = (tid - B.it0) / ri;
         const uint64_t hv = xxh3_64_any(m.klen, BaseReader8{L.keys, kst}, BaseReader64{L.keys, kst});
         const uint32_t bk = B.hash_base + (uint32_t)(hv % B.hash_w);
@@ -983,7 +1177,7 @@ __global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(4))) 
         atomicMax(&hhi[bk], ridx);
       }
     }
-    group_barrier();
+    group_barrier_lds();
     ENC_PHASE(3);
     // the stage is free: the next group's DMA runs under the tails and the hash
     if (Gn.k && !(kDiagBuild && (P.diag & 16))) issue_dma(Gn);
@@ -998,7 +1192,7 @@ __global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(4))) 
         L.img[p0 + hash_off + q] = (uint8_t)bucket_byte(hlo[B.hash_base + q], hhi[B.hash_base + q]);
       write_trailer_bytes(L.img, p0 + B.plen - kTrailerLen, ri, B.step, B.bin_len, bin_off, B.hash_w, hash_off, B.n);
     }
-    group_barrier();
+    group_barrier_lds();
     ENC_PHASE(4);
     // ---- payload xxh3_128: 1 KiB units over the 16 DPP rows
     {
@@ -1040,7 +1234,7 @@ __global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(4))) 
         }
       }
     }
-    group_barrier();
+    group_barrier_lds();
     ENC_PHASE(5);
     // ---- wave per block: the scramble chain and the merge (or the short path)
     for (uint32_t jb = wave; jb < (kDiagBuild && (P.diag & 10) ? 0 : k); jb += kGWaves) {
@@ -1072,7 +1266,7 @@ __global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(4))) 
       write_header_bytes(L.img, B.img, P.type, lo, hi, B.plen);
       if (lane == 0) P.status[G.b + jb] = ST_OK;
     }
-    group_barrier();
+    group_barrier_lds();
     ENC_PHASE(6);
     __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0): the next group's DMA pieces and item fields
     ENC_PHASE(7);
@@ -1096,7 +1290,6 @@ __global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(4))) 
     ++ph_n;
 #endif
     G = Gn;
-    m = mn;
   }
 #ifdef LSM_DIAG
   if ((P.diag & 0x80) && tid == 0) {
@@ -1261,13 +1454,23 @@ hipError_t launch_encode(const lsm_items& items, const uint32_t* starts, uint32_
   uint64_t* tiles = (uint64_t*)w; w += al256(scan_tiles(n_blocks) * 8);
   P.erec = (uint32_t*)w;
   hipError_t e;
-  hipLaunchKernelGGL(encode_plan_kernel, dim3((n_blocks + kPlanBlocks - 1) / kPlanBlocks), dim3(256), 0, st, P);
+  const dim3 pgrid((n_blocks + kPlanBlocks - 1) / kPlanBlocks);
+  if (P.type == 1)
+    hipLaunchKernelGGL(encode_plan_kernel<true>, pgrid, dim3(256), 0, st, P);
+  else
+    hipLaunchKernelGGL(encode_plan_kernel<false>, pgrid, dim3(256), 0, st, P);
   if ((e = launch_excl_scan(P.sizes, n_blocks, tiles,
                             EncodeOffOut{block_off, P.sizes, P.lists, P.list_count, n_blocks}, st)) != hipSuccess)
     return e;
   static uint64_t attr_done = 0;
   if ((e = set_lds_attr((const void*)encode_write_list_kernel, kImgBig, &attr_done)) != hipSuccess) return e;
-  hipLaunchKernelGGL(encode_group_kernel, dim3((n_blocks + kGRun - 1) / kGRun), dim3(kGThreads), 0, st, P);
+  const dim3 ggrid((n_blocks + kGRun - 1) / kGRun), gblock(kGThreads);
+  if (P.type == 1)
+    hipLaunchKernelGGL((encode_group_kernel<true, false>), ggrid, gblock, 0, st, P);
+  else if (P.ratio > 0.0f)
+    hipLaunchKernelGGL((encode_group_kernel<false, true>), ggrid, gblock, 0, st, P);
+  else
+    hipLaunchKernelGGL((encode_group_kernel<false, false>), ggrid, gblock, 0, st, P);
   hipLaunchKernelGGL(encode_write_list_kernel, dim3(2048), dim3(kWave), kImgMedium, st, P, kPlanMedium);
   hipLaunchKernelGGL(encode_write_list_kernel, dim3(512), dim3(kWave), kImgBig, st, P, kPlanBig);
   hipLaunchKernelGGL(encode_large_kernel, dim3(1024), dim3(64), 0, st, P);
