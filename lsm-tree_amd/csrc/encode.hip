@@ -574,13 +574,25 @@ constexpr uint32_t kErecHead = 0x8000u;
 
 // Group write kernel (E2) budget, see encode_group_kernel.
 constexpr uint32_t kGWaves = 4, kGThreads = kGWaves * kWave;
-constexpr uint32_t kGRun = 32;                 // blocks per workgroup
+#ifndef LSM_G_RUN
+#define LSM_G_RUN 32
+#endif
+constexpr uint32_t kGRun = LSM_G_RUN;          // blocks per workgroup (<= 63: one lane each)
 constexpr uint32_t kGBlocks = 16;              // blocks per group
 constexpr uint32_t kGItems = 256;              // items per group (one thread each)
 constexpr uint32_t kGSlack = 48;               // readable bytes past each staged span
-constexpr uint32_t kGKeys = 4096, kGVals = 14400, kGImg = 15872;
+#ifndef LSM_G_KEYS  // group LDS budget (four configs[1] blocks by default)
+#define LSM_G_KEYS 4096
+#define LSM_G_VALS 14400
+#define LSM_G_IMG 15872
+#define LSM_G_UNION 4096
+#endif
+#ifndef LSM_G_WPE
+#define LSM_G_WPE 4
+#endif
+constexpr uint32_t kGKeys = LSM_G_KEYS, kGVals = LSM_G_VALS, kGImg = LSM_G_IMG;
 constexpr uint32_t kGUnits = kGImg / 1024 + kGBlocks + 1;  // hash units per group
-constexpr uint32_t kGUnion = 4096;             // hash votes | hash contributions
+constexpr uint32_t kGUnion = LSM_G_UNION;      // hash votes | hash contributions
 constexpr uint32_t kGHash = kGUnion / 8;       // vote pairs
 static_assert(kGUnits * 64 <= kGUnion, "hash contributions");
 
@@ -963,7 +975,7 @@ __device__ __forceinline__ void group_barrier_lds() {
 // batch never takes are compiled out (their registers would spill the
 // common path: every scratch reload waits for all outstanding loads).
 template <bool kIndex, bool kHash>
-__global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(4))) void encode_group_kernel(EncodeParams P) {
+__global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(LSM_G_WPE))) void encode_group_kernel(EncodeParams P) {
   __shared__ GroupLds L;
   typedef __attribute__((address_space(3))) void lds_void_t;
   typedef const __attribute__((address_space(1))) void gbl_void_t;
