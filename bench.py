@@ -266,7 +266,7 @@ def ceilings(torch, nbytes=4 << 30, reps=5):
 
 
 # ------------------------------------------------------------- side legs
-def time_decode(torch, lsmgpu, blocks, boff, nb, n_items, steps, fields=DATA_FIELDS + ["handle_off"]):
+def time_decode(torch, lsmgpu, blocks, boff, nb, n_items, steps, fields=DATA_FIELDS):
     """Device-resident lsm_decode_blocks over a batch (count + scan + verify +
     parse), HIP events on the launch stream; checks every status and the count."""
     dec = lsmgpu.Decoder(blocks.device)
@@ -388,7 +388,7 @@ def bench_config5(torch, lsmgpu, steps, rank, world, dist, dev, threads, total_b
     import numpy as np
     blocks, boff, nb, n_items, nbytes, n_idx, checked = build_config5_shard(torch, lsmgpu, total_bytes / world,
                                                                             rank, threads)
-    ms, out = time_decode(torch, lsmgpu, blocks, boff, nb, n_items, steps)
+    ms, out = time_decode(torch, lsmgpu, blocks, boff, nb, n_items, steps, fields=DATA_FIELDS + ["handle_off"])
     host = blocks[:nbytes].cpu().numpy()
     hoff = boff.cpu().numpy().view(np.uint64)
     check_decode_all(out, host, hoff, nb, threads, fields=DATA_FIELDS + ["handle_off"])

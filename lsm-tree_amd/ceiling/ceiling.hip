@@ -9,6 +9,10 @@
 //   lsm_ceiling_read   the decode kernel's read shape alone: 4-wave
 //                      workgroups (four per CU) stage consecutive 32 KiB spans
 //                      into LDS by LDS-DMA, nothing computed: the read ceiling.
+//   lsm_ceiling_soa    WRITE_SIZE calibration for the decode output: the parsed
+//                      SoA (u64, 3 x u32, 2 x u16, u8 per item) written either
+//                      as the decode kernel writes it (thread = item, 1-8 B
+//                      per lane) or as 16 B/lane stores of the same arrays.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
@@ -75,7 +79,43 @@ __global__ __launch_bounds__(256) void read_kernel(const uint8_t* __restrict__ s
   if (acc == 0x9E3779B9u) sink[0] = acc;  // keeps the reads live
 }
 
+// mode 0: thread = item, one store per field (the decode kernel's shape);
+// mode 1: every array as 16 B/lane stores (same bytes).
+__global__ __launch_bounds__(256) void soa_kernel(uint8_t* __restrict__ out, uint64_t n, int mode) {
+  uint64_t* seq = (uint64_t*)out;
+  uint32_t* ko = (uint32_t*)(out + 8 * n);
+  uint32_t* vo = ko + n;
+  uint32_t* vl = vo + n;
+  uint16_t* kl = (uint16_t*)(vl + n);
+  uint16_t* pl = kl + n;
+  uint8_t* vt = (uint8_t*)(pl + n);
+  const uint64_t i = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  if (mode == 0) {
+    if (i >= n) return;
+    const uint32_t x = (uint32_t)i;
+    seq[i] = i;
+    ko[i] = x;
+    vo[i] = x + 1;
+    vl[i] = x + 2;
+    kl[i] = (uint16_t)x;
+    pl[i] = (uint16_t)(x + 3);
+    vt[i] = (uint8_t)x;
+  } else {
+    const uint64_t n16 = 25 * n / 16;  // (n a multiple of 16)
+    const u32x4 v = {(uint32_t)i, (uint32_t)i + 1, (uint32_t)i + 2, (uint32_t)i + 3};
+    if (i < n16) reinterpret_cast<u32x4*>(out)[i] = v;
+  }
+}
+
 }  // namespace
+
+extern "C" int lsm_ceiling_soa(void* out, uint64_t n_items, int mode, void* stream) {
+  if (((uintptr_t)out & 15) || (n_items & 15)) return 10;
+  const uint64_t threads = mode == 0 ? n_items : 25 * n_items / 16;
+  hipLaunchKernelGGL(soa_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     (uint8_t*)out, n_items, mode);
+  return hipGetLastError() == hipSuccess ? 0 : 11;
+}
 
 extern "C" int lsm_ceiling_copy_variant(const void* src, void* dst, uint64_t bytes, int variant, void* stream) {
   if (((uintptr_t)src | (uintptr_t)dst | bytes) & 15) return 10;

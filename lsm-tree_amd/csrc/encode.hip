@@ -466,6 +466,32 @@ __device__ __forceinline__ void write_header_bytes(uint8_t* dst, uint32_t hp, ui
   else if (lane < 33) dst[hp + lane] = (uint8_t)((uint32_t)hlo >> (8 * (lane - 29)));
 }
 
+// The same header written by a lane quad (lane q of the quad: bytes
+// [8q, 8q + 8), lane 0 also byte 32), every lane computing the 29-byte
+// checksum itself.
+__device__ __forceinline__ void write_header_quad(uint8_t* dst, uint32_t hp, uint32_t type, uint64_t ck_lo,
+                                                  uint64_t ck_hi, uint32_t plen, int q) {
+  const uint64_t w0 = 0x034D534CULL | ((uint64_t)type << 32) | (ck_lo << 40);
+  const uint64_t w1 = (ck_lo >> 24) | (ck_hi << 40);
+  const uint64_t w2 = (ck_hi >> 24) | ((uint64_t)plen << 40);
+  const uint64_t w3 = ((uint64_t)plen >> 24) | ((uint64_t)plen << 8);
+  auto r64 = [&](uint32_t o) -> uint64_t {  // LE u64 at byte o of w0..w3 (o <= 24)
+    const uint32_t qq = o >> 3, sft = (o & 7) * 8;
+    const uint64_t a = qq == 0 ? w0 : qq == 1 ? w1 : qq == 2 ? w2 : w3;
+    const uint64_t b = qq == 0 ? w1 : qq == 1 ? w2 : qq == 2 ? w3 : 0;
+    return sft ? (a >> sft) | (b << (64 - sft)) : a;
+  };
+  auto r8 = [&](uint32_t o) -> uint32_t { return (uint32_t)(r64(o) & 0xFF); };
+  uint64_t hlo, hhi;
+  xxh3_128_short(29, r8, r64, hlo, hhi);
+  // bytes 29..32: the low 4 bytes of the header checksum
+  const uint64_t w = q == 0 ? w0 : q == 1 ? w1 : q == 2 ? w2 : (w3 & 0xFFFFFFFFFFULL) | (hlo << 40);
+  const uint32_t at = hp + 8 * q;
+#pragma unroll
+  for (uint32_t i = 0; i < 8; ++i) dst[at + i] = (uint8_t)(w >> (8 * i));
+  if (q == 0) dst[hp + 32] = (uint8_t)(hlo >> 24);
+}
+
 // ------------------------------------------------------ E2: LDS write pass
 // Wave-local ordering of LDS traffic between lanes (no workgroup barrier:
 // the waves of a workgroup write independent blocks).
@@ -896,28 +922,37 @@ __device__ __forceinline__ void lds_copy(uint8_t* dst, uint32_t d, const uint8_t
   const uint32_t sp = s + h, sh = sp & 3u;
   const uint32_t* s32 = reinterpret_cast<const uint32_t*>(src + (sp & ~3u));
   uint32_t* d32 = reinterpret_cast<uint32_t*>(dst + d1);
-  uint32_t q = ((rot & 15u) * body) >> 4;  // 0 <= q < body
+  // 32 start points: a ds_read_b32 wave access is two groups of 32 lanes, so
+  // lanes with a 64-B source stride (16 dwords: two per bank) all differ.
+  uint32_t q = ((rot & 31u) * body) >> 5;  // 0 <= q < body
 #ifndef LSM_COPY_UNROLL
 #define LSM_COPY_UNROLL 4
 #endif
   constexpr uint32_t U = LSM_COPY_UNROLL;  // dwords per step (all reads before the writes)
+  // Each source dword is read once: destination dword p is
+  // alignbyte(src[p + 1], src[p]) and src[p] is the previous step's src[p + 1],
+  // except after the wrap to p = 0, which takes w0 = src[0].
+  const uint32_t w0 = s32[0];
+  uint32_t carry = s32[q];
   for (uint32_t j0 = 0; j0 < body; j0 += U) {
-    uint32_t lo[U], hi[U], at[U];
+    uint32_t hi[U], at[U];
 #pragma unroll
     for (uint32_t t = 0; t < U; ++t) {
       uint32_t p = q + t;
       p = p >= body ? p - body : p;
       at[t] = p;
-      if (j0 + t < body) {
-        lo[t] = s32[p];
-        hi[t] = s32[p + 1];
-      }
+      if (j0 + t < body) hi[t] = s32[p + 1];
     }
 #pragma unroll
-    for (uint32_t t = 0; t < U; ++t)
-      if (j0 + t < body) d32[at[t]] = alignbyte(hi[t], lo[t], sh);
+    for (uint32_t t = 0; t < U; ++t) {
+      if (j0 + t < body) {
+        const uint32_t lo = t == 0 ? carry : (at[t] == 0 ? w0 : hi[t - 1]);
+        d32[at[t]] = alignbyte(hi[t], lo, sh);
+      }
+    }
     q += U;
     q = q >= body ? q - body : q;
+    carry = q == 0 ? w0 : hi[U - 1];
   }
   const uint32_t t0 = d1 + 4 * body;  // 0..3 tail bytes
   uint32_t tb[3];
@@ -1082,6 +1117,7 @@ __global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(LSM_G
   }
   __builtin_amdgcn_s_waitcnt(0x0070);
   ENC_PHASE(11);
+  uint32_t iter = 0;  // rotates the chain wave over the SIMDs
   while (G.k) {
     ENC_PHASE(0);
     const uint32_t r0 = G.b - b_begin, k = G.k;
@@ -1248,35 +1284,45 @@ __global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(LSM_G
     }
     group_barrier_lds();
     ENC_PHASE(5);
-    // ---- wave per block: the scramble chain and the merge (or the short path)
-    for (uint32_t jb = wave; jb < (kDiagBuild && (P.diag & 10) ? 0 : k); jb += kGWaves) {
-      GBlk& B = L.blk[jb];
-      const uint32_t p0 = B.img + kHdrLen;
-      uint64_t lo, hi;
-      if (B.plen > 240) {
-        const int q = lane & 3;
+    // ---- one wave, a lane quad per block (k <= 16): the scramble chain and
+    // the merge (or the short path), then the header.  Lane q of the quad
+    // holds accumulator pair q; the chain is one instruction stream for all
+    // the group's blocks.
+    if (wave == (iter & (kGWaves - 1)) && !(kDiagBuild && (P.diag & 10))) {
+      const uint32_t jb = (uint32_t)lane >> 2;
+      const int q = lane & 3;
+      const bool in = jb < k;
+      const GBlk& B = L.blk[in ? jb : 0];
+      const uint32_t p0 = B.img + kHdrLen, plen = B.plen;
+      uint64_t lo = 0, hi = 0;
+      if (in && plen > 240) {
         uint64_t a0 = q == 0 ? (uint64_t)P32_3 : q == 1 ? P64_2 : q == 2 ? P64_4 : P64_5;
         uint64_t a1 = q == 0 ? P64_1 : q == 1 ? P64_3 : q == 2 ? (uint64_t)P32_2 : (uint64_t)P32_1;
         const uint64_t scr0 = L.secret.acc[16 + 2 * q], scr1 = L.secret.acc[16 + 2 * q + 1];
+        const uint64_t* cb = contrib + 8 * B.u0 + 2 * q;
         for (uint32_t n = 0; n < B.nbk; ++n) {
-          a0 += contrib[8 * (B.u0 + n) + 2 * q];
+          a0 += cb[8 * n];
           a0 ^= a0 >> 47; a0 ^= scr0; a0 *= P32_1;
-          a1 += contrib[8 * (B.u0 + n) + 2 * q + 1];
+          a1 += cb[8 * n + 1];
           a1 ^= a1 >> 47; a1 ^= scr1; a1 *= P32_1;
         }
-        a0 += contrib[8 * (B.u0 + B.nbk) + 2 * q];
-        a1 += contrib[8 * (B.u0 + B.nbk) + 2 * q + 1];
-        uint64_t tlo = mul_fold64(a0 ^ L.secret.mlo[2 * q], a1 ^ L.secret.mlo[2 * q + 1]);
-        uint64_t thi = mul_fold64(a0 ^ L.secret.mhi[2 * q], a1 ^ L.secret.mhi[2 * q + 1]);
-        tlo = quad_sum64(tlo);
-        thi = quad_sum64(thi);
-        lo = xxh3_avalanche((uint64_t)B.plen * P64_1 + tlo);
-        hi = xxh3_avalanche(~((uint64_t)B.plen * P64_2) + thi);
-      } else {
-        xxh3_128_short(B.plen, BaseReader8{L.img, p0}, BaseReader64{L.img, p0}, lo, hi);
+        a0 += cb[8 * B.nbk];
+        a1 += cb[8 * B.nbk + 1];
+        lo = mul_fold64(a0 ^ L.secret.mlo[2 * q], a1 ^ L.secret.mlo[2 * q + 1]);
+        hi = mul_fold64(a0 ^ L.secret.mhi[2 * q], a1 ^ L.secret.mhi[2 * q + 1]);
       }
-      write_header_bytes(L.img, B.img, P.type, lo, hi, B.plen);
-      if (lane == 0) P.status[G.b + jb] = ST_OK;
+      lo = quad_sum64(lo);  // (every lane: DPP reads of inactive lanes are undefined)
+      hi = quad_sum64(hi);
+      if (in) {
+        if (plen > 240) {
+          lo = xxh3_avalanche((uint64_t)plen * P64_1 + lo);
+          hi = xxh3_avalanche(~((uint64_t)plen * P64_2) + hi);
+        } else {
+          xxh3_128_short(plen, BaseReader8{L.img, p0}, BaseReader64{L.img, p0}, lo, hi);
+        }
+        write_header_quad(L.img, B.img, P.type, lo, hi, plen, q);
+        if (q == 0) P.status[G.b + jb] = ST_OK;
+      }
     }
     group_barrier_lds();
     ENC_PHASE(6);
@@ -1301,6 +1347,7 @@ __global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(LSM_G
 #ifdef LSM_DIAG
     ++ph_n;
 #endif
+    ++iter;
     G = Gn;
   }
 #ifdef LSM_DIAG

@@ -33,7 +33,7 @@ def main():
     items, starts, n_items = bench.make_workload(torch, lsmgpu, nb)
     enc = lsmgpu.Encoder().encode(items, starts, nb)
     dec = lsmgpu.Decoder()
-    out = dec.alloc_outputs(n_items, nb)
+    out = dec.alloc_outputs(n_items, nb, fields=bench.DATA_FIELDS)  # the bench's data-block outputs (no handle_off)
     dec.decode(enc["buf"], enc["block_off"], nb, out, n_items)
     torch.cuda.synchronize()
     v = [int(x, 0) for x in args.tuning.split(",")]
