@@ -642,7 +642,12 @@ __device__ __host__ __forceinline__ bool group_fits(uint64_t n, uint64_t kspan, 
 //      in its block, kept for E2 in erec.
 // Per block: size, binary-index step, hash-index size, size class, and the
 // key / value span starts E2 stages.
-constexpr uint32_t kPlanBlocks = 16;
+#ifndef LSM_PLAN_BLOCKS
+#define LSM_PLAN_BLOCKS 128
+#endif
+// blocks per workgroup: longer-lived workgroups (16 -> 128: 0.80 -> 0.68 ms per 1 M blocks)
+constexpr uint32_t kPlanBlocks = LSM_PLAN_BLOCKS;
+static_assert(kPlanBlocks <= 255, "thread nb loads the run's end: nb < 256 threads");
 #ifndef LSM_PLAN_PER
 #define LSM_PLAN_PER 2
 #endif
@@ -673,7 +678,12 @@ __device__ __forceinline__ Win16 gwin16(const uint8_t* p) {
 
 // Shared prefix past an equal first 16 bytes: 16 bytes per step (rare: long
 // common key prefixes; kept narrow so the common path's registers stay low).
-__device__ __noinline__ uint32_t lcp_tail(const uint8_t* keys, uint64_t a, uint64_t b, uint32_t n) {
+#ifdef LSM_LCP_INLINE
+__device__ __forceinline__
+#else
+__device__ __noinline__
+#endif
+uint32_t lcp_tail(const uint8_t* keys, uint64_t a, uint64_t b, uint32_t n) {
   for (uint32_t k = 16; k < n; k += 16) {
     const Win16 wa = gwin16(keys + a + k), wb = gwin16(keys + b + k);
     const uint64_t x0 = wa.lo ^ wb.lo, x1 = wa.hi ^ wb.hi;
@@ -1032,6 +1042,14 @@ __global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(LSM_G
   const BlockPlan r_plan = (in_run && rb < b_end) ? P.plans[rb] : BlockPlan{0, 0, 0, 0};
   const uint32_t r_hash = r_plan.hash_w;
   const uint32_t r_hpre = wave_incl_scan_u32(r_hash) - r_hash;  // exclusive prefix over the run
+  // payload hash units (1 KiB, long path only) per block, exclusive prefix over the run
+  uint32_t r_upre;
+  {
+    const uint64_t nx = wave_shfl_u64(r_off, min(lane + 1, 63));
+    const uint32_t plen = (rb < b_end) ? (uint32_t)(nx - r_off) - kHdrLen : 0;
+    const uint32_t units = plen > 240 ? (plen - 1) / 1024 + 1 : 0;
+    r_upre = wave_incl_scan_u32(units) - units;
+  }
   auto lane_u32 = [&](uint32_t v, uint32_t l) { return (uint32_t)__shfl((int)v, (int)min(l, 63u)); };
   auto lane_u64 = [&](uint64_t v, uint32_t l) { return wave_shfl_u64(v, (int)min(l, 63u)); };
   // the same for a wave-uniform lane index: v_readlane into a scalar register
@@ -1174,16 +1192,9 @@ __global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(LSM_G
     group_barrier_lds();
     ENC_PHASE(1);
     // ---- item t: its block (record offset and shared prefix from E1)
+    // (block starts from the run registers, v_readlane: no LDS round trip)
     uint32_t j = 0;
-    if (live) {
-      uint32_t lo = 0, hi = k;
-      while (hi - lo > 1) {
-        const uint32_t mid = (lo + hi) >> 1;
-        if (L.blk[mid].it0 <= tid) lo = mid;
-        else hi = mid;
-      }
-      j = lo;
-    }
+    for (uint32_t jb = 1; jb < k; ++jb) j += (rl32(r_start, r0 + jb) - i0 <= tid) ? 1u : 0u;
     const bool head = (m.e & kErecHead) != 0;
     m.sh = head ? 0u : m.e >> 16;
     // ---- item t: its record into the image
@@ -1245,12 +1256,12 @@ __global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(LSM_G
     // ---- payload xxh3_128: 1 KiB units over the 16 DPP rows
     {
       const uint32_t row = wave * 4 + (lane >> 4), r = lane & 15, q = r & 3, s = r >> 2;
-      const uint32_t units = (kDiagBuild && (P.diag & 10))
-                                 ? 0 : L.blk[k - 1].u0 + (L.blk[k - 1].plen > 240 ? L.blk[k - 1].nbk + 1 : 0);
+      const uint32_t ubase = rl32(r_upre, r0);
+      const uint32_t units = (kDiagBuild && (P.diag & 10)) ? 0 : rl32(r_upre, r0 + k) - ubase;
       const uint64_t* acc = L.secret.acc + s + 2 * q;
       for (uint32_t u = row; u < units; u += 16) {
-        uint32_t jb = 0;
-        while (jb + 1 < k && L.blk[jb + 1].u0 <= u) ++jb;
+        uint32_t jb = 0;  // (unit starts from the run registers: no dependent LDS reads)
+        for (uint32_t x = 1; x < k; ++x) jb += (rl32(r_upre, r0 + x) - ubase <= u) ? 1u : 0u;
         const GBlk& B = L.blk[jb];
         const uint32_t n = u - B.u0, p0 = B.img + kHdrLen;
         uint64_t c0 = 0, c1 = 0;
