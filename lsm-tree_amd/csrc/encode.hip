@@ -942,8 +942,8 @@ __device__ __forceinline__ void lds_copy(uint8_t* dst, uint32_t d, const uint8_t
   // Each source dword is read once: destination dword p is
   // alignbyte(src[p + 1], src[p]) and src[p] is the previous step's src[p + 1],
   // except after the wrap to p = 0, which takes w0 = src[0].
-  const uint32_t w0 = s32[0];
-  uint32_t carry = s32[q];
+  const uint32_t w0 = body ? s32[0] : 0;
+  uint32_t carry = body ? s32[q] : 0;
   for (uint32_t j0 = 0; j0 < body; j0 += U) {
     uint32_t hi[U], at[U];
 #pragma unroll
@@ -1343,16 +1343,25 @@ __global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(LSM_G
     {
       const uint32_t total = (uint32_t)(rl64(r_off, r0 + k) - obase);
       uint8_t* gdst = reinterpret_cast<uint8_t*>(dabs & ~15ULL);
-      const uint32_t chunks = (kDiagBuild && (P.diag & 4)) ? 0 : (pad + total + 15) >> 4;
-      for (uint32_t c = tid; c < chunks; c += kGThreads) {
-        const uint32_t lo = c * 16, hi = lo + 16;
-        if (lo >= pad && hi <= pad + total) {
-          __builtin_nontemporal_store(reinterpret_cast<const u32x4*>(L.img)[c], reinterpret_cast<u32x4*>(gdst) + c);
-        } else {
-          for (uint32_t x = max(lo, pad); x < min(hi, pad + total); ++x)
-            ((__attribute__((address_space(1))) uint8_t*)gdst)[x] = L.img[x];
-        }
+      const uint32_t end = (kDiagBuild && (P.diag & 4)) ? pad : pad + total;
+      const uint32_t c0 = (pad + 15) >> 4, c1 = end >> 4;  // the whole 16-B pieces [c0, c1)
+      const u32x4* src = reinterpret_cast<const u32x4*>(L.img);
+      u32x4* dst = reinterpret_cast<u32x4*>(gdst);
+      for (uint32_t c = c0 + tid; c < c1; c += 4 * kGThreads) {  // four pieces in flight per thread
+        u32x4 v[4];
+#pragma unroll
+        for (uint32_t t = 0; t < 4; ++t)
+          if (c + t * kGThreads < c1) v[t] = src[c + t * kGThreads];
+#pragma unroll
+        for (uint32_t t = 0; t < 4; ++t)
+          if (c + t * kGThreads < c1) __builtin_nontemporal_store(v[t], dst + c + t * kGThreads);
       }
+      // the partial pieces at both ends (shared with the neighbouring groups' bytes)
+      auto* gb = (__attribute__((address_space(1))) uint8_t*)gdst;
+      if (tid == 0)
+        for (uint32_t x = pad; x < min(16 * c0, end); ++x) gb[x] = L.img[x];
+      if (tid == kWave && c1 >= c0)
+        for (uint32_t x = 16 * c1; x < end; ++x) gb[x] = L.img[x];
     }
     ENC_PHASE(8);
 #ifdef LSM_DIAG
