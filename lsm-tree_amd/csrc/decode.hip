@@ -47,8 +47,26 @@ constexpr uint32_t kStagePad = 256;  // readable LDS bytes past the span (fast p
 // restart head's key; [48,53) group block, 53 restart head, 54 valid,
 // [55,58) seqno bytes and [58,60) shared bytes of a header shape phase A has
 // verified (0 = not verified: phase B decodes the header itself).
-constexpr int kRecEndShift = 16, kRecKeyShift = 32, kRecBlockShift = 48, kRecN1Shift = 55, kRecN2Shift = 58;
-constexpr uint64_t kRecRestart = 1ULL << 53, kRecValid = 1ULL << 54;
+// Two layouts: kWide = false for stages < 64 KiB (16-bit image offsets),
+// kWide = true for the big-block kernel's stage (17-bit offsets; the end is
+// kept as its distance from the start, clamped to 2^15 - 1: longer than any
+// record the straight-line parsers take, so a clamped end can only mismatch).
+template <bool kWide>
+struct RecLayout {
+  static constexpr int kPosBits = kWide ? 17 : 16;
+  static constexpr uint32_t kPosMask = (1u << kPosBits) - 1;
+  static constexpr int kKeyShift = 32, kBlockShift = 32 + kPosBits;
+  static constexpr uint64_t kRestart = 1ULL << (kBlockShift + 5), kValid = 1ULL << (kBlockShift + 6);
+  static constexpr int kN1Shift = kBlockShift + 7, kN2Shift = kBlockShift + 10;
+  __device__ static __forceinline__ uint32_t lo(uint32_t a, uint32_t end) {
+    return kWide ? a | (min(end - a, 0x7FFFu) << 17) : a | (end << 16);
+  }
+  __device__ static __forceinline__ uint32_t start(uint64_t d) { return (uint32_t)d & kPosMask; }
+  __device__ static __forceinline__ uint32_t end(uint64_t d) {
+    return kWide ? ((uint32_t)d & kPosMask) + (((uint32_t)d >> 17) & 0x7FFF) : (uint32_t)d >> 16;
+  }
+};
+static_assert(RecLayout<true>::kN2Shift + 2 <= 64 && RecLayout<false>::kN2Shift + 2 <= 64, "descriptor bits");
 
 struct alignas(16) BlockMeta {
   // first 16 bytes: what phase B needs per record (one ds_read_b128)
@@ -223,8 +241,9 @@ __device__ __forceinline__ uint32_t wave_max_u32(uint32_t v) {
   return v;
 }
 
+template <class RL>
 __device__ __forceinline__ uint64_t rec_desc(uint32_t a, uint32_t end, uint32_t key, uint64_t tag) {
-  return (uint64_t)a | ((uint64_t)end << kRecEndShift) | ((uint64_t)key << kRecKeyShift) | tag;
+  return (uint64_t)RL::lo(a, end) | ((uint64_t)key << RL::kKeyShift) | tag;
 }
 
 // Predicted header shape of a non-restart record: n1 seqno bytes, n2 shared
@@ -235,9 +254,10 @@ struct Shape {
   uint64_t msk, pat;
   uint64_t bits;  // descriptor shape bits
 };
+template <class RL>
 __device__ __forceinline__ Shape make_shape(uint32_t n1, uint32_t n2) {
   Shape s;
-  s.bits = ((uint64_t)n1 << kRecN1Shift) | ((uint64_t)n2 << kRecN2Shift);
+  s.bits = ((uint64_t)n1 << RL::kN1Shift) | ((uint64_t)n2 << RL::kN2Shift);
   s.hdr = n1 + n2 + 2;  // <= 8
   s.kshift = 8 * (s.hdr - 1);
   s.msk = 0x8080808080808000ULL & (s.hdr >= 8 ? ~0ULL : ((1ULL << (8 * s.hdr)) - 1));
@@ -273,8 +293,10 @@ __device__ __forceinline__ uint32_t rec_len(uint32_t vt, uint32_t q, uint32_t z)
 // the same 16-byte LDS window; only a shape change, a long key suffix or a
 // long varint leaves the straight path.  The loop is wave-uniform: lanes
 // past their interval's end store to rec[dummy].
+template <bool kWide = false>
 __device__ __forceinline__ void phase_a(const uint8_t* img, BlockMeta* meta, const uint8_t* owner, uint64_t* rec,
                                         uint32_t c_first, uint32_t c_step, uint32_t total, uint32_t dummy) {
+  typedef RecLayout<kWide> RL;
   const int lane = threadIdx.x & (kWave - 1);
   for (uint32_t c0 = c_first; c0 < total; c0 += c_step) {
     const uint32_t c = c0 + lane;
@@ -292,7 +314,7 @@ __device__ __forceinline__ void phase_a(const uint8_t* img, BlockMeta* meta, con
     const uint32_t count = (live && ok) ? (last_iv ? t.item_count - r * t.ri : t.ri) : 0;
     if (live && !ok) atomicCAS(&meta[j].st, ST_OK, ST_PARSE);
     const uint32_t ib0 = m.item0 + r * t.ri;
-    const uint64_t tag = ((uint64_t)j << kRecBlockShift) | kRecValid;
+    const uint64_t tag = ((uint64_t)j << RL::kBlockShift) | RL::kValid;
     const uint32_t stop = p0 + e_rel;
     uint32_t a = p0 + (ok ? s_rel : 0), key = a;
     const uint32_t max_count = __builtin_amdgcn_readfirstlane(wave_max_u32(count));
@@ -304,12 +326,12 @@ __device__ __forceinline__ void phase_a(const uint8_t* img, BlockMeta* meta, con
       const RecHead hd = rec_head(w.lo, true);
       const uint32_t nxt = a + rec_len(hd.vt, hd.q, read_u16_unaligned(img, a + hd.q));
       key = a + hd.hdr;
-      sp = make_shape(min(hd.e1 >> 3, 5u), 1);
+      sp = make_shape<RL>(min(hd.e1 >> 3, 5u), 1);
       defer = count > 1 && !(hd.ok && valid_vtype(hd.vt));
       const bool act = count > 0 && !defer;
       if (count > 1 && act) ok = nxt < rec_end;
-      const uint64_t rbits = (count > 1) ? ((uint64_t)(hd.e1 >> 3) << kRecN1Shift) : 0;  // verified only if walked
-      rec[act ? ib0 : dummy] = rec_desc(a, count == 1 ? stop : nxt, key, tag | kRecRestart | rbits);
+      const uint64_t rbits = (count > 1) ? ((uint64_t)(hd.e1 >> 3) << RL::kN1Shift) : 0;  // verified only if walked
+      rec[act ? ib0 : dummy] = rec_desc<RL>(a, count == 1 ? stop : nxt, key, tag | RL::kRestart | rbits);
       a = (act && ok) ? nxt : a;
     }
     // The straight-line step, kept short because it is one wave's serial
@@ -320,7 +342,7 @@ __device__ __forceinline__ void phase_a(const uint8_t* img, BlockMeta* meta, con
     // marker and phase B rejects any record that does not end where its
     // descriptor says.
     uint32_t qp = 0;
-    uint32_t hi = (uint32_t)((((uint64_t)key << kRecKeyShift) | tag | sp.bits) >> 32);
+    uint32_t hi = (uint32_t)((((uint64_t)key << RL::kKeyShift) | tag | sp.bits) >> 32);
     const uint32_t dmy = dummy;
     for (uint32_t jj = 1; jj < max_count; ++jj) {
       const uint64_t h = read_u64_unaligned(img, a);
@@ -330,17 +352,17 @@ __device__ __forceinline__ void phase_a(const uint8_t* img, BlockMeta* meta, con
       uint32_t vt = (uint32_t)h & 0xFF;
       if (((~h & sp.msk) != sp.pat) | (q != qp)) {  // rare: header shape or key length changed
         const RecHead hd = rec_head(h, false);
-        if (hd.ok) sp = make_shape(hd.e1 >> 3, (hd.e2 - hd.e1) >> 3);
+        if (hd.ok) sp = make_shape<RL>(hd.e1 >> 3, (hd.e2 - hd.e1) >> 3);
         defer = defer || (jj < count && !hd.ok);  // seqno >= 2^49, shared >= 2^21 or key length >= 128
         q = hd.q;
         z = read_u16_unaligned(img, a + q);
         qp = q;
-        hi = (uint32_t)((((uint64_t)key << kRecKeyShift) | tag | sp.bits) >> 32);
+        hi = (uint32_t)((((uint64_t)key << RL::kKeyShift) | tag | sp.bits) >> 32);
       }
       const uint32_t nxt = min(a + rec_len(vt, q, z), rec_end);
       const bool act = jj < count && !defer;
       const uint32_t end = jj + 1 == count ? stop : nxt;
-      rec[act ? ib0 + jj : dmy] = ((uint64_t)hi << 32) | (uint64_t)(a | (end << kRecEndShift));
+      rec[act ? ib0 + jj : dmy] = ((uint64_t)hi << 32) | (uint64_t)RL::lo(a, end);
       a = act ? nxt : a;
     }
     if (defer) meta[j].st = ST_DEFER;                             // wins over PARSE
@@ -403,29 +425,30 @@ __device__ __forceinline__ void store_fields(const DecodeParams& P, bool all_fie
 // Phase B: thread = record.  Full parse + validation of every descriptor
 // (the oracle's parse_data_item checks, and the record must end exactly at
 // the descriptor's end), then coalesced stores of all fields.
-template <bool kAllFields>
+template <bool kAllFields, bool kWide = false>
 __device__ __forceinline__ void phase_b(const DecodeParams& P, const uint8_t* img, BlockMeta* meta,
                                         const uint64_t* rec, uint32_t n_items, uint32_t g_item0, uint32_t tid,
                                         uint32_t nthr) {
+  typedef RecLayout<kWide> RL;
   constexpr bool all_fields = kAllFields;
   const bool store = !(kDiagBuild && (P.flags & kDiagSkipStore));
   for (uint32_t i0 = 0; i0 < n_items; i0 += nthr) {
     const uint32_t i = i0 + tid;
     if (i >= n_items) break;
     const uint64_t d = rec[i];
-    if (!(d & kRecValid)) continue;  // not reached: its block has failed
-    const uint32_t j = (uint32_t)(d >> kRecBlockShift) & 31;
+    if (!(d & RL::kValid)) continue;  // not reached: its block has failed
+    const uint32_t j = (uint32_t)(d >> RL::kBlockShift) & 31;
     const u32x4 hot = *reinterpret_cast<const u32x4*>(&meta[j]);  // p0, rec_end, st, type
     const uint32_t p0 = hot.x, end = hot.y - p0;
     if ((int32_t)hot.z != ST_OK) continue;  // block already failed: outputs unspecified
-    const uint32_t a = ((uint32_t)d & 0xFFFF) - p0;
-    const uint32_t want = ((uint32_t)(d >> kRecEndShift) & 0xFFFF) - p0;
-    const uint32_t base_key = ((uint32_t)(d >> kRecKeyShift) & 0xFFFF) - p0;
-    const bool restart = (d & kRecRestart) != 0;
+    const uint32_t a = RL::start(d) - p0;
+    const uint32_t want = RL::end(d) - p0;
+    const uint32_t base_key = ((uint32_t)(d >> RL::kKeyShift) & RL::kPosMask) - p0;
+    const bool restart = (d & RL::kRestart) != 0;
     const uint64_t gi = (uint64_t)g_item0 + i;
     ItemFields f;
     uint32_t next;
-    const uint32_t n1 = (uint32_t)(d >> kRecN1Shift) & 7, n2 = (uint32_t)(d >> kRecN2Shift) & 3;
+    const uint32_t n1 = (uint32_t)(d >> RL::kN1Shift) & 7, n2 = (uint32_t)(d >> RL::kN2Shift) & 3;
     const int rc = n1 ? parse_data_shape(img, p0, a, end, restart, base_key, n1, n2, f, next)
                       : parse_data_fast(img, p0, a, end, restart, base_key, f, next);
     if (rc > 0 && store) store_fields(P, all_fields, gi, f);
@@ -637,6 +660,199 @@ __global__ __launch_bounds__(kBigWaves * kWave) void decode_deferred_staged_kern
   }
 }
 
+// Large blocks (SURVEY configs[4]: 16 / 64 KiB data blocks) listed by the
+// group kernel: persistent 8-wave workgroups, two per CU (one stage each:
+// the other workgroup's decode overlaps this one's DMA).  Per block:
+//   all waves   LDS-DMA of the block
+//   wave 0      header fields and trailer (lane 0), then phase A over every
+//               restart interval (lane = interval) ...
+//   waves 1..7  ... while these compute the per-KiB XXH3 contributions
+//   wave 7      the serial XXH3 scramble chain + tail, the header checksum
+//               (at raised priority: it is the block's critical path) ...
+//   waves 0..6  ... while these run phase B (thread = record)
+// Blocks larger than the stage, with more items than kBigGTile, index blocks
+// and rare record shapes go on to the general path (defer2 list).
+#ifndef LSM_BIG_WAVES
+#define LSM_BIG_WAVES 8
+#endif
+constexpr uint32_t kBigGWaves = LSM_BIG_WAVES;
+constexpr uint32_t kBigGStage = 69376;  // 67.75 KiB: a 64 KiB-target block of 69.2 KB plus alignment
+constexpr uint32_t kBigGSlot = kBigGStage + kStagePad;
+constexpr uint32_t kBigGTile = 832;
+constexpr uint32_t kBigGRec = ((kBigGTile + 1) * 8 + 15) & ~15u;
+constexpr uint32_t kBigGContrib = (kBigGStage / 1024 + 1) * 64;
+constexpr uint32_t kBigGOwner = (kBigGTile + 15) & ~15u;
+constexpr uint32_t kBigGLds = 80 + kBigGRec + kBigGOwner + kBigGContrib + kBigGSlot;
+constexpr uint32_t kBigGPerCU = 2;
+static_assert(kBigGLds * kBigGPerCU <= 160 * 1024, "big-block workgroups per CU");
+
+__device__ __forceinline__ void defer2_block(const DecodeParams& P, uint32_t b) {
+  const uint32_t slot = atomicAdd(P.defer2_count, 1u);
+  gstore(P.defer2_list, slot, b);
+}
+
+// A listed block's handle and item range; fits = it takes the stage path.
+struct BigBlk {
+  uint32_t li, b, it0, it1;
+  uint64_t off, end, span0, span1;
+  bool fits;
+};
+__device__ __forceinline__ BigBlk big_blk(const DecodeParams& P, uint32_t li) {
+  BigBlk x;
+  x.li = li;
+  x.b = gload(P.defer_list, li);
+  x.off = gload(P.block_off, x.b);
+  x.end = gload(P.block_off, x.b + 1);
+  x.it0 = gload(P.item_start, x.b);
+  x.it1 = gload(P.item_start, x.b + 1);
+  x.span0 = x.off & ~15ULL;
+  x.span1 = (max(x.end, x.off) + 15) & ~15ULL;
+  x.fits = x.end >= x.off && x.span1 - x.span0 <= kBigGStage && x.it1 - x.it0 <= kBigGTile;
+  return x;
+}
+
+#ifdef LSM_DIAG
+// Diagnostic builds: per-phase s_memtime totals of wave 0 of every big-block
+// workgroup (read by lsm_diag_decode_phases).
+__device__ unsigned long long g_dec_phase[16];
+#define DEC_PHASE(i)                                  \
+  {                                                   \
+    const uint64_t t_ = __builtin_amdgcn_s_memtime(); \
+    ph[i] += t_ - t_last;                             \
+    t_last = t_;                                      \
+  }
+#else
+#define DEC_PHASE(i)
+#endif
+
+template <bool kAllFields>
+__global__ __launch_bounds__(kBigGWaves * kWave) void decode_big_kernel(DecodeParams P) {
+#ifdef LSM_DIAG
+  uint64_t t_last = __builtin_amdgcn_s_memtime(), ph[8] = {};
+  uint32_t nblk = 0;
+#endif
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  BlockMeta* meta = reinterpret_cast<BlockMeta*>(smem);
+  uint64_t* rec = reinterpret_cast<uint64_t*>(smem + 80);
+  uint8_t* owner = smem + 80 + kBigGRec;
+  uint64_t* contrib = reinterpret_cast<uint64_t*>(smem + 80 + kBigGRec + kBigGOwner);
+  uint8_t* stages = smem + 80 + kBigGRec + kBigGOwner + kBigGContrib;
+  constexpr uint32_t kThreads = kBigGWaves * kWave;
+  const uint32_t tid = threadIdx.x;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid / kWave);
+  const int lane = tid & (kWave - 1);
+  const uint32_t n = gload(P.defer_count, 0);
+  // the listed blocks of this workgroup that fit a stage, in list order
+  auto next_fit = [&](uint32_t li) -> BigBlk {
+    for (;; li += gridDim.x) {
+      if (li >= n) {
+        BigBlk z{};
+        z.li = li;
+        z.fits = false;
+        return z;
+      }
+      const BigBlk x = big_blk(P, li);
+      if (x.fits) return x;
+      if (tid == 0) defer2_block(P, x.b);  // (workgroup-uniform)
+    }
+  };
+  auto issue_dma = [&](const BigBlk& x, uint8_t* dst) {  // wave w moves 1-KiB pieces w, w + 8, ...
+    const uint32_t chunks = (uint32_t)((x.span1 - x.span0) >> 4);
+    const uint8_t* src = P.blocks + x.span0 + 16 * lane;
+    for (uint32_t c = wave; c * kWave < chunks; c += kBigGWaves)
+      if (c * kWave + lane < chunks)
+        __builtin_amdgcn_global_load_lds((gbl_void_t*)(src + 1024 * c), (lds_void_t*)(dst + 1024 * c), 16, 0, 0);
+  };
+  BigBlk X = next_fit(blockIdx.x);
+  if (X.fits) issue_dma(X, stages);
+  while (X.fits) {
+    uint8_t* stage = stages;
+    const uint32_t b = X.b, n_items = X.it1 - X.it0;
+    DEC_PHASE(7);
+    vm_wait<0>();  // this block's stage (and every earlier store)
+    lds_barrier();
+    DEC_PHASE(0);
+    for (uint32_t x = tid; x <= n_items; x += kThreads) rec[x] = 0;
+    lds_barrier();
+    DEC_PHASE(0);
+    // wave 0: header, trailer, then phase A over every restart interval;
+    // waves 1..: the per-KiB XXH3 contributions of the payload as the handle
+    // gives it (they count only if the header agrees: data_length == handle - 33)
+    const uint32_t hb = (uint32_t)(X.off - X.span0);
+    const uint64_t hlen = X.end - X.off;
+    if (wave == 0) {
+      if (lane == 0) {
+        BlockMeta m;
+        meta_header_fields(stage, hb, hlen, m);
+        m.item0 = 0;
+        m.hdr_st = m.st;
+        m.ck_bad = 0;
+        m.hck_bad = 0;
+        meta_trailer(stage, P.expect_type, n_items, m);
+        if (m.st == ST_OK && m.type == 1) m.st = ST_DEFER;  // index blocks: general path
+        m.chain0 = 0;
+        meta[0] = m;
+      }
+      wave_sync();
+      const uint32_t total = meta[0].st == ST_OK ? meta[0].bin_len : 0;
+      for (uint32_t r = lane; r < total; r += kWave) owner[r] = 0;
+      wave_sync();
+      phase_a<true>(stage, meta, owner, rec, 0, kWave, total, kBigGTile);
+    } else if (!(P.flags & LSM_DECODE_PAYLOAD_VERIFIED) && hlen > kHdrLen + 240) {
+      xxh3_kib_contribs(stage, hb + kHdrLen, (uint32_t)hlen - kHdrLen, &kLongSecret, contrib, wave - 1,
+                        kBigGWaves - 1);
+    }
+    lds_barrier();
+    DEC_PHASE(3);
+    const BigBlk Xn = next_fit(X.li + gridDim.x);
+    const bool hash = meta[0].hdr_st == ST_OK && !(P.flags & LSM_DECODE_PAYLOAD_VERIFIED) &&
+                      !(kDiagBuild && (P.flags & kDiagSkipHash));
+    const uint32_t plen = meta[0].len - kHdrLen;
+    if (wave == kBigGWaves - 1) {  // the serial chain + tail, and the header checksum ...
+      if (hash) {
+        // the chain is this block's critical path: ahead of the phase-B waves on its SIMD
+        __builtin_amdgcn_s_setprio(3);
+        uint64_t lo, hi;
+        if (plen > 240) xxh3_128_wave_finish(stage, hb + kHdrLen, plen, &kLongSecret, contrib, lo, hi);
+        else xxh3_128_wave(stage, hb + kHdrLen, plen, &kLongSecret, lo, hi);
+        const bool hck = header_cksum_ok(stage, hb);
+        if (lane == 0) {
+          meta[0].ck_bad = lo != meta[0].ck_lo || hi != meta[0].ck_hi;
+          meta[0].hck_bad = !hck;
+        }
+        __builtin_amdgcn_s_setprio(0);
+      }
+    } else if (!(kDiagBuild && (P.flags & kDiagSkipPhaseB))) {  // ... while the other waves run phase B
+      phase_b<kAllFields, true>(P, stage, meta, rec, n_items, X.it0, tid, (kBigGWaves - 1) * kWave);
+    }
+    lds_barrier();
+    DEC_PHASE(4);
+    if (tid == 0) {
+      const BlockMeta& m = meta[0];
+      const int32_t st = m.hdr_st != ST_OK ? m.hdr_st
+                         : m.hck_bad ? (int32_t)ST_HDR_CKSUM
+                         : m.ck_bad  ? (int32_t)ST_CKSUM
+                                     : m.st;
+      if (st == ST_DEFER) defer2_block(P, b);
+      else gstore(P.status, b, st);
+    }
+    lds_barrier();  // (meta / rec / owner are rewritten for the next block)
+    DEC_PHASE(5);
+    if (Xn.fits) issue_dma(Xn, stages);
+    DEC_PHASE(6);
+#ifdef LSM_DIAG
+    ++nblk;
+#endif
+    X = Xn;
+  }
+#ifdef LSM_DIAG
+  if (tid == 0) {
+    for (int i = 0; i < 8; ++i) atomicAdd(&g_dec_phase[i], (unsigned long long)ph[i]);
+    atomicAdd(&g_dec_phase[15], (unsigned long long)nblk);
+  }
+#endif
+}
+
 // Workgroup = kGroupWaves waves sharing one LDS stage (default 32 KiB: eight
 // 4-KiB blocks, ~32 restart intervals).  Per group:
 //   all waves   LDS-DMA of the span (wave w moves 1-KiB pieces w, w+4, ...)
@@ -843,7 +1059,7 @@ static size_t tiles_bytes(uint32_t n_blocks) { return (scan_tiles(n_blocks) * 8 
 static size_t defer_bytes(uint32_t n_blocks) { return ((size_t)n_blocks * 4 + 256 + 255) / 256 * 256; }
 
 size_t decode_workspace_size(uint32_t n_blocks) {
-  return counts_bytes(n_blocks) + tiles_bytes(n_blocks) + defer_bytes(n_blocks);
+  return counts_bytes(n_blocks) + tiles_bytes(n_blocks) + 2 * defer_bytes(n_blocks);
 }
 
 uint32_t decode_lds_bytes(uint32_t stage_bytes, uint32_t tile_items, uint32_t blocks_per_wave) {
@@ -859,8 +1075,12 @@ hipError_t launch_decode(const DecodeParams& P0, void* ws, hipStream_t st) {
   uint8_t* dws = (uint8_t*)ws + counts_bytes(P.n_blocks) + tiles_bytes(P.n_blocks);
   P.defer_count = (uint32_t*)dws;
   P.defer_list = (uint32_t*)(dws + 256);
+  uint8_t* dws2 = dws + defer_bytes(P.n_blocks);
+  P.defer2_count = (uint32_t*)dws2;
+  P.defer2_list = (uint32_t*)(dws2 + 256);
   hipError_t e = hipMemsetAsync(P.defer_count, 0, 4, st);
   if (e != hipSuccess) return e;
+  if ((e = hipMemsetAsync(P.defer2_count, 0, 4, st)) != hipSuccess) return e;
   if (!(P.flags & LSM_DECODE_ITEM_START_VALID)) {
     hipLaunchKernelGGL(trailer_counts_kernel, dim3((P.n_blocks + 255) / 256), dim3(256), 0, st, P.blocks,
                        P.block_off, P.n_blocks, counts);
@@ -880,14 +1100,48 @@ hipError_t launch_decode(const DecodeParams& P0, void* ws, hipStream_t st) {
     hipLaunchKernelGGL((decode_blocks_kernel<true>), dim3(grid), dim3(kGroupWaves * kWave), lds, st, P);
   else
     hipLaunchKernelGGL((decode_blocks_kernel<false>), dim3(grid), dim3(kGroupWaves * kWave), lds, st, P);
+  // listed blocks: the big-block kernel (two workgroups per CU), then the
+  // general path for what it hands on (its list read as defer_count / defer_list)
+  static int cu_count[64] = {};  // per device (benign race: every writer stores the same count)
+  int dev = 0;
+  if ((e = hipGetDevice(&dev)) != hipSuccess) return e;
+  int n_cu = dev < 64 ? __atomic_load_n(&cu_count[dev], __ATOMIC_RELAXED) : 0;
+  if (!n_cu) {
+    if ((e = hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess) return e;
+    if (dev < 64) __atomic_store_n(&cu_count[dev], n_cu, __ATOMIC_RELAXED);
+  }
+  const uint32_t bgrid = min(P.n_blocks, (uint32_t)n_cu * kBigGPerCU);
+  if (bgrid) {
+    static uint64_t done_bg_all = 0, done_bg_some = 0;
+    e = all ? set_lds_attr((const void*)decode_big_kernel<true>, kBigGLds, &done_bg_all)
+            : set_lds_attr((const void*)decode_big_kernel<false>, kBigGLds, &done_bg_some);
+    if (e != hipSuccess) return e;
+    if (all)
+      hipLaunchKernelGGL((decode_big_kernel<true>), dim3(bgrid), dim3(kBigGWaves * kWave), kBigGLds, st, P);
+    else
+      hipLaunchKernelGGL((decode_big_kernel<false>), dim3(bgrid), dim3(kBigGWaves * kWave), kBigGLds, st, P);
+  }
   const uint32_t dgrid = P.n_blocks < 1024 ? P.n_blocks : 1024;
   if (dgrid) {
+    DecodeParams P2 = P;
+    P2.defer_count = P.defer2_count;
+    P2.defer_list = P.defer2_list;
     static uint64_t done_big = 0;
     const uint32_t big = kBigStageOff + kBigStage + kStagePad;
     if ((e = set_lds_attr((const void*)decode_deferred_staged_kernel, big, &done_big)) != hipSuccess) return e;
-    hipLaunchKernelGGL(decode_deferred_staged_kernel, dim3(dgrid), dim3(kBigWaves * kWave), big, st, P);
+    hipLaunchKernelGGL(decode_deferred_staged_kernel, dim3(dgrid), dim3(kBigWaves * kWave), big, st, P2);
   }
   return hipGetLastError();
 }
 
 }  // namespace lsmgpu
+
+#ifdef LSM_DIAG
+// Diagnostic builds only: copy out and clear the big-block kernel's phase totals.
+extern "C" int lsm_diag_decode_phases(uint64_t* out16) {
+  if (hipDeviceSynchronize() != hipSuccess) return -1;
+  if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(lsmgpu::g_dec_phase), 16 * sizeof(uint64_t)) != hipSuccess) return -1;
+  static const uint64_t z[16] = {};
+  return hipMemcpyToSymbol(HIP_SYMBOL(lsmgpu::g_dec_phase), z, sizeof(z)) == hipSuccess ? 0 : -1;
+}
+#endif

@@ -28,8 +28,10 @@ struct DecodeParams {
   uint32_t stage_bytes;
   uint32_t tile_items;
   uint32_t flags;
-  uint32_t* defer_count;  // workspace: blocks handed to the general path
+  uint32_t* defer_count;  // workspace: blocks the group kernel hands on (large / lone blocks, index blocks, rare shapes)
   uint32_t* defer_list;
+  uint32_t* defer2_count;  // workspace: blocks decode_big_kernel hands on to the general path
+  uint32_t* defer2_list;
   uint64_t seqno_add;     // added to every decoded seqno (Scanner's global_seqno, scanner.rs:84)
 };
 

@@ -487,15 +487,26 @@ __device__ __forceinline__ void xxh3_kib_contribs(const uint8_t* base, uint32_t 
   const int q = lane & 3, s = lane >> 2;
   const uint64_t k0 = ls->acc[s + 2 * q], k1 = ls->acc[s + 2 * q + 1];
   const uint32_t nb_blocks = (len - 1) / 1024;
-  for (uint32_t n = w; n < nb_blocks; n += nw) {
-    const Win16 win = read_win16(base, pos + n * 1024 + 16 * lane);
-    uint64_t c0 = 0, c1 = 0;
-    stripe_part(win, k0, k1, c0, c1);
+  // two KiB blocks per step (both windows read before either is reduced)
+  for (uint32_t n = w; n < nb_blocks; n += 2 * nw) {
+    const bool two = n + nw < nb_blocks;
+    const Win16 wa = read_win16(base, pos + n * 1024 + 16 * lane);
+    Win16 wb = {0, 0};
+    if (two) wb = read_win16(base, pos + (n + nw) * 1024 + 16 * lane);
+    uint64_t c0 = 0, c1 = 0, d0 = 0, d1 = 0;
+    stripe_part(wa, k0, k1, c0, c1);
+    stripe_part(wb, k0, k1, d0, d1);
     c0 = quad_group_sum64(c0);
     c1 = quad_group_sum64(c1);
+    d0 = quad_group_sum64(d0);
+    d1 = quad_group_sum64(d1);
     if (lane < 4) {
       contrib[8 * n + 2 * q] = c0;
       contrib[8 * n + 2 * q + 1] = c1;
+      if (two) {
+        contrib[8 * (n + nw) + 2 * q] = d0;
+        contrib[8 * (n + nw) + 2 * q + 1] = d1;
+      }
     }
   }
 }
@@ -511,11 +522,26 @@ __device__ __forceinline__ void xxh3_128_wave_finish(const uint8_t* base, uint32
   uint64_t a1 = q == 0 ? P64_1 : q == 1 ? P64_3 : q == 2 ? (uint64_t)P32_2 : (uint64_t)P32_1;
   const uint64_t scr0 = ls->acc[16 + 2 * q], scr1 = ls->acc[16 + 2 * q + 1];
   const uint32_t nb_blocks = (len - 1) / 1024;
-  for (uint32_t n = 0; n < nb_blocks; ++n) {
-    a0 += contrib[8 * n + 2 * q];
-    a0 ^= a0 >> 47; a0 ^= scr0; a0 *= P32_1;
-    a1 += contrib[8 * n + 2 * q + 1];
-    a1 ^= a1 >> 47; a1 ^= scr1; a1 *= P32_1;
+  // the serial chain: eight KiB blocks' contributions read ahead of their steps
+  for (uint32_t n0 = 0; n0 < nb_blocks; n0 += 8) {
+    uint64_t c0[8], c1[8];
+#pragma unroll
+    for (uint32_t t = 0; t < 8; ++t) {
+      c0[t] = c1[t] = 0;
+      if (n0 + t < nb_blocks) {
+        c0[t] = contrib[8 * (n0 + t) + 2 * q];
+        c1[t] = contrib[8 * (n0 + t) + 2 * q + 1];
+      }
+    }
+#pragma unroll
+    for (uint32_t t = 0; t < 8; ++t) {
+      if (n0 + t < nb_blocks) {
+        a0 += c0[t];
+        a0 ^= a0 >> 47; a0 ^= scr0; a0 *= P32_1;
+        a1 += c1[t];
+        a1 ^= a1 >> 47; a1 ^= scr1; a1 *= P32_1;
+      }
+    }
   }
   {
     const uint32_t tail0 = nb_blocks * 1024;

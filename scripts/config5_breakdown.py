@@ -21,7 +21,7 @@ def main():
         enc = lsmgpu.Encoder().encode(items, starts, nb)
         torch.cuda.synchronize()
         total = int(enc["block_off"][nb].item())
-        for tun in (None, (0, 0, 0, 1 | 0x10000)):
+        for tun in (None, (0, 0, 0, lsmgpu.DECODE_ITEM_START_VALID)):
             dec = lsmgpu.Decoder()
             out = dec.alloc_outputs(n, nb, fields=bench.DATA_FIELDS)
             dec.decode(enc["buf"], enc["block_off"], nb, out, n)
