@@ -515,6 +515,15 @@ __device__ __forceinline__ void decode_block_direct(const DecodeParams& P, uint3
 typedef __attribute__((address_space(3))) void lds_void_t;
 typedef const __attribute__((address_space(1))) void gbl_void_t;
 
+// Blocks whose span exceeds this go to the big-block kernel: those larger
+// than the stage.  (Half the stage measured slower: the 17 KB blocks of the
+// 16 KiB random-key class run at 0.82 TB/s through the big-block kernel, one
+// block per iteration, and at 1.42 TB/s here, one block per group.)
+#ifndef LSM_LONE_DIV
+#define LSM_LONE_DIV 1
+#endif
+__device__ __forceinline__ uint32_t lone_bytes(const DecodeParams& P) { return P.stage_bytes / LSM_LONE_DIV; }
+
 // A group: the longest run of consecutive blocks from b that fits the stage
 // (k == 0: block b alone is too large and takes the direct path).  Lane j of
 // every wave holds block b+j's handle and item range.
@@ -543,7 +552,7 @@ __device__ __forceinline__ Group form_group(const DecodeParams& P, uint32_t b, u
   G.g_item0 = wave_readlane_u32(G.it0_j, 0);
   G.span0 = off_b & ~15ULL;
   // lone blocks (lone_block) never join a group: they are listed for the general path up front
-  const bool lone = ((G.end_j + 15) & ~15ULL) - (G.off_j & ~15ULL) > P.stage_bytes ||
+  const bool lone = ((G.end_j + 15) & ~15ULL) - (G.off_j & ~15ULL) > lone_bytes(P) ||
                     G.it1_j - G.it0_j > P.tile_items;
   const bool fits = in_run && !lone && G.end_j >= G.off_j && G.off_j >= off_b &&
                     ((G.end_j + 15) & ~15ULL) - G.span0 <= P.stage_bytes && G.it1_j - G.g_item0 <= P.tile_items;
@@ -928,7 +937,7 @@ __global__ __launch_bounds__(kGroupWaves * kWave) __attribute__((amdgpu_waves_pe
     const uint64_t nx = wave_shfl_u64(offr, min(lane + 1, kWave - 1));
     const uint32_t ix = (uint32_t)__shfl((int)itr, min(lane + 1, kWave - 1));
     const bool in = b_begin + lane < b_end;
-    const bool lone = in && (((nx + 15) & ~15ULL) - (offr & ~15ULL) > P.stage_bytes || ix - itr > P.tile_items);
+    const bool lone = in && (((nx + 15) & ~15ULL) - (offr & ~15ULL) > lone_bytes(P) || ix - itr > P.tile_items);
     defer_blocks_wave(P, lone, b_begin + lane);
   }
   Group G = next_group(b_begin);
