@@ -110,8 +110,8 @@ __global__ __launch_bounds__(64) void xxh3_file_finish_kernel(const uint8_t* __r
 #pragma unroll 8
     for (uint32_t u = 0; u < kChunk; ++u) {
       const uint64_t c0 = st[8 * u + 2 * q], c1 = st[8 * u + 2 * q + 1];
-      a0 += c0; a0 ^= a0 >> 47; a0 ^= scr0; a0 *= P32_1;
-      a1 += c1; a1 ^= a1 >> 47; a1 ^= scr1; a1 *= P32_1;
+      a0 = xxh3_scr(a0, c0, scr0);
+      a1 = xxh3_scr(a1, c1, scr1);
     }
     __syncthreads();
   }
@@ -125,13 +125,13 @@ __global__ __launch_bounds__(64) void xxh3_file_finish_kernel(const uint8_t* __r
     }
 #pragma unroll
     for (int u = 0; u < 4; ++u) {
-      a0 += c[2 * u]; a0 ^= a0 >> 47; a0 ^= scr0; a0 *= P32_1;
-      a1 += c[2 * u + 1]; a1 ^= a1 >> 47; a1 ^= scr1; a1 *= P32_1;
+      a0 = xxh3_scr(a0, c[2 * u], scr0);
+      a1 = xxh3_scr(a1, c[2 * u + 1], scr1);
     }
   }
   for (; n < nb; ++n) {
-    a0 += contrib[8 * n + 2 * q]; a0 ^= a0 >> 47; a0 ^= scr0; a0 *= P32_1;
-    a1 += contrib[8 * n + 2 * q + 1]; a1 ^= a1 >> 47; a1 ^= scr1; a1 *= P32_1;
+    a0 = xxh3_scr(a0, contrib[8 * n + 2 * q], scr0);
+    a1 = xxh3_scr(a1, contrib[8 * n + 2 * q + 1], scr1);
   }
   {  // tail stripes of the last (partial) KiB block, then the last stripe (secret + 121)
     const uint64_t tail0 = nb * 1024;

@@ -671,14 +671,15 @@ __global__ __launch_bounds__(kBigWaves * kWave) void decode_deferred_staged_kern
 
 // Large blocks (SURVEY configs[4]: 16 / 64 KiB data blocks) listed by the
 // group kernel: persistent 8-wave workgroups, two per CU (one stage each:
-// the other workgroup's decode overlaps this one's DMA).  Per block:
-//   all waves   LDS-DMA of the block
+// the other workgroup's decode overlaps this one's DMA).  Per block, after
+// the LDS-DMA, three concurrent streams hand off through LDS flags:
 //   wave 0      header fields and trailer (lane 0), then phase A over every
-//               restart interval (lane = interval) ...
-//   waves 1..7  ... while these compute the per-KiB XXH3 contributions
-//   wave 7      the serial XXH3 scramble chain + tail, the header checksum
-//               (at raised priority: it is the block's critical path) ...
-//   waves 0..6  ... while these run phase B (thread = record)
+//               restart interval (lane = interval), then phase B
+//   waves 1..6  the per-KiB XXH3 contributions, each published as it is
+//               done, then phase B once phase A has finished
+//   wave 7      the serial XXH3 scramble chain over the contributions as they
+//               arrive, the tail and the header checksum (raised priority:
+//               it is the block's critical path)
 // Blocks larger than the stage, with more items than kBigGTile, index blocks
 // and rare record shapes go on to the general path (defer2 list).
 #ifndef LSM_BIG_WAVES
@@ -691,7 +692,16 @@ constexpr uint32_t kBigGTile = 832;
 constexpr uint32_t kBigGRec = ((kBigGTile + 1) * 8 + 15) & ~15u;
 constexpr uint32_t kBigGContrib = (kBigGStage / 1024 + 1) * 64;
 constexpr uint32_t kBigGOwner = (kBigGTile + 15) & ~15u;
-constexpr uint32_t kBigGLds = 80 + kBigGRec + kBigGOwner + kBigGContrib + kBigGSlot;
+// Cross-wave hand-offs of one block (tags: the block's list index + 1, so
+// nothing is reset between blocks).
+struct BigSync {
+  uint32_t a_done;  // phase A finished
+  uint32_t hck;     // header checksum ok (chain wave)
+  uint64_t lo, hi;  // payload xxh3_128 (chain wave)
+  uint32_t ready[kBigGStage / 1024 + 1];  // KiB block n's contribution published
+};
+constexpr uint32_t kBigGSync = (sizeof(BigSync) + 15) & ~15u;
+constexpr uint32_t kBigGLds = 80 + kBigGSync + kBigGRec + kBigGOwner + kBigGContrib + kBigGSlot;
 constexpr uint32_t kBigGPerCU = 2;
 static_assert(kBigGLds * kBigGPerCU <= 160 * 1024, "big-block workgroups per CU");
 
@@ -742,10 +752,11 @@ __global__ __launch_bounds__(kBigGWaves * kWave) void decode_big_kernel(DecodePa
 #endif
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   BlockMeta* meta = reinterpret_cast<BlockMeta*>(smem);
-  uint64_t* rec = reinterpret_cast<uint64_t*>(smem + 80);
-  uint8_t* owner = smem + 80 + kBigGRec;
-  uint64_t* contrib = reinterpret_cast<uint64_t*>(smem + 80 + kBigGRec + kBigGOwner);
-  uint8_t* stages = smem + 80 + kBigGRec + kBigGOwner + kBigGContrib;
+  BigSync* sync = reinterpret_cast<BigSync*>(smem + 80);
+  uint64_t* rec = reinterpret_cast<uint64_t*>(smem + 80 + kBigGSync);
+  uint8_t* owner = smem + 80 + kBigGSync + kBigGRec;
+  uint64_t* contrib = reinterpret_cast<uint64_t*>(smem + 80 + kBigGSync + kBigGRec + kBigGOwner);
+  uint8_t* stages = smem + 80 + kBigGSync + kBigGRec + kBigGOwner + kBigGContrib;
   constexpr uint32_t kThreads = kBigGWaves * kWave;
   const uint32_t tid = threadIdx.x;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(tid / kWave);
@@ -772,80 +783,90 @@ __global__ __launch_bounds__(kBigGWaves * kWave) void decode_big_kernel(DecodePa
       if (c * kWave + lane < chunks)
         __builtin_amdgcn_global_load_lds((gbl_void_t*)(src + 1024 * c), (lds_void_t*)(dst + 1024 * c), 16, 0, 0);
   };
+  for (uint32_t x = tid; x < kBigGStage / 1024 + 1; x += kThreads) sync->ready[x] = 0;
+  if (tid == 0) sync->a_done = 0;
   BigBlk X = next_fit(blockIdx.x);
   if (X.fits) issue_dma(X, stages);
   while (X.fits) {
     uint8_t* stage = stages;
     const uint32_t b = X.b, n_items = X.it1 - X.it0;
+    const uint32_t tag = X.li + 1;  // this block's publication tag (list indices only grow)
+    for (uint32_t x = tid; x <= n_items; x += kThreads) rec[x] = 0;
     DEC_PHASE(7);
     vm_wait<0>();  // this block's stage (and every earlier store)
     lds_barrier();
     DEC_PHASE(0);
-    for (uint32_t x = tid; x <= n_items; x += kThreads) rec[x] = 0;
-    lds_barrier();
-    DEC_PHASE(0);
-    // wave 0: header, trailer, then phase A over every restart interval;
-    // waves 1..: the per-KiB XXH3 contributions of the payload as the handle
-    // gives it (they count only if the header agrees: data_length == handle - 33)
     const uint32_t hb = (uint32_t)(X.off - X.span0);
     const uint64_t hlen = X.end - X.off;
-    if (wave == 0) {
-      if (lane == 0) {
-        BlockMeta m;
-        meta_header_fields(stage, hb, hlen, m);
-        m.item0 = 0;
-        m.hdr_st = m.st;
-        m.ck_bad = 0;
-        m.hck_bad = 0;
-        meta_trailer(stage, P.expect_type, n_items, m);
-        if (m.st == ST_OK && m.type == 1) m.st = ST_DEFER;  // index blocks: general path
-        m.chain0 = 0;
-        meta[0] = m;
-      }
-      wave_sync();
-      const uint32_t total = meta[0].st == ST_OK ? meta[0].bin_len : 0;
-      for (uint32_t r = lane; r < total; r += kWave) owner[r] = 0;
-      wave_sync();
-      phase_a<true>(stage, meta, owner, rec, 0, kWave, total, kBigGTile);
-    } else if (!(P.flags & LSM_DECODE_PAYLOAD_VERIFIED) && hlen > kHdrLen + 240) {
-      xxh3_kib_contribs(stage, hb + kHdrLen, (uint32_t)hlen - kHdrLen, &kLongSecret, contrib, wave - 1,
-                        kBigGWaves - 1);
-    }
-    lds_barrier();
-    DEC_PHASE(3);
-    const BigBlk Xn = next_fit(X.li + gridDim.x);
-    const bool hash = meta[0].hdr_st == ST_OK && !(P.flags & LSM_DECODE_PAYLOAD_VERIFIED) &&
-                      !(kDiagBuild && (P.flags & kDiagSkipHash));
-    const uint32_t plen = meta[0].len - kHdrLen;
-    if (wave == kBigGWaves - 1) {  // the serial chain + tail, and the header checksum ...
+    // the payload checksum as the handle gives it: it counts only if the
+    // header's fields check out (then data_length == handle - 33)
+    const bool hash = !(P.flags & LSM_DECODE_PAYLOAD_VERIFIED) && !(kDiagBuild && (P.flags & kDiagSkipHash)) &&
+                      hlen >= kHdrLen;
+    const uint32_t plen = hash ? (uint32_t)hlen - kHdrLen : 0;
+    if (wave == kBigGWaves - 1) {
+      // the serial XXH3 chain, consuming the contributions as waves 1.. publish
+      // them, then the tail and the header checksum (raised priority: the
+      // chain is the block's critical path)
       if (hash) {
-        // the chain is this block's critical path: ahead of the phase-B waves on its SIMD
         __builtin_amdgcn_s_setprio(3);
         uint64_t lo, hi;
-        if (plen > 240) xxh3_128_wave_finish(stage, hb + kHdrLen, plen, &kLongSecret, contrib, lo, hi);
+        if (plen > 240) xxh3_128_wave_finish(stage, hb + kHdrLen, plen, &kLongSecret, contrib, lo, hi, sync->ready, tag);
         else xxh3_128_wave(stage, hb + kHdrLen, plen, &kLongSecret, lo, hi);
         const bool hck = header_cksum_ok(stage, hb);
         if (lane == 0) {
-          meta[0].ck_bad = lo != meta[0].ck_lo || hi != meta[0].ck_hi;
-          meta[0].hck_bad = !hck;
+          sync->lo = lo;
+          sync->hi = hi;
+          sync->hck = hck;
         }
         __builtin_amdgcn_s_setprio(0);
       }
-    } else if (!(kDiagBuild && (P.flags & kDiagSkipPhaseB))) {  // ... while the other waves run phase B
-      phase_b<kAllFields, true>(P, stage, meta, rec, n_items, X.it0, tid, (kBigGWaves - 1) * kWave);
+    } else {
+      if (wave == 0) {  // header, trailer, then phase A over every restart interval
+        if (lane == 0) {
+          BlockMeta m;
+          meta_header_fields(stage, hb, hlen, m);
+          m.item0 = 0;
+          m.hdr_st = m.st;
+          m.ck_bad = 0;
+          m.hck_bad = 0;
+          meta_trailer(stage, P.expect_type, n_items, m);
+          if (m.st == ST_OK && m.type == 1) m.st = ST_DEFER;  // index blocks: general path
+          m.chain0 = 0;
+          meta[0] = m;
+        }
+        wave_sync();
+        const uint32_t total = meta[0].st == ST_OK ? meta[0].bin_len : 0;
+        for (uint32_t r = lane; r < total; r += kWave) owner[r] = 0;
+        wave_sync();
+        phase_a<true>(stage, meta, owner, rec, 0, kWave, total, kBigGTile);
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+        if (lane == 0) __hip_atomic_store(&sync->a_done, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      } else {  // the per-KiB contributions, then wait for phase A
+        if (hash && plen > 240)
+          xxh3_kib_contribs(stage, hb + kHdrLen, plen, &kLongSecret, contrib, wave - 1, kBigGWaves - 2, sync->ready,
+                            tag);
+        while (__hip_atomic_load(&sync->a_done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) != tag)
+          __builtin_amdgcn_s_sleep(1);
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+      }
+      // phase B on waves 0 .. kBigGWaves - 2, under the chain
+      if (!(kDiagBuild && (P.flags & kDiagSkipPhaseB)))
+        phase_b<kAllFields, true>(P, stage, meta, rec, n_items, X.it0, tid, (kBigGWaves - 1) * kWave);
     }
     lds_barrier();
     DEC_PHASE(4);
-    if (tid == 0) {
+    const BigBlk Xn = next_fit(X.li + gridDim.x);
+    if (tid == 0) {  // statuses in oracle order: header, header checksum, payload checksum, trailer / parse
       const BlockMeta& m = meta[0];
-      const int32_t st = m.hdr_st != ST_OK ? m.hdr_st
-                         : m.hck_bad ? (int32_t)ST_HDR_CKSUM
-                         : m.ck_bad  ? (int32_t)ST_CKSUM
-                                     : m.st;
+      const bool chk = hash && m.hdr_st == ST_OK;
+      const int32_t st = m.hdr_st != ST_OK                              ? m.hdr_st
+                         : (chk && !sync->hck)                          ? (int32_t)ST_HDR_CKSUM
+                         : (chk && (sync->lo != m.ck_lo || sync->hi != m.ck_hi)) ? (int32_t)ST_CKSUM
+                                                                         : m.st;
       if (st == ST_DEFER) defer2_block(P, b);
       else gstore(P.status, b, st);
     }
-    lds_barrier();  // (meta / rec / owner are rewritten for the next block)
+    lds_barrier();  // (meta / rec / owner / the stage are rewritten for the next block)
     DEC_PHASE(5);
     if (Xn.fits) issue_dma(Xn, stages);
     DEC_PHASE(6);

@@ -47,6 +47,19 @@ enum : int32_t {
 
 // ---------------------------------------------------------------- XXH3 consts
 constexpr uint32_t P32_1 = 0x9E3779B1U, P32_2 = 0x85EBCA77U, P32_3 = 0xC2B2AE3DU;
+
+// One XXH3 accumulator step of the long loop's scramble (XXH3_scrambleAcc)
+// after adding the KiB block's contribution c: x = a + c;
+// ((x ^ (x >> 47)) ^ s) * PRIME32_1.  x >> 47 < 2^17 only touches the low
+// word, and the multiply by a 32-bit prime is one 32x32+64 mad: a short
+// dependent chain for the serial per-KiB scramble.
+__host__ __device__ __forceinline__ uint64_t xxh3_scr(uint64_t a, uint64_t c, uint64_t s) {
+  const uint64_t x = a + c;
+  const uint32_t hi = (uint32_t)(x >> 32);
+  const uint32_t lo = (uint32_t)x ^ (hi >> 15) ^ (uint32_t)s;
+  const uint32_t hs = hi ^ (uint32_t)(s >> 32);
+  return (uint64_t)lo * P32_1 + ((uint64_t)(hs * P32_1) << 32);
+}
 constexpr uint64_t P64_1 = 0x9E3779B185EBCA87ULL, P64_2 = 0xC2B2AE3D27D4EB4FULL,
                    P64_3 = 0x165667B19E3779F9ULL, P64_4 = 0x85EBCA77C2B2AE63ULL,
                    P64_5 = 0x27D4EB2F165667C5ULL, PMX1 = 0x165667919E3779F9ULL,
@@ -435,10 +448,10 @@ __device__ __forceinline__ void xxh3_128_wave_long(const uint8_t* base, uint32_t
     c1 = quad_group_sum64(c1);
     d0 = quad_group_sum64(d0);
     d1 = quad_group_sum64(d1);
-    a0 += c0; a0 ^= a0 >> 47; a0 ^= scr0; a0 *= P32_1;
-    a1 += c1; a1 ^= a1 >> 47; a1 ^= scr1; a1 *= P32_1;
-    a0 += d0; a0 ^= a0 >> 47; a0 ^= scr0; a0 *= P32_1;
-    a1 += d1; a1 ^= a1 >> 47; a1 ^= scr1; a1 *= P32_1;
+    a0 = xxh3_scr(a0, c0, scr0);
+    a1 = xxh3_scr(a1, c1, scr1);
+    a0 = xxh3_scr(a0, d0, scr0);
+    a1 = xxh3_scr(a1, d1, scr1);
   }
   if (n < nb_blocks) {
     const Win16 w = read_win16(base, pos + n * 1024 + 16 * lane);
@@ -446,8 +459,8 @@ __device__ __forceinline__ void xxh3_128_wave_long(const uint8_t* base, uint32_t
     stripe_part(w, k0, k1, c0, c1);
     c0 = quad_group_sum64(c0);
     c1 = quad_group_sum64(c1);
-    a0 += c0; a0 ^= a0 >> 47; a0 ^= scr0; a0 *= P32_1;
-    a1 += c1; a1 ^= a1 >> 47; a1 ^= scr1; a1 *= P32_1;
+    a0 = xxh3_scr(a0, c0, scr0);
+    a1 = xxh3_scr(a1, c1, scr1);
   }
   {
     const uint32_t tail0 = nb_blocks * 1024;
@@ -480,9 +493,11 @@ __device__ __forceinline__ void xxh3_128_wave_long(const uint8_t* base, uint32_t
 // wave w of nw reduces KiB blocks w, w + nw, ... into contrib[8 n ..] (LDS);
 // after a workgroup barrier one wave runs the serial scramble chain over
 // them and the tail (xxh3_128_wave_finish).  len > 240.
+// With `ready`, KiB block n's contribution is published to a concurrent
+// xxh3_128_wave_finish by ready[n] = tag (LDS, workgroup release).
 __device__ __forceinline__ void xxh3_kib_contribs(const uint8_t* base, uint32_t pos, uint32_t len,
                                                   const LongSecret* __restrict__ ls, uint64_t* contrib, uint32_t w,
-                                                  uint32_t nw) {
+                                                  uint32_t nw, uint32_t* ready = nullptr, uint32_t tag = 0) {
   const int lane = threadIdx.x & 63;
   const int q = lane & 3, s = lane >> 2;
   const uint64_t k0 = ls->acc[s + 2 * q], k1 = ls->acc[s + 2 * q + 1];
@@ -508,12 +523,22 @@ __device__ __forceinline__ void xxh3_kib_contribs(const uint8_t* base, uint32_t 
         contrib[8 * (n + nw) + 2 * q + 1] = d1;
       }
     }
+    if (ready) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+      if (lane == 0) {
+        __hip_atomic_store(&ready[n], tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        if (two) __hip_atomic_store(&ready[n + nw], tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+    }
   }
 }
 
+// With `ready`, the chain consumes the contributions as xxh3_kib_contribs
+// publishes them (waits for ready[n] == tag).
 __device__ __forceinline__ void xxh3_128_wave_finish(const uint8_t* base, uint32_t pos, uint32_t len,
                                                      const LongSecret* __restrict__ ls, const uint64_t* contrib,
-                                                     uint64_t& out_lo, uint64_t& out_hi) {
+                                                     uint64_t& out_lo, uint64_t& out_hi,
+                                                     const uint32_t* ready = nullptr, uint32_t tag = 0) {
   const int lane = threadIdx.x & 63;
   const int q = lane & 3;
   const int s = lane >> 2;
@@ -525,6 +550,18 @@ __device__ __forceinline__ void xxh3_128_wave_finish(const uint8_t* base, uint32
   // the serial chain: eight KiB blocks' contributions read ahead of their steps
   for (uint32_t n0 = 0; n0 < nb_blocks; n0 += 8) {
     uint64_t c0[8], c1[8];
+    if (ready) {  // (every lane reads the same flags: the loop is wave-uniform)
+      for (;;) {
+        bool all = true;
+#pragma unroll
+        for (uint32_t t = 0; t < 8; ++t)
+          if (n0 + t < nb_blocks)
+            all &= __hip_atomic_load(&ready[n0 + t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == tag;
+        if (all) break;
+        __builtin_amdgcn_s_sleep(1);
+      }
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
+    }
 #pragma unroll
     for (uint32_t t = 0; t < 8; ++t) {
       c0[t] = c1[t] = 0;
@@ -536,10 +573,8 @@ __device__ __forceinline__ void xxh3_128_wave_finish(const uint8_t* base, uint32
 #pragma unroll
     for (uint32_t t = 0; t < 8; ++t) {
       if (n0 + t < nb_blocks) {
-        a0 += c0[t];
-        a0 ^= a0 >> 47; a0 ^= scr0; a0 *= P32_1;
-        a1 += c1[t];
-        a1 ^= a1 >> 47; a1 ^= scr1; a1 *= P32_1;
+        a0 = xxh3_scr(a0, c0[t], scr0);
+        a1 = xxh3_scr(a1, c1[t], scr1);
       }
     }
   }
@@ -630,8 +665,8 @@ __device__ __forceinline__ void xxh3_128_row_long(const uint8_t* base, uint32_t 
     for (int t = 0; t < 4; ++t) stripe_part(w[t], k0[t], k1[t], c0, c1);
     c0 = row_quad_sum64(c0);
     c1 = row_quad_sum64(c1);
-    a0 += c0; a0 ^= a0 >> 47; a0 ^= scr0; a0 *= P32_1;
-    a1 += c1; a1 ^= a1 >> 47; a1 ^= scr1; a1 *= P32_1;
+    a0 = xxh3_scr(a0, c0, scr0);
+    a1 = xxh3_scr(a1, c1, scr1);
   }
   {
     const uint32_t tail0 = nb_blocks * 1024;
@@ -680,8 +715,8 @@ __device__ __forceinline__ void xxh3_128_row_long_lean(const uint8_t* base, uint
     }
     c0 = row_quad_sum64(c0);
     c1 = row_quad_sum64(c1);
-    a0 += c0; a0 ^= a0 >> 47; a0 ^= ls->acc[16 + 2 * q]; a0 *= P32_1;
-    a1 += c1; a1 ^= a1 >> 47; a1 ^= ls->acc[16 + 2 * q + 1]; a1 *= P32_1;
+    a0 = xxh3_scr(a0, c0, ls->acc[16 + 2 * q]);
+    a1 = xxh3_scr(a1, c1, ls->acc[16 + 2 * q + 1]);
   }
   {
     const uint32_t tail0 = nb_blocks * 1024;
@@ -742,8 +777,8 @@ __device__ __forceinline__ void xxh3_128_oct_long(const uint8_t* base, uint32_t 
     }
     c0 += mov_dpp64<0xB1>(c0);  // quad_perm [1,0,3,2]: the other half of the pair
     c1 += mov_dpp64<0xB1>(c1);
-    a0 += c0; a0 ^= a0 >> 47; a0 ^= scr0; a0 *= P32_1;
-    a1 += c1; a1 ^= a1 >> 47; a1 ^= scr1; a1 *= P32_1;
+    a0 = xxh3_scr(a0, c0, scr0);
+    a1 = xxh3_scr(a1, c1, scr1);
   }
   {
     const uint32_t tail0 = nb_blocks * 1024;
@@ -813,10 +848,7 @@ __device__ __noinline__ uint64_t xxh3_64_long_lane(uint32_t len, R64 r64, const 
     for (uint32_t s = 0; s < 16; ++s) stripe(n * 1024 + 64 * s, ls->acc + s);
 #pragma unroll
     for (int i = 0; i < 8; ++i) {
-      uint64_t a = acc[i];
-      a ^= a >> 47;
-      a ^= ls->acc[16 + i];
-      acc[i] = a * P32_1;
+      acc[i] = xxh3_scr(acc[i], 0, ls->acc[16 + i]);
     }
   }
   const uint32_t ns = ((len - 1) - nb * 1024) / 64;

@@ -1312,10 +1312,8 @@ __global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(LSM_G
         const uint64_t scr0 = L.secret.acc[16 + 2 * q], scr1 = L.secret.acc[16 + 2 * q + 1];
         const uint64_t* cb = contrib + 8 * B.u0 + 2 * q;
         for (uint32_t n = 0; n < B.nbk; ++n) {
-          a0 += cb[8 * n];
-          a0 ^= a0 >> 47; a0 ^= scr0; a0 *= P32_1;
-          a1 += cb[8 * n + 1];
-          a1 ^= a1 >> 47; a1 ^= scr1; a1 *= P32_1;
+          a0 = xxh3_scr(a0, cb[8 * n], scr0);
+          a1 = xxh3_scr(a1, cb[8 * n + 1], scr1);
         }
         a0 += cb[8 * B.nbk];
         a1 += cb[8 * B.nbk + 1];
