@@ -535,6 +535,7 @@ __device__ __forceinline__ void xxh3_kib_contribs(const uint8_t* base, uint32_t 
 
 // With `ready`, the chain consumes the contributions as xxh3_kib_contribs
 // publishes them (waits for ready[n] == tag).
+template <uint32_t kBatch = 8>
 __device__ __forceinline__ void xxh3_128_wave_finish(const uint8_t* base, uint32_t pos, uint32_t len,
                                                      const LongSecret* __restrict__ ls, const uint64_t* contrib,
                                                      uint64_t& out_lo, uint64_t& out_hi,
@@ -547,14 +548,14 @@ __device__ __forceinline__ void xxh3_128_wave_finish(const uint8_t* base, uint32
   uint64_t a1 = q == 0 ? P64_1 : q == 1 ? P64_3 : q == 2 ? (uint64_t)P32_2 : (uint64_t)P32_1;
   const uint64_t scr0 = ls->acc[16 + 2 * q], scr1 = ls->acc[16 + 2 * q + 1];
   const uint32_t nb_blocks = (len - 1) / 1024;
-  // the serial chain: eight KiB blocks' contributions read ahead of their steps
-  for (uint32_t n0 = 0; n0 < nb_blocks; n0 += 8) {
-    uint64_t c0[8], c1[8];
+  // the serial chain: kBatch KiB blocks' contributions read ahead of their steps
+  for (uint32_t n0 = 0; n0 < nb_blocks; n0 += kBatch) {
+    uint64_t c0[kBatch], c1[kBatch];
     if (ready) {  // (every lane reads the same flags: the loop is wave-uniform)
       for (;;) {
         bool all = true;
 #pragma unroll
-        for (uint32_t t = 0; t < 8; ++t)
+        for (uint32_t t = 0; t < kBatch; ++t)
           if (n0 + t < nb_blocks)
             all &= __hip_atomic_load(&ready[n0 + t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == tag;
         if (all) break;
@@ -563,7 +564,7 @@ __device__ __forceinline__ void xxh3_128_wave_finish(const uint8_t* base, uint32
       __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
     }
 #pragma unroll
-    for (uint32_t t = 0; t < 8; ++t) {
+    for (uint32_t t = 0; t < kBatch; ++t) {
       c0[t] = c1[t] = 0;
       if (n0 + t < nb_blocks) {
         c0[t] = contrib[8 * (n0 + t) + 2 * q];
@@ -571,7 +572,7 @@ __device__ __forceinline__ void xxh3_128_wave_finish(const uint8_t* base, uint32
       }
     }
 #pragma unroll
-    for (uint32_t t = 0; t < 8; ++t) {
+    for (uint32_t t = 0; t < kBatch; ++t) {
       if (n0 + t < nb_blocks) {
         a0 = xxh3_scr(a0, c0[t], scr0);
         a1 = xxh3_scr(a1, c1[t], scr1);
