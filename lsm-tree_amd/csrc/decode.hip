@@ -600,6 +600,104 @@ constexpr uint32_t kBigStage = 72 * 1024;
 constexpr uint32_t kBigContrib = 256;                        // LDS: contributions, 64 B per KiB
 constexpr uint32_t kBigStageOff = kBigContrib + (kBigStage / 1024 + 1) * 64;
 
+// An index block larger than the stage (a full block index: ~25 B per data
+// block, hundreds of KiB for a 64 MiB table), on all four waves of the
+// general-path workgroup, through the stage in 64 KiB chunks.  Index blocks
+// have restart interval 1, so every record starts at its binary-index entry
+// and the records are independent: per chunk, each thread parses the records
+// (its intervals r = tid, tid + 256, ...) that start in the chunk, from LDS;
+// all waves compute the per-KiB XXH3 contributions of the chunk's KiB blocks
+// and wave 0 carries the serial chain across chunks.  Same results as the
+// interval walk of decode_block_direct (walk_interval), which still takes an
+// interval whose record count is not 1 (malformed trailers).
+constexpr uint32_t kIndexChunk = 64 * 1024;
+static_assert(kIndexChunk + 1024 + 256 <= kBigStage, "chunk + one KiB unit + a record header");
+
+__device__ __forceinline__ void decode_index_chunked(const DecodeParams& P, uint32_t b, const uint8_t* gbase,
+                                                     uint32_t span, BlockMeta* meta, uint32_t* cks_bad,
+                                                     uint64_t* contrib, uint8_t* stage) {
+  const uint32_t tid = threadIdx.x;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid / kWave);
+  const int lane = tid & (kWave - 1);
+  constexpr uint32_t kThreads = kBigWaves * kWave;
+  const BlockMeta m = meta[1];
+  const TrailerInfo t = trailer_of(m);
+  const uint32_t p0 = m.p0;  // span-relative payload start
+  const uint32_t plen = m.len - kHdrLen;
+  const uint64_t item_base = gload(P.item_start, b);
+  const bool hash = !(P.flags & LSM_DECODE_PAYLOAD_VERIFIED);
+  const uint32_t nbk = plen > 240 ? (plen - 1) / 1024 : 0;
+  uint64_t a0, a1;
+  xxh3_acc_init(lane & 3, a0, a1);
+  const uint64_t scr0 = kLongSecret.acc[16 + 2 * (lane & 3)], scr1 = kLongSecret.acc[16 + 2 * (lane & 3) + 1];
+  const uint32_t nint = t.bin_len;
+  uint32_t r = tid;
+  uint32_t s_cur = r < nint ? bin_get(gbase, p0, t, r) : 0xFFFFFFFFu;
+  bool ok = true;
+  for (uint32_t cs = 0; cs < span; cs += kIndexChunk) {
+    const uint32_t ce = min(cs + kIndexChunk, span);
+    const uint32_t ss = min(ce + 1024 + 256, span);  // staged: [cs, ss)
+    {
+      const uint32_t chunks = (ss - cs) >> 4;
+      const uint8_t* src = gbase + cs + 16 * lane;
+      for (uint32_t c = wave; c * kWave < chunks; c += kBigWaves)
+        if (c * kWave + lane < chunks)
+          __builtin_amdgcn_global_load_lds((gbl_void_t*)(src + 1024 * c), (lds_void_t*)(stage + 1024 * c), 16, 0, 0);
+    }
+    vm_wait<0>();
+    lds_barrier();
+    const uint8_t* sbase = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(stage) - cs);  // span-relative
+    // the KiB blocks that start in this chunk
+    const uint32_t n0 = min(nbk, cs > p0 ? (cs - p0 + 1023) / 1024 : 0u);
+    const uint32_t n1 = min(nbk, ce > p0 ? (ce - p0 + 1023) / 1024 : 0u);
+    if (hash && n1 > n0)
+      xxh3_kib_contribs(sbase, p0 + 1024 * n0, (n1 - n0) * 1024 + 1, &kLongSecret, contrib, wave, kBigWaves);
+    // the records that start in this chunk
+    while (r < nint && p0 + s_cur < ce) {
+      const bool last = r + 1 == nint;
+      const uint32_t stop = last ? t.rec_end : bin_get(gbase, p0, t, r + 1);
+      const uint32_t count = last ? t.item_count - r : 1;
+      if (s_cur > t.rec_end || stop > t.rec_end || (r == 0 && s_cur != 0)) {
+        ok = false;
+      } else if (count != 1) {
+        ok &= walk_interval(gbase, p0, m, r, [&](uint32_t j, const ItemFields& f) {
+          emit_global(P.out, item_base + j, f, P.seqno_add);
+        });
+      } else {
+        ItemFields f;
+        uint32_t next;
+        if (parse_record(sbase, p0, s_cur, t, 1, true, 0, f, next) && next == stop)
+          emit_global(P.out, item_base + r, f, P.seqno_add);
+        else
+          ok = false;
+      }
+      r += kThreads;
+      s_cur = r < nint ? bin_get(gbase, p0, t, r) : 0xFFFFFFFFu;
+    }
+    lds_barrier();
+    if (wave == 0 && hash) {  // the chain over this chunk's KiB blocks, in order
+      for (uint32_t n = 0; n < n1 - n0; ++n) {
+        a0 = xxh3_scr(a0, contrib[8 * n + 2 * (lane & 3)], scr0);
+        a1 = xxh3_scr(a1, contrib[8 * n + 2 * (lane & 3) + 1], scr1);
+      }
+    }
+    lds_barrier();  // (the next chunk overwrites the stage and the contributions)
+  }
+  if (r < nint) ok = false;  // a record start beyond the block
+  if (!ok) atomicCAS(&meta[1].st, ST_OK, ST_PARSE);
+  if (wave == 0 && hash) {
+    uint64_t lo, hi;
+    if (plen > 240) xxh3_wave_tail_merge(gbase, p0, plen, &kLongSecret, a0, a1, lo, hi);
+    else xxh3_128_wave(gbase, p0, plen, &kLongSecret, lo, hi);
+    if (lane == 0) *cks_bad = lo != m.ck_lo || hi != m.ck_hi;
+  }
+  lds_barrier();
+  if (tid == 0) {
+    const int32_t st = meta[0].st != ST_OK ? meta[0].st : *cks_bad ? (int32_t)ST_CKSUM : meta[1].st;
+    gstore(P.status, b, st);
+  }
+}
+
 __global__ __launch_bounds__(kBigWaves * kWave) void decode_deferred_staged_kernel(DecodeParams P) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   BlockMeta* meta = reinterpret_cast<BlockMeta*>(smem);  // [0] header view, [1] trailer view
@@ -614,8 +712,21 @@ __global__ __launch_bounds__(kBigWaves * kWave) void decode_deferred_staged_kern
     const uint32_t b = gload(P.defer_list, i);
     const uint64_t off = gload(P.block_off, b), end = gload(P.block_off, b + 1);
     const uint64_t span0 = off & ~15ULL, span1 = (max(end, off) + 15) & ~15ULL;
-    if (span1 - span0 > kBigStage) {  // HBM path
-      if (wave == 0) decode_block_direct(P, b, meta);
+    if (span1 - span0 > kBigStage) {  // larger than the stage
+      const uint8_t* gbase = P.blocks + span0;
+      const uint32_t cap = gload(P.item_start, b + 1) - gload(P.item_start, b);
+      if (tid == 0) {
+        meta_header(gbase, (uint32_t)(off - span0), end >= off ? end - off : 0, meta[0]);
+        meta[1] = meta[0];
+        meta_trailer(gbase, P.expect_type, cap, meta[1]);
+        *cks_bad = 0;
+      }
+      lds_barrier();
+      if (meta[1].st == ST_OK && meta[1].type == 1) {  // index blocks (a full index of a large table)
+        decode_index_chunked(P, b, gbase, (uint32_t)(span1 - span0), meta, cks_bad, contrib, stage);
+      } else if (wave == 0) {  // anything else: one wave straight from HBM
+        decode_block_direct(P, b, meta);
+      }
       lds_barrier();
       continue;
     }

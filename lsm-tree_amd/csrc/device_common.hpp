@@ -535,17 +535,54 @@ __device__ __forceinline__ void xxh3_kib_contribs(const uint8_t* base, uint32_t 
 
 // With `ready`, the chain consumes the contributions as xxh3_kib_contribs
 // publishes them (waits for ready[n] == tag).
+// XXH3-128 long path, wave-level pieces: the initial accumulators of lane
+// quad position q (pair 2q, 2q+1), and the tail (the stripes after the last
+// full KiB block, the last stripe) + merge + avalanche after the chain.
+__device__ __forceinline__ void xxh3_acc_init(int q, uint64_t& a0, uint64_t& a1) {
+  a0 = q == 0 ? (uint64_t)P32_3 : q == 1 ? P64_2 : q == 2 ? P64_4 : P64_5;
+  a1 = q == 0 ? P64_1 : q == 1 ? P64_3 : q == 2 ? (uint64_t)P32_2 : (uint64_t)P32_1;
+}
+__device__ __forceinline__ void xxh3_wave_tail_merge(const uint8_t* base, uint32_t pos, uint32_t len,
+                                                     const LongSecret* __restrict__ ls, uint64_t a0, uint64_t a1,
+                                                     uint64_t& out_lo, uint64_t& out_hi) {
+  const int lane = threadIdx.x & 63;
+  const int q = lane & 3;
+  const int s = lane >> 2;
+  const uint64_t k0 = ls->acc[s + 2 * q], k1 = ls->acc[s + 2 * q + 1];
+  const uint32_t nb_blocks = (len - 1) / 1024;
+  {
+    const uint32_t tail0 = nb_blocks * 1024;
+    const uint32_t nb_stripes = ((len - 1) - tail0) / 64;
+    uint64_t c0 = 0, c1 = 0;
+    if ((uint32_t)s < nb_stripes) {
+      Win16 w = read_win16(base, pos + tail0 + 16 * lane);
+      stripe_part(w, k0, k1, c0, c1);
+    }
+    if (lane < 4) {  // last stripe: input[len-64 .. len), secret + 121
+      Win16 w = read_win16(base, pos + len - 64 + 16 * lane);
+      stripe_part(w, ls->last[2 * q], ls->last[2 * q + 1], c0, c1);
+    }
+    a0 += quad_group_sum64(c0);
+    a1 += quad_group_sum64(c1);
+  }
+  uint64_t tlo = mul_fold64(a0 ^ ls->mlo[2 * q], a1 ^ ls->mlo[2 * q + 1]);
+  uint64_t thi = mul_fold64(a0 ^ ls->mhi[2 * q], a1 ^ ls->mhi[2 * q + 1]);
+  tlo += shfl_xor64(tlo, 1);
+  thi += shfl_xor64(thi, 1);
+  tlo += shfl_xor64(tlo, 2);
+  thi += shfl_xor64(thi, 2);
+  out_lo = xxh3_avalanche((uint64_t)len * P64_1 + tlo);
+  out_hi = xxh3_avalanche(~((uint64_t)len * P64_2) + thi);
+}
+
 template <uint32_t kBatch = 8>
 __device__ __forceinline__ void xxh3_128_wave_finish(const uint8_t* base, uint32_t pos, uint32_t len,
                                                      const LongSecret* __restrict__ ls, const uint64_t* contrib,
                                                      uint64_t& out_lo, uint64_t& out_hi,
                                                      const uint32_t* ready = nullptr, uint32_t tag = 0) {
-  const int lane = threadIdx.x & 63;
-  const int q = lane & 3;
-  const int s = lane >> 2;
-  const uint64_t k0 = ls->acc[s + 2 * q], k1 = ls->acc[s + 2 * q + 1];
-  uint64_t a0 = q == 0 ? (uint64_t)P32_3 : q == 1 ? P64_2 : q == 2 ? P64_4 : P64_5;
-  uint64_t a1 = q == 0 ? P64_1 : q == 1 ? P64_3 : q == 2 ? (uint64_t)P32_2 : (uint64_t)P32_1;
+  const int q = threadIdx.x & 3;
+  uint64_t a0, a1;
+  xxh3_acc_init(q, a0, a1);
   const uint64_t scr0 = ls->acc[16 + 2 * q], scr1 = ls->acc[16 + 2 * q + 1];
   const uint32_t nb_blocks = (len - 1) / 1024;
   // the serial chain: kBatch KiB blocks' contributions read ahead of their steps
@@ -579,29 +616,7 @@ __device__ __forceinline__ void xxh3_128_wave_finish(const uint8_t* base, uint32
       }
     }
   }
-  {
-    const uint32_t tail0 = nb_blocks * 1024;
-    const uint32_t nb_stripes = ((len - 1) - tail0) / 64;
-    uint64_t c0 = 0, c1 = 0;
-    if ((uint32_t)s < nb_stripes) {
-      Win16 w = read_win16(base, pos + tail0 + 16 * lane);
-      stripe_part(w, k0, k1, c0, c1);
-    }
-    if (lane < 4) {  // last stripe: input[len-64 .. len), secret + 121
-      Win16 w = read_win16(base, pos + len - 64 + 16 * lane);
-      stripe_part(w, ls->last[2 * q], ls->last[2 * q + 1], c0, c1);
-    }
-    a0 += quad_group_sum64(c0);
-    a1 += quad_group_sum64(c1);
-  }
-  uint64_t tlo = mul_fold64(a0 ^ ls->mlo[2 * q], a1 ^ ls->mlo[2 * q + 1]);
-  uint64_t thi = mul_fold64(a0 ^ ls->mhi[2 * q], a1 ^ ls->mhi[2 * q + 1]);
-  tlo += shfl_xor64(tlo, 1);
-  thi += shfl_xor64(thi, 1);
-  tlo += shfl_xor64(tlo, 2);
-  thi += shfl_xor64(thi, 2);
-  out_lo = xxh3_avalanche((uint64_t)len * P64_1 + tlo);
-  out_hi = xxh3_avalanche(~((uint64_t)len * P64_2) + thi);
+  xxh3_wave_tail_merge(base, pos, len, ls, a0, a1, out_lo, out_hi);
 }
 
 // Window-backed readers for the per-lane short path over an aligned base.

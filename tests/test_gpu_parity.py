@@ -185,6 +185,34 @@ def test_index_blocks(gpu):
     assert (g["status"] == 7).all()  # TYPE_MISMATCH (util.rs:81-86)
 
 
+def test_large_index_blocks(gpu):
+    """Full block indexes larger than the general path's stage (> 72 KiB, as a
+    64 MiB table of 4 KiB blocks has): decoded through the stage in 64 KiB
+    chunks with the XXH3 chain carried across them (decode_index_chunked).
+    Valid blocks, a flipped payload bit (CKSUM), a broken record re-sealed with
+    valid checksums, and a re-sealed item count that leaves the last interval
+    two records (the interval walk fallback): statuses and fields == oracle."""
+    items = index_items(14000, seed=11)
+    starts = np.array([0, 6000, 6001, 14000], np.uint32)
+    buf, off = pyoracle.encode_blocks(items, starts, block_type=1)
+    assert np.diff(off.astype(np.int64)).max() > 150 * 1024
+    blocks = [bytes(buf[int(off[i]):int(off[i + 1])]) for i in range(3)]
+    bad_ck = bytearray(blocks[0])
+    bad_ck[33 + 70000] ^= 0x10
+    rec = bytearray(blocks[2][33:])
+    step, bin_off = rec[-30], int.from_bytes(rec[-25:-21], "little")  # trailer.rs:118-163
+    start = int.from_bytes(rec[bin_off + step * 4000:bin_off + step * 4001], "little")
+    rec[start] = 1  # record 4000's tag byte (index records start with 0)
+    cnt = bytearray(blocks[2][33:])
+    cnt[-4] += 1  # item_count = bin_len + 1
+    tests = blocks + [bytes(bad_ck), pyoracle.block_write(bytes(rec), 1), pyoracle.block_write(bytes(cnt), 1)]
+    buf2, off2 = pack(tests)
+    g = gpu_decode(gpu, buf2, off2)
+    parsed, item_start, status = pyoracle.decode_blocks(buf2, off2)
+    assert (status[:3] == 0).all() and status[3] == 4 and (status[4:] != 0).all(), status
+    compare_decode(g, parsed, item_start, status)
+
+
 # ------------------------------------------------------------------ configs (reduced counts)
 
 def test_config2_shape_counter_keys(gpu):
