@@ -1236,22 +1236,32 @@ __global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(LSM_G
         atomicMax(&hhi[bk], ridx);
       }
     }
+    // ---- tails, wave per block: marker, hash-index bytes, trailer (trailer.rs:78-173);
+    // without hash indexes they need nothing from the other waves' records
+    // (disjoint bytes), so they go before the barrier
+    auto tails = [&]() {
+      for (uint32_t jb = wave; jb < (kDiagBuild && (P.diag & 8) ? 0 : k); jb += kGWaves) {
+        const GBlk& B = L.blk[jb];
+        const uint32_t p0 = B.img + kHdrLen, bin_off = B.recs + 1;
+        if (lane == 0) L.img[p0 + B.recs] = kTrailerMarker;
+        const uint32_t hash_off = B.hash_w ? bin_off + B.bin_len * B.step : 0;
+        if (kHash)
+          for (uint32_t q = lane; q < B.hash_w; q += kWave)
+            L.img[p0 + hash_off + q] = (uint8_t)bucket_byte(hlo[B.hash_base + q], hhi[B.hash_base + q]);
+        write_trailer_bytes(L.img, p0 + B.plen - kTrailerLen, ri, B.step, B.bin_len, bin_off, B.hash_w, hash_off,
+                            B.n);
+      }
+    };
+    if (!kHash) tails();
     group_barrier_lds();
     ENC_PHASE(3);
     // the stage is free: the next group's DMA runs under the tails and the hash
     if (Gn.k && !(kDiagBuild && (P.diag & 16))) issue_dma(Gn);
     ENC_PHASE(10);
-    // ---- tails, wave per block: marker, hash-index bytes, trailer (trailer.rs:78-173)
-    for (uint32_t jb = wave; jb < (kDiagBuild && (P.diag & 8) ? 0 : k); jb += kGWaves) {
-      const GBlk& B = L.blk[jb];
-      const uint32_t p0 = B.img + kHdrLen, bin_off = B.recs + 1;
-      if (lane == 0) L.img[p0 + B.recs] = kTrailerMarker;
-      const uint32_t hash_off = B.hash_w ? bin_off + B.bin_len * B.step : 0;
-      for (uint32_t q = lane; q < B.hash_w; q += kWave)
-        L.img[p0 + hash_off + q] = (uint8_t)bucket_byte(hlo[B.hash_base + q], hhi[B.hash_base + q]);
-      write_trailer_bytes(L.img, p0 + B.plen - kTrailerLen, ri, B.step, B.bin_len, bin_off, B.hash_w, hash_off, B.n);
+    if (kHash) {  // the hash-index bytes need every vote
+      tails();
+      group_barrier_lds();
     }
-    group_barrier_lds();
     ENC_PHASE(4);
     // ---- payload xxh3_128: 1 KiB units over the 16 DPP rows
     {
