@@ -585,16 +585,21 @@ __device__ __forceinline__ void xxh3_128_wave_finish(const uint8_t* base, uint32
   xxh3_acc_init(q, a0, a1);
   const uint64_t scr0 = ls->acc[16 + 2 * q], scr1 = ls->acc[16 + 2 * q + 1];
   const uint32_t nb_blocks = (len - 1) / 1024;
-  // the serial chain: kBatch KiB blocks' contributions read ahead of their steps
+  // the serial chain: kBatch KiB blocks' contributions read ahead of their
+  // steps.  The flag and contribution reads are unconditional (no branch, so
+  // no wait, between them): past the last KiB block they read LDS beyond the
+  // arrays (the callers' stage follows), and those values are not used.
   for (uint32_t n0 = 0; n0 < nb_blocks; n0 += kBatch) {
     uint64_t c0[kBatch], c1[kBatch];
     if (ready) {  // (every lane reads the same flags: the loop is wave-uniform)
       for (;;) {
-        bool all = true;
+        uint32_t f[kBatch];
 #pragma unroll
         for (uint32_t t = 0; t < kBatch; ++t)
-          if (n0 + t < nb_blocks)
-            all &= __hip_atomic_load(&ready[n0 + t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) == tag;
+          f[t] = __hip_atomic_load(&ready[n0 + t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        bool all = true;
+#pragma unroll
+        for (uint32_t t = 0; t < kBatch; ++t) all &= (n0 + t >= nb_blocks) | (f[t] == tag);
         if (all) break;
         __builtin_amdgcn_s_sleep(1);
       }
@@ -602,11 +607,8 @@ __device__ __forceinline__ void xxh3_128_wave_finish(const uint8_t* base, uint32
     }
 #pragma unroll
     for (uint32_t t = 0; t < kBatch; ++t) {
-      c0[t] = c1[t] = 0;
-      if (n0 + t < nb_blocks) {
-        c0[t] = contrib[8 * (n0 + t) + 2 * q];
-        c1[t] = contrib[8 * (n0 + t) + 2 * q + 1];
-      }
+      c0[t] = contrib[8 * (n0 + t) + 2 * q];
+      c1[t] = contrib[8 * (n0 + t) + 2 * q + 1];
     }
 #pragma unroll
     for (uint32_t t = 0; t < kBatch; ++t) {
