@@ -621,6 +621,7 @@ constexpr uint32_t kGUnits = kGImg / 1024 + kGBlocks + 1;  // hash units per gro
 constexpr uint32_t kGUnion = LSM_G_UNION;      // hash votes | hash contributions
 constexpr uint32_t kGHash = kGUnion / 8;       // vote pairs
 static_assert(kGUnits * 64 <= kGUnion, "hash contributions");
+static_assert((kGUnits + 4) * 64 <= kGUnion, "the chain's batched reads stay inside L.uni");
 
 
 __device__ __host__ __forceinline__ bool group_fits(uint64_t n, uint64_t kspan, uint64_t vspan, uint64_t total,
@@ -1321,9 +1322,22 @@ __global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(LSM_G
         uint64_t a1 = q == 0 ? P64_1 : q == 1 ? P64_3 : q == 2 ? (uint64_t)P32_2 : (uint64_t)P32_1;
         const uint64_t scr0 = L.secret.acc[16 + 2 * q], scr1 = L.secret.acc[16 + 2 * q + 1];
         const uint64_t* cb = contrib + 8 * B.u0 + 2 * q;
-        for (uint32_t n = 0; n < B.nbk; ++n) {
-          a0 = xxh3_scr(a0, cb[8 * n], scr0);
-          a1 = xxh3_scr(a1, cb[8 * n + 1], scr1);
+        // four KiB blocks' contributions per batch, read without branches (past
+        // the block they read other contributions in L.uni, unused)
+        for (uint32_t n0 = 0; n0 < B.nbk; n0 += 4) {
+          uint64_t c0[4], c1[4];
+#pragma unroll
+          for (uint32_t t = 0; t < 4; ++t) {
+            c0[t] = cb[8 * (n0 + t)];
+            c1[t] = cb[8 * (n0 + t) + 1];
+          }
+#pragma unroll
+          for (uint32_t t = 0; t < 4; ++t) {
+            if (n0 + t < B.nbk) {
+              a0 = xxh3_scr(a0, c0[t], scr0);
+              a1 = xxh3_scr(a1, c1[t], scr1);
+            }
+          }
         }
         a0 += cb[8 * B.nbk];
         a1 += cb[8 * B.nbk + 1];
