@@ -844,15 +844,22 @@ __device__ __forceinline__ BigBlk big_blk(const DecodeParams& P, uint32_t li) {
 #ifdef LSM_DIAG
 // Diagnostic builds: per-phase s_memtime totals of wave 0 of every big-block
 // workgroup (read by lsm_diag_decode_phases).
-__device__ unsigned long long g_dec_phase[16];
+__device__ unsigned long long g_dec_phase[32];
 #define DEC_PHASE(i)                                  \
   {                                                   \
     const uint64_t t_ = __builtin_amdgcn_s_memtime(); \
     ph[i] += t_ - t_last;                             \
     t_last = t_;                                      \
   }
+// Role timer: time since the last phase mark into ph[i], one count into ph[i + 1].
+#define DEC_ROLE(i)                                   \
+  {                                                   \
+    ph[i] += __builtin_amdgcn_s_memtime() - t_last;   \
+    ph[(i) + 1] += 1;                                 \
+  }
 #else
 #define DEC_PHASE(i)
+#define DEC_ROLE(i)
 #endif
 
 template <bool kAllFields>
@@ -1011,10 +1018,21 @@ __global__ __launch_bounds__(kBigGWaves * kWave) void decode_big_kernel(DecodePa
 #define LSM_DEC_WPE 3
 #endif
 constexpr uint32_t kGroupWaves = LSM_DEC_WAVES;
+#ifndef LSM_PRIO_A
+#define LSM_PRIO_A 0
+#endif
+#ifndef LSM_PRIO_H
+#define LSM_PRIO_H 0
+#endif
+constexpr int kPrioA = LSM_PRIO_A;  // s_setprio of the phase-A wave
+constexpr int kPrioH = LSM_PRIO_H;  // s_setprio of a wave hashing one whole block
 
 template <bool kAllFields>
 __global__ __launch_bounds__(kGroupWaves * kWave) __attribute__((amdgpu_waves_per_eu(LSM_DEC_WPE))) void decode_blocks_kernel(DecodeParams P) {
   // LDS: [meta: G x 80 B][rec: u64 per item + 1 scratch][owner: u8 per item][staged bytes + pad][secret]
+#ifdef LSM_DIAG
+  uint64_t t_last = __builtin_amdgcn_s_memtime(), ph[16] = {};
+#endif
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint32_t gmax = min(kMaxGroup, P.blocks_per_wave);
   BlockMeta* meta = reinterpret_cast<BlockMeta*>(smem);
@@ -1082,6 +1100,7 @@ __global__ __launch_bounds__(kGroupWaves * kWave) __attribute__((amdgpu_waves_pe
     for (uint32_t i = tid; i < G.n_items; i += kGroupWaves * kWave) rec[i] = 0;
     vm_wait<0>();
     lds_barrier();
+    DEC_PHASE(0);
     const Group Gn = next_group(b + k);
     // ---- 2. wave 0: headers, trailers, restart-interval numbering; owner[c] = block of interval c
     if (wave == 0) {
@@ -1105,6 +1124,7 @@ __global__ __launch_bounds__(kGroupWaves * kWave) __attribute__((amdgpu_waves_pe
       }
     }
     lds_barrier();
+    DEC_PHASE(1);
     // ---- 3. phase A on nA waves (64 intervals each)  ||  payload checksums on the others
     {
       const uint32_t total = (kDiagBuild && (P.flags & kDiagSkipParse)) ? 0
@@ -1114,20 +1134,26 @@ __global__ __launch_bounds__(kGroupWaves * kWave) __attribute__((amdgpu_waves_pe
       // payload checksums (not when verified upstream: the LZ4 path checks the stored bytes)
       const bool hash = !(kDiagBuild && (P.flags & kDiagSkipHash)) && !(P.flags & LSM_DECODE_PAYLOAD_VERIFIED);
       if (role < nA) {
+        if (kPrioA) __builtin_amdgcn_s_setprio(kPrioA);  // the serial walk is the group's critical path
         phase_a(stage, meta, owner, rec, role * kWave, nA * kWave, total, P.tile_items);
+        if (kPrioA) __builtin_amdgcn_s_setprio(0);
+        DEC_ROLE(8);
       } else if (hash && k <= kGroupWaves - nA) {
         // few (large) blocks: one wave per block, the 64-lane XXH3 (1 KiB per step)
         const uint32_t jb = role - nA;
         if (jb < k && meta[jb].hdr_st == ST_OK) {
           const uint32_t hb = meta[jb].hb, plen = meta[jb].len - kHdrLen;
           uint64_t lo, hi;
+          if (kPrioH) __builtin_amdgcn_s_setprio(kPrioH);
           xxh3_128_wave(stage, hb + kHdrLen, plen, ls, lo, hi);
+          if (kPrioH) __builtin_amdgcn_s_setprio(0);
           const bool hck = header_cksum_ok(stage, hb);
           if (lane == 0) {
             meta[jb].ck_bad = lo != meta[jb].ck_lo || hi != meta[jb].ck_hi;
             meta[jb].hck_bad = !hck;
           }
         }
+        DEC_ROLE(10);
       } else if (hash) {
         const uint32_t rows = (kGroupWaves - nA) * 4;
         for (uint32_t jb = (role - nA) * 4 + (lane >> 4); jb < k; jb += rows) {
@@ -1143,13 +1169,16 @@ __global__ __launch_bounds__(kGroupWaves * kWave) __attribute__((amdgpu_waves_pe
             meta[jb].hck_bad = !hck;
           }
         }
+        DEC_ROLE(12);
       }
     }
     lds_barrier();
+    DEC_PHASE(2);
     // ---- 4. phase B: thread = record; full parse + validation; coalesced stores
     if (!(kDiagBuild && (P.flags & (kDiagSkipParse | kDiagSkipPhaseB))))
       phase_b<kAllFields>(P, stage, meta, rec, G.n_items, G.g_item0, threadIdx.x, blockDim.x);
     lds_barrier();
+    DEC_PHASE(3);
     if (wave == 0) {
       int32_t st = ST_OK;
       if ((uint32_t)lane < k) {
@@ -1163,8 +1192,19 @@ __global__ __launch_bounds__(kGroupWaves * kWave) __attribute__((amdgpu_waves_pe
       defer_blocks_wave(P, (uint32_t)lane < k && st == ST_DEFER, b + lane);
     }
     if (Gn.k) issue_dma(Gn, img);  // refill the stage after phase B
+    DEC_PHASE(4);
+#ifdef LSM_DIAG
+    ph[5] += 1;
+    ph[6] += k;
+#endif
     G = Gn;
   }
+#ifdef LSM_DIAG
+  if (lane == 0) {
+    for (int i = 0; i < 16; ++i)
+      if ((i >= 8 || wave == 0) && ph[i]) atomicAdd(&g_dec_phase[16 + i], (unsigned long long)ph[i]);
+  }
+#endif
 }
 
 // item counts from the trailers (trailer.rs:57-75), same rule as
@@ -1279,10 +1319,11 @@ hipError_t launch_decode(const DecodeParams& P0, void* ws, hipStream_t st) {
 
 #ifdef LSM_DIAG
 // Diagnostic builds only: copy out and clear the big-block kernel's phase totals.
-extern "C" int lsm_diag_decode_phases(uint64_t* out16) {
+// Entries 16..31 are the group kernel's (wave 0 per group, role timers summed over waves).
+extern "C" int lsm_diag_decode_phases(uint64_t* out32) {
   if (hipDeviceSynchronize() != hipSuccess) return -1;
-  if (hipMemcpyFromSymbol(out16, HIP_SYMBOL(lsmgpu::g_dec_phase), 16 * sizeof(uint64_t)) != hipSuccess) return -1;
-  static const uint64_t z[16] = {};
+  if (hipMemcpyFromSymbol(out32, HIP_SYMBOL(lsmgpu::g_dec_phase), 32 * sizeof(uint64_t)) != hipSuccess) return -1;
+  static const uint64_t z[32] = {};
   return hipMemcpyToSymbol(HIP_SYMBOL(lsmgpu::g_dec_phase), z, sizeof(z)) == hipSuccess ? 0 : -1;
 }
 #endif

@@ -19,7 +19,7 @@ NAMES = {0: "wait DMA", 1: "header/trailer", 2: "owner fill", 3: "phase A | cont
          5: "status", 6: "issue next DMA", 7: "next-block handle"}
 torch.cuda.set_device(0)
 L = lsmgpu.lib()
-buf = (C.c_uint64 * 16)()
+buf = (C.c_uint64 * 32)()
 for bs, ipb, kind, est in bench.C5_SEGMENTS[4:]:
     nb = int((8 << 30) / 6 / est)
     items, starts, n = bench.make_workload(torch, lsmgpu, nb, items_per_block=ipb, kind=kind)

@@ -15,9 +15,15 @@ import lsmgpu  # noqa: E402
 
 def main():
     torch.cuda.set_device(0)
-    for si, (bs, ipb, kind, est) in enumerate(bench.C5_SEGMENTS):
-        nb = int((8 << 30) / 6 / est)
-        items, starts, n = bench.make_workload(torch, lsmgpu, nb, items_per_block=ipb, kind=kind)
+    import os
+    cases = [(bs, (8 << 30) // 6 // est, dict(items_per_block=ipb, kind=kind)) for bs, ipb, kind, est in bench.C5_SEGMENTS]
+    if os.environ.get("C5_EXTRA"):  # configs[1] and configs[3] shapes too
+        cases = [(4096, 1 << 20, dict(items_per_block=52)),
+                 (16384, 262144, dict(items_per_block=56, key_len=40, val_len=256, kind="prefix"))] + cases
+    for bs, nb, kw in cases:
+        kind = kw.get("kind", "counter") + ("" if kw.get("val_len", 64) == 64 else "-c3")
+        nb = int(nb)
+        items, starts, n = bench.make_workload(torch, lsmgpu, nb, **kw)
         enc = lsmgpu.Encoder().encode(items, starts, nb)
         torch.cuda.synchronize()
         total = int(enc["block_off"][nb].item())
