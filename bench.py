@@ -71,7 +71,8 @@ def host_threads(world=1):
         n = len(os.sched_getaffinity(0))
     except AttributeError:
         n = os.cpu_count() or 1
-    return max(1, min(HOST_THREADS, n) // max(1, world))
+    # each rank's share of the machine, at most the per-GPU CPU share
+    return max(1, min(HOST_THREADS, n // max(1, world)))
 
 
 def cpu_model():
@@ -900,14 +901,23 @@ def main():
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
     dist = None
+    # LSM_BENCH_REHEARSE=1: rehearse the N > 1 path on a one-GPU box (every
+    # rank on cuda:0, the two timing reductions over gloo on the host); never
+    # set by the driver, whose N > 1 runs use one GPU per rank and RCCL
+    rehearse = world > 1 and os.environ.get("LSM_BENCH_REHEARSE") == "1"
     if world > 1:
         import torch.distributed as dist
-        torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if rehearse:
+            torch.cuda.set_device(0)
+            dist.init_process_group("gloo")
+        else:
+            torch.cuda.set_device(local)
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(0)
     dev = torch.device("cuda", torch.cuda.current_device())
-    threads = host_threads(world)
+    red_dev = torch.device("cpu") if rehearse else dev  # where the timing / byte reductions run
+    threads = max(1, HOST_THREADS // world) if rehearse else host_threads(world)  # (rehearsal: one GPU's CPU share)
 
     def barrier():
         if dist is not None:
@@ -956,10 +966,10 @@ def main():
     el = time.perf_counter() - t0
     gpu_ms = e0.elapsed_time(e1)
     if dist is not None:
-        t = torch.tensor([el], dtype=torch.float64, device=dev)
+        t = torch.tensor([el], dtype=torch.float64, device=red_dev)
         dist.all_reduce(t, op=dist.ReduceOp.MAX)
         el = float(t.item())
-        tb = torch.tensor([total_bytes], dtype=torch.int64, device=dev)
+        tb = torch.tensor([total_bytes], dtype=torch.int64, device=red_dev)
         dist.all_reduce(tb, op=dist.ReduceOp.SUM)
         all_bytes = int(tb.item())
     else:
@@ -1017,7 +1027,7 @@ def main():
     if not args.no_extra and not args.skip_verify:
         if world == 1:
             extra["config4"] = bench_config4(torch, lsmgpu, max(3, args.steps // 4), rank, threads)
-        extra["config5"] = bench_config5(torch, lsmgpu, max(3, args.steps // 4), rank, world, dist, dev, threads)
+        extra["config5"] = bench_config5(torch, lsmgpu, max(3, args.steps // 4), rank, world, dist, red_dev, threads)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu and ref_buf is not None:

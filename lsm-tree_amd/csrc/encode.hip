@@ -281,6 +281,30 @@ __device__ __forceinline__ RawItem load_raw(const EncodeParams& P, uint64_t i) {
   return r;
 }
 
+// The same from a wave-uniform base item and a per-lane offset t < 2^29:
+// base pointers in SGPRs and 32-bit byte offsets (one VGPR per address).
+template <bool kIndex>
+__device__ __forceinline__ RawItem load_raw_rel(const EncodeParams& P, uint64_t base, uint32_t t) {
+  auto at64 = [&](const uint64_t* a, uint32_t k) {
+    return *reinterpret_cast<const uint64_t*>(reinterpret_cast<const uint8_t*>(a + base) + 8u * k);
+  };
+  RawItem r;
+  r.ko = at64(P.it.key_off, t);
+  r.ko1 = at64(P.it.key_off, t + 1);
+  r.seq = at64(P.it.seqno, t);
+  r.e = 0;
+  if (kIndex) {
+    r.vo = at64(P.it.handle_off, t);
+    r.vo1 = (P.it.handle_size + base)[t];
+    r.vt = 0;
+  } else {
+    r.vo = at64(P.it.val_off, t);
+    r.vo1 = at64(P.it.val_off, t + 1);
+    r.vt = (P.it.vtype + base)[t];
+  }
+  return r;
+}
+
 // Derived fields of a raw item and the writer's argument checks (key length
 // <= u16, a known value type, value length <= u32).
 template <bool kIndex>
@@ -695,7 +719,10 @@ uint32_t lcp_tail(const uint8_t* keys, uint64_t a, uint64_t b, uint32_t n) {
 }
 
 template <bool kIndex>
-__global__ __launch_bounds__(256) void encode_plan_kernel(EncodeParams P) {
+#ifndef LSM_PLAN_WPE
+#define LSM_PLAN_WPE 1
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LSM_PLAN_WPE))) void encode_plan_kernel(EncodeParams P) {
   __shared__ uint32_t bst[kPlanBlocks + 1];
   __shared__ unsigned long long bfirst[kPlanBlocks], bend[kPlanBlocks], lhead[kPlanBlocks];
   __shared__ unsigned long long psum[4];
@@ -717,14 +744,17 @@ __global__ __launch_bounds__(256) void encode_plan_kernel(EncodeParams P) {
   const uint32_t ri = kIndex ? 1 : P.ri;
   constexpr bool index = kIndex;
   // a non-monotone item_start run is a caller error: its blocks are rejected below
-  const uint64_t i_begin = bst[0], i_end = mono ? bst[nb] : bst[0];
+  // (wave-uniform: chunk bases stay in SGPRs, so item loads take the saddr form)
+  const uint64_t i_begin = (uint32_t)__builtin_amdgcn_readfirstlane(bst[0]);
+  const uint64_t i_end = (uint32_t)__builtin_amdgcn_readfirstlane(mono ? bst[nb] : bst[0]);
   uint64_t carry = 0;
   for (uint64_t base = i_begin; base < i_end; base += kPlanChunk) {
     const uint64_t i0 = base + kPlanPer * tid;
     // ---- 1. item fields, block of each item
     RawItem raw[kPlanPer];
 #pragma unroll
-    for (uint32_t q = 0; q < kPlanPer; ++q) raw[q] = load_raw<kIndex>(P, min(i0 + q, i_end - 1));
+    for (uint32_t q = 0; q < kPlanPer; ++q)
+      raw[q] = load_raw_rel<kIndex>(P, base, (uint32_t)min(i0 + q, i_end - 1) - (uint32_t)base);
     ItemMeta m[kPlanPer];
     uint32_t jq[kPlanPer], jjq[kPlanPer];
     uint32_t j = 0;

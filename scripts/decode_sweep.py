@@ -49,7 +49,7 @@ def main():
 
     variants = {}
     def tun(v, extra=0):
-        v = list(v) + [0] * (7 - len(v))
+        v = list(v) + [0] * (4 - len(v))
         v[3] |= 1 | extra
         return tuple(v)
 
