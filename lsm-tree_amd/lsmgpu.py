@@ -575,3 +575,122 @@ def shard_blocks(block_off, world):
         bounds.append(max(bounds[-1], min(b, n)))
     bounds.append(n)
     return bounds
+
+
+def shard_items(starts, key_off, val_off, world):
+    """Encode-side split: `world` contiguous block ranges,
+    cut only at block boundaries, of about equal key + value BYTES.
+    starts: host [n_blocks+1] item starts; key_off / val_off: host [n_items+1].
+    Returns world+1 block indices (as shard_blocks)."""
+    import numpy as np
+    st = np.asarray(starts, dtype=np.int64)
+    w = np.asarray(key_off, dtype=np.uint64)[st] + np.asarray(val_off, dtype=np.uint64)[st]
+    return shard_blocks(w, world)
+
+
+def _dev_items(items, i0, i1, device):
+    """Items [i0, i1) of a host SoA (pyoracle.Items layout) as rebased, padded device tensors."""
+    import numpy as np
+    torch = _torch()
+    k0, k1 = int(items.key_off[i0]), int(items.key_off[i1])
+    v0, v1 = int(items.val_off[i0]), int(items.val_off[i1])
+    d = {"keys": to_device_bytes(items.keys[k0:k1], device), "vals": to_device_bytes(items.vals[v0:v1], device)}
+    d["key_off"] = torch.from_numpy((items.key_off[i0:i1 + 1] - np.uint64(k0)).astype(np.int64)).to(device)
+    d["val_off"] = torch.from_numpy((items.val_off[i0:i1 + 1] - np.uint64(v0)).astype(np.int64)).to(device)
+    d["seqno"] = torch.from_numpy(np.ascontiguousarray(items.seqno[i0:i1]).view(np.int64)).to(device)
+    d["vtype"] = torch.from_numpy(np.ascontiguousarray(items.vtype[i0:i1])).to(device)
+    d["handle_off"] = torch.from_numpy(np.ascontiguousarray(items.handle_off[i0:i1]).view(np.int64)).to(device)
+    d["handle_size"] = torch.from_numpy(np.ascontiguousarray(items.handle_size[i0:i1]).view(np.int32)).to(device)
+    return d
+
+
+def encode_sharded(items, starts, devices, restart_interval=16, hash_ratio=0.0, block_type=BLOCK_DATA):
+    """Single-process multi-device encode:
+    the blocks of a host write buffer (pyoracle.Items layout, starts [n+1]) are
+    split into len(devices) contiguous shards at block cuts (shard_items), each
+    shard is copied to its device and encoded there on that device's current
+    stream (all shards in flight together: the library keeps per-device state
+    only for its LDS attributes), and the one exchange step is the host
+    exclusive scan of the shards' byte totals, which places every shard at its
+    offset in one packed buffer.  Returns (packed bytes, block_off [n+1],
+    status [n]) as host numpy arrays, equal to a single-device encode."""
+    import numpy as np
+    torch = _torch()
+    starts = np.asarray(starts, dtype=np.int64)
+    n_blocks = len(starts) - 1
+    bounds = shard_items(starts, items.key_off, items.val_off, len(devices))
+    pend = []
+    for r, dev in enumerate(devices):
+        b0, b1 = bounds[r], bounds[r + 1]
+        if b1 == b0:
+            continue
+        i0, i1 = int(starts[b0]), int(starts[b1])
+        with torch.cuda.device(dev):
+            d_items = _dev_items(items, i0, i1, dev)
+            d_starts = torch.from_numpy((starts[b0:b1 + 1] - i0).astype(np.int32)).to(dev)
+            enc = Encoder(dev).encode(d_items, d_starts, b1 - b0, restart_interval, hash_ratio, block_type)
+        pend.append((b0, b1, dev, enc))
+    parts, offs, stats, base = [], [np.zeros(1, np.uint64)], [], 0
+    for b0, b1, dev, enc in pend:  # exchange: exclusive scan of the shard totals
+        with torch.cuda.device(dev):
+            torch.cuda.current_stream(dev).synchronize()
+            off = enc["block_off"][:b1 - b0 + 1].cpu().numpy().view(np.uint64)
+            parts.append(enc["buf"][:int(off[-1])].cpu().numpy())
+            stats.append(enc["status"][:b1 - b0].cpu().numpy())
+        offs.append(off[1:] + np.uint64(base))
+        base += int(off[-1])
+    packed = np.concatenate(parts) if parts else np.zeros(0, np.uint8)
+    status = np.concatenate(stats) if stats else np.zeros(0, np.int32)
+    block_off = np.concatenate(offs)
+    assert len(block_off) == n_blocks + 1
+    return packed, block_off, status
+
+
+def decode_sharded(blocks, block_off, devices, expect_type=-1, fields=None):
+    """Single-process multi-device decode: the on-disk blocks
+    of a host buffer (e.g. an mmap'd SST's data section; block_off [n+1]) are
+    split into len(devices) byte-balanced contiguous shards (shard_blocks),
+    each shard is copied to its device and decoded there, all in flight
+    together; the parsed rows are gathered in block order, item_start rebased
+    by the exclusive scan of the shards' item totals.  Returns host numpy
+    arrays: every requested field, item_start [n+1] and status [n]."""
+    import numpy as np
+    torch = _torch()
+    boff = np.asarray(block_off, dtype=np.uint64)
+    data = np.frombuffer(blocks, np.uint8) if isinstance(blocks, (bytes, bytearray, memoryview)) else \
+        np.asarray(blocks, np.uint8)
+    n_blocks = len(boff) - 1
+    bounds = shard_blocks(boff, len(devices))
+    fields = fields or [f for f, _ in PARSED_FIELDS]
+    pend = []
+    for r, dev in enumerate(devices):
+        b0, b1 = bounds[r], bounds[r + 1]
+        if b1 == b0:
+            continue
+        o0, o1 = int(boff[b0]), int(boff[b1])
+        with torch.cuda.device(dev):
+            d_blocks = to_device_bytes(data[o0:o1], dev)
+            d_off = torch.from_numpy((boff[b0:b1 + 1] - np.uint64(o0)).astype(np.int64)).to(dev)
+            cap = (o1 - o0) // 3 + 1
+            dec = Decoder(dev)
+            out = dec.alloc_outputs(cap, b1 - b0, fields)
+            dec.decode(d_blocks, d_off, b1 - b0, out, cap, expect_type)
+        pend.append((b0, b1, dev, out, d_blocks, d_off))
+    res = {f: [] for f in fields}
+    starts, stats, base = [np.zeros(1, np.int64)], [], 0
+    for b0, b1, dev, out, _, _ in pend:
+        with torch.cuda.device(dev):
+            torch.cuda.current_stream(dev).synchronize()
+            ist = out["item_start"][:b1 - b0 + 1].cpu().numpy().astype(np.int64)
+            n = int(ist[-1])
+            for f in fields:
+                res[f].append(out[f][:n].cpu().numpy())
+            stats.append(out["status"][:b1 - b0].cpu().numpy())
+        starts.append(ist[1:] + base)
+        base += n
+    for f in fields:
+        res[f] = np.concatenate(res[f]) if res[f] else np.zeros(0)
+    res["item_start"] = np.concatenate(starts)
+    res["status"] = np.concatenate(stats) if stats else np.zeros(0, np.int32)
+    assert len(res["item_start"]) == n_blocks + 1
+    return res

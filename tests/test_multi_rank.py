@@ -86,3 +86,25 @@ def test_two_rank_gloo_shards_cover_batch():
     seq = np.concatenate([parts[r][bounds[r + 1] - bounds[r]:] for r in range(2)])
     assert (st == status).all()
     assert (seq.view(np.uint64) == parsed["seqno"][:int(item_start[-1])]).all()
+
+
+def test_shard_items_cuts_at_blocks_and_balances_bytes():
+    """Encode-side split: block-aligned, about equal key + value bytes."""
+    import numpy as np
+    import lsmgpu
+    rng = np.random.default_rng(3)
+    per_block = rng.integers(1, 200, 997)
+    starts = np.concatenate([[0], np.cumsum(per_block)]).astype(np.int64)
+    n_items = int(starts[-1])
+    kl = rng.integers(1, 64, n_items).astype(np.uint64)
+    vl = rng.integers(0, 512, n_items).astype(np.uint64)
+    ko = np.concatenate([[0], np.cumsum(kl)]).astype(np.uint64)
+    vo = np.concatenate([[0], np.cumsum(vl)]).astype(np.uint64)
+    for world in (1, 2, 3, 8):
+        b = lsmgpu.shard_items(starts, ko, vo, world)
+        assert len(b) == world + 1 and b[0] == 0 and b[-1] == len(per_block)
+        assert all(x <= y for x, y in zip(b, b[1:]))
+        w = ko[starts] + vo[starts]
+        sizes = [int(w[b[r + 1]] - w[b[r]]) for r in range(world)]
+        blk = np.diff(w.astype(np.int64))
+        assert max(sizes) - min(sizes) <= 2 * int(blk.max())
