@@ -31,6 +31,12 @@ def seq(literals: bytes, offset=None, match_len=0) -> bytes:
             offset.to_bytes(2, "little") + (_ext(ml - 15) if ml >= 15 else b""))
 
 
+def _unaligned_expected(lit300):
+    a = bytes(range(7)) + bytes(range(5))  # 7 literals, then 5 bytes from offset 7
+    b = a + lit300[:257]                   # a 257-byte literal run starting at output byte 12
+    return b + b[len(b) - 200:len(b) - 191] + lit300[:5]
+
+
 def handmade():
     """(name, stream, expected bytes or None for malformed, uncompressed_length)."""
     r = np.random.default_rng(3)
@@ -45,6 +51,9 @@ def handmade():
         ("long_literals_ext", seq(lit300) + b"", lit300),
         ("long_lit_then_long_match", seq(lit300, 300, 270 + 255 * 3) + seq(b"q"),
          lit300 + (lit300 * 4)[:270 + 255 * 3] + b"q"),
+        ("match_ext_past_window", seq(b"ab", 2, 2000) + seq(b"!"), b"ab" * 1001 + b"!"),
+        ("unaligned_literal_runs", seq(bytes(range(7)), 7, 5) + seq(lit300[:257], 200, 9) + seq(lit300[:5]),
+         _unaligned_expected(lit300)),
         ("offset0", seq(b"abcd", 0, 8) + seq(b""), None),
         ("offset_beyond", seq(b"abcd", 5, 8) + seq(b""), None),
         ("truncated_offset", seq(b"abcd", 4, 8)[:-1], None),
