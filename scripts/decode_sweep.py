@@ -63,8 +63,6 @@ def main():
         variants["ablate phase-A only"] = tun(a, 0x800)
         variants["ablate A no-hash"] = tun(a, 0x800 | SKIP_HASH)
         variants["ablate stage-only"] = tun(a, SKIP_HASH | SKIP_PARSE | SKIP_STORE)
-        variants["ablate half-walk"] = tun(a, 0x1000)
-        variants["ablate A-only half-walk"] = tun(a, 0x800 | SKIP_HASH | 0x1000)
     times = {k: [] for k in variants}
     for _ in range(args.rounds):
         for name, tun in variants.items():
