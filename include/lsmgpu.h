@@ -127,9 +127,9 @@ typedef struct lsm_block_params {
  * other than LSM_DECODE_ITEM_START_VALID / LSM_DECODE_PAYLOAD_VERIFIED is
  * rejected with LSM_BAD_ARG. */
 typedef struct lsm_decode_tuning {
-    uint32_t blocks_per_wave;  /* consecutive blocks one workgroup owns (1..63, default 48) */
-    uint32_t stage_bytes;      /* LDS stage bytes (256..65536, default 32768); larger blocks take the general path */
-    uint32_t tile_items;       /* items one stage may hold (default 448, at most 8192) */
+    uint32_t blocks_per_wave;  /* consecutive blocks one workgroup owns (1..63, default 54) */
+    uint32_t stage_bytes;      /* LDS stage bytes (256..65536, default 34560); larger blocks take the general path */
+    uint32_t tile_items;       /* items one stage may hold (default 480, at most 8192) */
     uint32_t flags;            /* LSM_DECODE_ITEM_START_VALID: d_item_start already holds the
                                   prefix sum of this batch (skip the count + scan pass) */
 } lsm_decode_tuning;

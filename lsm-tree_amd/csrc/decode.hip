@@ -7,7 +7,7 @@
 //
 // Launch shape: 4-wave workgroups, four per CU.  Workgroup w
 // owns blocks [w*BPW, (w+1)*BPW) and walks them in GROUPS — the longest run of
-// consecutive blocks that fits the 32 KiB LDS stage (consecutive blocks are
+// consecutive blocks that fits the 33.75 KiB LDS stage (consecutive blocks are
 // contiguous on disk, so a group is one contiguous span):
 //   1. lane j of every wave holds block j's handle and item range;
 //   2. all waves copy the span HBM -> LDS with global_load_lds_dwordx4;
@@ -33,7 +33,13 @@ namespace lsmgpu {
 // -DLSM_DIAG builds; the release library rejects them with LSM_BAD_ARG): drop
 // one phase to price it in a profile.  Outputs are NOT valid with them set.
 
-constexpr uint32_t kMaxGroup = 32;  // blocks per staged group
+// (16 blocks x 80 B of block metadata: the LDS this frees lets the stage hold
+// two 17 KB blocks of the 16 KiB random-key class, or nine 4 KiB blocks,
+// inside the 40 KiB that keeps four workgroups per CU)
+#ifndef LSM_DEC_MAX_GROUP
+#define LSM_DEC_MAX_GROUP 16
+#endif
+constexpr uint32_t kMaxGroup = LSM_DEC_MAX_GROUP;  // blocks per staged group
 // Internal status: the block needs the general path (index block, a record
 // shape the straight-line parsers do not take, a block larger than the
 // stage).  The main kernel lists it; decode_deferred_kernel re-decodes it

@@ -8,11 +8,22 @@
 
 namespace lsmgpu {
 
-// Default decode tuning (lsm_decode_tuning zeros): 48 blocks per 4-wave
-// workgroup, a 32 KiB LDS stage (four workgroups per CU, ~40 KiB LDS each).
-constexpr uint32_t kDefaultBlocksPerWave = 48;
-constexpr uint32_t kDefaultStageBytes = 32768;
-constexpr uint32_t kDefaultTileItems = 448;
+// Default decode tuning (lsm_decode_tuning zeros): 54 blocks per 4-wave
+// workgroup (six groups of nine 4 KiB blocks), a 33.75 KiB LDS stage (two
+// 17 KB blocks of the 16 KiB random-key class), 480 items per group: 40816 B
+// of LDS per workgroup, four workgroups per CU.  Measured against 48 / 32 KiB
+// / 448: configs[1] equal within 1 %, configs[4]'s 16 KiB random class 0.99 ->
+// 0.65 ms (profiles/r02s5_decode_stage_ab.txt).
+#ifndef LSM_DEC_STAGE
+#define LSM_DEC_STAGE 34560
+#define LSM_DEC_TILE 480
+#endif
+#ifndef LSM_DEC_BPW
+#define LSM_DEC_BPW 54
+#endif
+constexpr uint32_t kDefaultBlocksPerWave = LSM_DEC_BPW;
+constexpr uint32_t kDefaultStageBytes = LSM_DEC_STAGE;
+constexpr uint32_t kDefaultTileItems = LSM_DEC_TILE;
 
 struct DecodeParams {
   const uint8_t* blocks;
