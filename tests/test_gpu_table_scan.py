@@ -78,7 +78,7 @@ def test_scan_mixed_tables(gpu, oracle, two_level):
 
 @pytest.mark.parametrize("two_level", [False, True])
 def test_scan_many_blocks(gpu, oracle, two_level):
-    # ~3000 data blocks: several decode workgroups per level, a TLI larger than the 32 KiB stage
+    # ~3000 data blocks: several decode workgroups per level, a TLI larger than the LDS stage
     t = _table(oracle, counter_items(52 * 3000, seed=8), two_level)
     g = _scan(gpu, t, 1)
     _check_against_scanner(oracle, g, t, 1)
