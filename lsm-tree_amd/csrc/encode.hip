@@ -1138,10 +1138,14 @@ __global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(LSM_G
   // (threads past the group's items load its last item), so nothing waits
   // for them until the next iteration cooks them (the plan pass has vetted
   // every group-class item: no `bad` checks here)
+  // Groups of few items (16 KiB blocks of long values: 56 items) give each
+  // item 2 or 4 threads (tpi = 1 << tsh), which split its value copy; thread t
+  // serves item t >> tsh, part t & (tpi - 1).
+  auto tpi_shift = [&](uint32_t n) -> uint32_t { return n <= kGThreads / 4 ? 2u : n <= kGThreads / 2 ? 1u : 0u; };
   auto load_items = [&](const Grp& g, RawItem& r) {
     const uint32_t r0 = g.b - b_begin;
     const uint32_t i0 = rl32(r_start, r0), n = rl32(r_start, r0 + g.k) - i0;
-    const uint64_t i = (uint64_t)i0 + min(tid, n - 1);
+    const uint64_t i = (uint64_t)i0 + min(tid >> tpi_shift(n), n - 1);
     r = load_raw<kIndex>(P, i);
     r.e = P.erec[i];
   };
@@ -1175,7 +1179,8 @@ __global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(LSM_G
     const uint64_t obase = rl64(r_off, r0);
     const uint64_t dabs = (uint64_t)(uintptr_t)P.out + obase;
     const uint32_t pad = (uint32_t)(dabs & 15);
-    const bool live = tid < n_items;
+    const uint32_t tsh = tpi_shift(n_items), part = tid & ((1u << tsh) - 1), item = tid >> tsh;
+    const bool live = item < n_items;
     // the next group's item fields: in flight under this whole group
     const Grp Gn = next_group(G.b + k);
     ItemMeta m = cook(raw);
@@ -1225,10 +1230,12 @@ __global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(LSM_G
     // ---- item t: its block (record offset and shared prefix from E1)
     // (block starts from the run registers, v_readlane: no LDS round trip)
     uint32_t j = 0;
-    for (uint32_t jb = 1; jb < k; ++jb) j += (rl32(r_start, r0 + jb) - i0 <= tid) ? 1u : 0u;
+    for (uint32_t jb = 1; jb < k; ++jb) j += (rl32(r_start, r0 + jb) - i0 <= item) ? 1u : 0u;
     const bool head = (m.e & kErecHead) != 0;
     m.sh = head ? 0u : m.e >> 16;
-    // ---- item t: its record into the image
+    // ---- item t: its record into the image (one thread per item, or for
+    // groups of few items tpi threads per item splitting the value copy)
+    if (tsh == 0) {
     if (live && !(kDiagBuild && (P.diag & 9))) {
       const GBlk& B = L.blk[j];
       const uint32_t roff = m.e & 0x7FFFu;
@@ -1266,6 +1273,55 @@ __global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(LSM_G
         atomicMin(&hlo[bk], ridx);
         atomicMax(&hhi[bk], ridx);
       }
+    }
+    } else {
+    if (live && !(kDiagBuild && (P.diag & 9))) {
+      const GBlk& B = L.blk[j];
+      const uint32_t roff = m.e & 0x7FFFu;
+      const uint32_t p0 = B.img + kHdrLen;
+      uint32_t pos = p0 + roff;
+      const uint32_t kst = (uint32_t)(m.ko - kbase);
+      if (index) {
+        if (part == 0) {
+          L.img[pos++] = 0;
+          pos = lds_put_leb(L.img, pos, m.vo);
+          pos = lds_put_leb(L.img, pos, m.vl);
+          pos = lds_put_leb(L.img, pos, m.seq);
+          pos = lds_put_leb(L.img, pos, m.klen);
+          lds_copy(L.img, pos, L.keys, kst, m.klen, lane);
+        }
+      } else {
+        const uint32_t from = head ? 0 : m.sh;
+        if (part == 0) {  // header varints, key suffix, value length
+          L.img[pos++] = (uint8_t)m.vt;
+          pos = lds_put_leb(L.img, pos, m.seq);
+          if (!head) pos = lds_put_leb(L.img, pos, m.sh);
+          pos = lds_put_leb(L.img, pos, m.klen - from);
+          lds_copy(L.img, pos, L.keys, kst + from, m.klen - from, lane);
+          pos += m.klen - from;
+          if (!is_tombstone(m.vt)) pos = lds_put_leb(L.img, pos, m.vl);
+        }
+        if (!is_tombstone(m.vt)) {  // the value: part q copies bytes [q vl / tpi, (q + 1) vl / tpi)
+          uint32_t vpos = pos;
+          if (part != 0)
+            vpos = p0 + roff + 1 + leb_len(m.seq) + (head ? 0u : leb_len(m.sh)) + leb_len(m.klen - from) +
+                   (m.klen - from) + leb_len(m.vl);
+          const uint32_t va = (part * m.vl) >> tsh, vb = ((part + 1) * m.vl) >> tsh;
+          lds_copy(L.img, vpos + va, L.vals, (uint32_t)(m.vo - vbase) + va, vb - va, lane);
+        }
+      }
+      if (head && part == 0) {
+        const uint32_t bp = p0 + B.recs + 1 + (m.e >> 16) * B.step;
+        for (uint32_t q = 0; q < B.step; ++q) L.img[bp + q] = (uint8_t)(roff >> (8 * q));
+      }
+      if (kHash && B.hash_w && part == 0) {
+        const uint32_t ridx = (item - B.it0) / ri;
+        const uint64_t hv = xxh3_64_any(m.klen, BaseReader8{L.keys, kst}, BaseReader64{L.keys, kst});
+        const uint32_t bk = B.hash_base + (uint32_t)(hv % B.hash_w);
+        atomicMin(&hlo[bk], ridx);
+        atomicMax(&hhi[bk], ridx);
+      }
+    }
     }
     // ---- tails, wave per block: marker, hash-index bytes, trailer (trailer.rs:78-173);
     // without hash indexes they need nothing from the other waves' records
