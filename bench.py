@@ -1068,6 +1068,10 @@ def main():
             "host_inclusive": hostinc or None,
             "gpu_event_ms_per_step": round(gpu_ms / args.steps, 4),
         }
+        if rehearse:  # every rank on cuda:0: a rehearsal of the N > 1 path, never a multi-GPU measurement
+            line["rehearsal"] = True
+            line["physical_gpus"] = 1
+            line["data"] += f"; REHEARSAL: {world} ranks shared one GPU, not a multi-GPU measurement"
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.barrier()

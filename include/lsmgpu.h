@@ -25,6 +25,8 @@
  *   lsm_point_read_blocks <- DataBlock::point_read src/table/data_block/mod.rs:412-472
  *   lsm_seek_blocks    <- data_block::Iter::seek / seek_upper (+ _exclusive)  data_block/iter.rs:37-176
  *   lsm_xxh3_128_file  <- ChecksummedWriter         src/checksum.rs:59-96 (whole-file checksum)
+ *   lsm_xxh3_128_stream_{init,update,digest}
+ *                      <- ChecksummedWriter::{new,write,checksum} src/checksum.rs:59-96 (streaming)
  *   lsm_lz4_decompress_blocks <- Block::from_reader/from_file, CompressionType::Lz4  block/mod.rs:87-182
  *   lsm_lz4_plan_output <- the builder_unzeroed(uncompressed_length) sizing of the same  block/mod.rs:104-112
  *   lsm_lz4_plan_framed / lsm_lz4_decompress_framed + lsm_decode_blocks_tuned(LSM_DECODE_PAYLOAD_VERIFIED)
@@ -210,13 +212,37 @@ int lsm_xxh3_128_batch(const uint8_t* d_data, const uint64_t* d_off, uint32_t n,
                        void* stream);
 /* Whole-file checksum: xxh3_128 of d_data[0 .. len) into d_out[0] (low), d_out[1]
  * (high), spread over the whole GPU (per-KiB contributions in parallel, then
- * one wave runs the scramble chain).  Replaces ChecksummedWriter's streaming
- * digest over an SST file (src/checksum.rs:59-96; equal to the one-shot
- * xxh3_128, tests/table_full_file_checksum.rs:26-31).  d_data readable up to
- * 16 bytes past len; workspace: lsm_xxh3_128_file_workspace_size(len) bytes. */
+ * the scramble chains: 8 waves, one accumulator each).  Replaces
+ * ChecksummedWriter's streaming digest over an SST file held whole in HBM
+ * (src/checksum.rs:59-96; equal to the one-shot xxh3_128,
+ * tests/table_full_file_checksum.rs:26-31).  d_data readable up to 16 bytes
+ * past len; workspace (16-byte aligned, any len incl. 0):
+ * lsm_xxh3_128_file_workspace_size(len) bytes. */
 size_t lsm_xxh3_128_file_workspace_size(uint64_t len);
 int lsm_xxh3_128_file(const uint8_t* d_data, uint64_t len, uint64_t* d_out, void* d_workspace,
                       size_t workspace_bytes, void* stream);
+/* The same checksum as a resumable stream, for a writer that emits the file
+ * piece by piece (ChecksummedWriter::write per flushed region: data blocks,
+ * then index, filter, meta and TOC, src/table/writer/mod.rs:66,99-102):
+ *   init    ChecksummedWriter::new: a fresh running state in d_state
+ *           (device memory, 16-byte aligned, lsm_xxh3_128_stream_state_size()
+ *           bytes, caller-owned);
+ *   update  ChecksummedWriter::write (checksum.rs:92-95): feed d_data[0 .. len)
+ *           (device, any alignment, readable 16 bytes past len); workspace
+ *           lsm_xxh3_128_stream_workspace_size(len) bytes, free again when
+ *           the call's work on `stream` has finished;
+ *   digest  ChecksummedWriter::checksum (Xxh3Default::digest128): xxh3_128 of
+ *           everything fed so far into d_out[0..2] (low, high); the state is
+ *           not changed, so updates may continue.
+ * Any split of the input into updates gives the one-shot xxh3_128 of the
+ * concatenation.  All three are asynchronous on `stream`; calls on one state
+ * must be ordered (same stream, or events). */
+size_t lsm_xxh3_128_stream_state_size(void);
+size_t lsm_xxh3_128_stream_workspace_size(uint64_t len);
+int lsm_xxh3_128_stream_init(void* d_state, void* stream);
+int lsm_xxh3_128_stream_update(void* d_state, const uint8_t* d_data, uint64_t len, void* d_workspace,
+                               size_t workspace_bytes, void* stream);
+int lsm_xxh3_128_stream_digest(const void* d_state, uint64_t* d_out, void* stream);
 
 /* ---- point read -----------------------------------------------------------
  * Batched DataBlock::point_read(needle, snapshot_seqno) (data_block/mod.rs:412-472),

@@ -5,6 +5,8 @@
 // ranges themselves (e.g. Block::write_into of externally built payloads).
 #include <hip/hip_runtime.h>
 
+#include <stddef.h>
+
 #include "decode.hpp"
 #include "device_common.hpp"
 #include "lsmgpu.h"
@@ -26,17 +28,6 @@ __global__ __launch_bounds__(64) void xxh3_128_batch_kernel(const uint8_t* __res
   }
 }
 
-__global__ __launch_bounds__(64) void xxh3_file_short_kernel(const uint8_t* __restrict__ data, uint64_t len,
-                                                             uint64_t* __restrict__ out) {
-  const uint8_t* base = data - ((uintptr_t)data & 15);
-  uint64_t lo, hi;
-  xxh3_128_wave(base, (uint32_t)((uintptr_t)data & 15), (uint32_t)len, &kLongSecret, lo, hi);
-  if (threadIdx.x == 0) {
-    out[0] = lo;
-    out[1] = hi;
-  }
-}
-
 hipError_t launch_xxh3_128_batch(const uint8_t* data, const uint64_t* off, uint32_t n, uint64_t* out,
                                  hipStream_t st) {
   if (n == 0) return hipSuccess;
@@ -44,23 +35,89 @@ hipError_t launch_xxh3_128_batch(const uint8_t* data, const uint64_t* off, uint3
   return hipGetLastError();
 }
 
-// ---- whole-file xxh3_128 (ChecksummedWriter, src/checksum.rs:59-96: the
-// streaming digest equals the one-shot xxh3_128 of the file,
-// tests/table_full_file_checksum.rs:26-31).  One input of any length, spread
-// over the whole GPU: the per-KiB contributions of the XXH3 long loop do not
-// depend on the accumulators, so K1 computes them for every KiB block in
-// parallel (wave per KiB, 64 B per KiB into the workspace) and K2 (one wave)
-// runs the serial scramble chain, the tail stripes and the merge.
-__global__ __launch_bounds__(256) void xxh3_file_contrib_kernel(const uint8_t* __restrict__ data, uint64_t nb,
-                                                                uint64_t* __restrict__ contrib) {
+// ---- whole-file xxh3_128 as a resumable stream (ChecksummedWriter,
+// src/checksum.rs:59-96: every write() feeds a running Xxh3Default, whose
+// digest128 equals the one-shot xxh3_128 of the file,
+// tests/table_full_file_checksum.rs:26-31).
+//
+// The running state lives in device memory (Xxh3Stream).  XXH3's long loop
+// consumes the input in 1 KiB blocks: each block adds a contribution to the 8
+// accumulators that does not depend on them (16 stripes), then scrambles
+// them.  A block is consumed only once at least one byte follows it (a final
+// full KiB is the tail of the one-shot algorithm, never scrambled), so the
+// state keeps 1..1024 pending bytes, plus the 64 bytes before them for the
+// last stripe (input[len-64 .. len) may reach back into consumed data).
+// update(data, len) = K1 the contributions of every KiB block of
+// pending || data that can be consumed (whole GPU, wave per KiB) + K2 the
+// serial scramble chains over them (8 single-wave workgroups, accumulator k
+// on workgroup k) + K3 the new pending / history bytes.  digest() = tail stripes + last stripe + merge
+// (one wave), the state is left unchanged.
+struct alignas(16) Xxh3Stream {
+  uint64_t acc[8];
+  uint64_t total;      // bytes fed so far
+  uint32_t pending;    // bytes in buf (1..1024 once total > 0)
+  uint32_t magic;      // kStreamMagic after init
+  uint8_t pad[48];
+  uint8_t hist[64];    // the 64 bytes just before buf (valid once a KiB block was consumed)
+  uint8_t buf[1024];   // pending bytes
+  uint8_t slack[64];   // readable past buf (window reads)
+};
+static_assert(sizeof(Xxh3Stream) == 1280 && offsetof(Xxh3Stream, hist) == 128 && offsetof(Xxh3Stream, buf) == 192,
+              "Xxh3Stream layout: hist immediately precedes buf");
+constexpr uint32_t kStreamMagic = 0x58583353u;  // "S3XX"
+
+__global__ __launch_bounds__(64) void xxh3_stream_init_kernel(Xxh3Stream* st) {
+  const int lane = threadIdx.x;
+  uint64_t a0, a1;
+  xxh3_acc_init(lane & 3, a0, a1);
+  if (lane < 4) {
+    st->acc[2 * lane] = a0;
+    st->acc[2 * lane + 1] = a1;
+  }
+  if (lane == 0) {
+    st->total = 0;
+    st->pending = 0;
+    st->magic = kStreamMagic;
+  }
+}
+
+// KiB blocks of pending || data that this update consumes: all but the last
+// (partial or full) KiB of the combined input.
+__device__ __forceinline__ uint64_t stream_blocks(uint32_t pending, uint64_t len) {
+  const uint64_t t = (uint64_t)pending + len;
+  return t ? (t - 1) / 1024 : 0;
+}
+
+// K1: wave per consumable KiB block j of pending || data; lane l reduces bytes
+// [1024 j + 16 l, +16) (stripe l >> 2, accumulator pair l & 3).
+__global__ __launch_bounds__(256) void xxh3_stream_contrib_kernel(const Xxh3Stream* __restrict__ st,
+                                                                  const uint8_t* __restrict__ data, uint64_t len,
+                                                                  uint64_t* __restrict__ contrib) {
   const int lane = threadIdx.x & 63;
   const int q = lane & 3, s = lane >> 2;
   const LongSecret* ls = &kLongSecret;
   const uint64_t k0 = ls->acc[s + 2 * q], k1 = ls->acc[s + 2 * q + 1];
+  const uint32_t pend = st->pending;
+  const uint64_t nb = stream_blocks(pend, len);
   const uint64_t waves = (uint64_t)gridDim.x * (blockDim.x / 64);
   for (uint64_t n = (uint64_t)blockIdx.x * (blockDim.x / 64) + (threadIdx.x >> 6); n < nb; n += waves) {
-    const uint64_t a = (uint64_t)(uintptr_t)(data + n * 1024);
-    const Win16 w = read_win16(reinterpret_cast<const uint8_t*>(a & ~15ULL), (uint32_t)(a & 15) + 16 * lane);
+    const uint64_t o = n * 1024 + 16 * lane;  // offset in pending || data
+    Win16 w;
+    if (o >= pend) {
+      const uint64_t a = (uint64_t)(uintptr_t)(data + (o - pend));
+      w = read_win16(reinterpret_cast<const uint8_t*>(a & ~15ULL), (uint32_t)(a & 15));
+    } else if (o + 16 <= pend) {
+      const u32x4 v = *reinterpret_cast<const u32x4*>(st->buf + o);
+      w = Win16{(uint64_t)v.x | ((uint64_t)v.y << 32), (uint64_t)v.z | ((uint64_t)v.w << 32)};
+    } else {  // the 16 bytes straddle the end of the pending bytes
+      uint64_t lo = 0, hi = 0;
+      for (uint32_t i = 0; i < 16; ++i) {
+        const uint64_t x = o + i < pend ? st->buf[o + i] : data[o + i - pend];
+        if (i < 8) lo |= x << (8 * i);
+        else hi |= x << (8 * (i - 8));
+      }
+      w = Win16{lo, hi};
+    }
     uint64_t c0 = 0, c1 = 0;
     stripe_part(w, k0, k1, c0, c1);
     c0 = quad_group_sum64(c0);
@@ -72,111 +129,178 @@ __global__ __launch_bounds__(256) void xxh3_file_contrib_kernel(const uint8_t* _
   }
 }
 
-__global__ __launch_bounds__(64) void xxh3_file_finish_kernel(const uint8_t* __restrict__ data, uint64_t len,
-                                                              const uint64_t* __restrict__ contrib,
-                                                              uint64_t* __restrict__ out) {
+// The serial scramble chain of accumulator k (this wave) over n >= 1 KiB
+// blocks' contributions c[8 i + k], from the accumulator value acc.  One
+// dependent VALU chain per wave: the 8 accumulators are independent, so 8
+// single-wave workgroups (on different SIMDs) run them side by side; a wave
+// holding two chains issues twice the quarter-rate multiplies per step and is
+// slower per step than two waves (scripts/exp/chain_exp.cpp: 1 chain / wave
+// 53 cycles per KiB, 2 chains / wave 79, the one-wave lane-quad chain 133).
+// Step i: acc = scramble(acc + c_i); the addition of c_{i+1} is folded into
+// the addend of the next multiply: y = lo' * P32_1 + (c_{i+1} + (hs * P32_1 << 32)).
+// Contributions arrive 64 steps per coalesced load, kDepth loads in flight,
+// and reach the chain by v_readlane.
+template <int kDepth = 8>
+__device__ __forceinline__ uint64_t xxh3_chain_wave(const uint64_t* __restrict__ c, uint64_t n, uint32_t k,
+                                                     uint64_t acc, uint64_t s) {
   const int lane = threadIdx.x & 63;
-  const int q = lane & 3, s = lane >> 2;
-  const LongSecret* ls = &kLongSecret;
-  const uint64_t k0 = ls->acc[s + 2 * q], k1 = ls->acc[s + 2 * q + 1];
-  uint64_t a0 = q == 0 ? (uint64_t)P32_3 : q == 1 ? P64_2 : q == 2 ? P64_4 : P64_5;
-  uint64_t a1 = q == 0 ? P64_1 : q == 1 ? P64_3 : q == 2 ? (uint64_t)P32_2 : (uint64_t)P32_1;
-  const uint64_t scr0 = ls->acc[16 + 2 * q], scr1 = ls->acc[16 + 2 * q + 1];
-  const uint64_t nb = (len - 1) / 1024;
-  uint64_t n = 0;
-  // The chain is one wave's dependent VALU work; feeding it straight from HBM
-  // stalls on load latency every few steps.  Instead the whole wave streams
-  // the contributions of kChunk KiB blocks (16 KiB) into registers one chunk
-  // ahead, parks them in LDS, and the chain reads LDS only.
-  constexpr uint32_t kChunk = 256;
-  __shared__ u32x4 stage[kChunk * 4];  // 64 B of contributions per KiB block
-  const uint64_t nchunks = nb / kChunk;
-  const u32x4* src = reinterpret_cast<const u32x4*>(contrib);
-  u32x4 r[16];
-  if (nchunks) {
+  const uint32_t s_lo = (uint32_t)s, s_hi = (uint32_t)(s >> 32);
+  // y = acc + c_0, lane-varying by construction (+0): keeps the chain in VGPRs (VALU)
+  uint64_t y = acc + c[k] + __builtin_amdgcn_mbcnt_lo(0, 0);
+  auto step = [&](uint64_t cn) {  // y = scramble(y) + cn
+    const uint32_t hi = (uint32_t)(y >> 32);
+    const uint32_t lo = (uint32_t)y ^ (hi >> 15) ^ s_lo;
+    const uint32_t hs = hi ^ s_hi;
+    y = (uint64_t)lo * P32_1 + (cn + ((uint64_t)(hs * P32_1) << 32));
+  };
+  const uint64_t* cn = c + 8;  // the contributions that follow c_0
+  const uint64_t m = n - 1, full = m / 64;
+  uint64_t buf[kDepth];
 #pragma unroll
-    for (int i = 0; i < 16; ++i) r[i] = __builtin_nontemporal_load(&src[i * 64 + lane]);
-  }
-  for (uint64_t c = 0; c < nchunks; ++c) {
+  for (int d = 0; d < kDepth; ++d) buf[d] = (uint64_t)d < full ? cn[8 * (64 * d + lane) + k] : 0;
+  for (uint64_t b = 0; b < full; ++b) {
+    const uint32_t lo = (uint32_t)buf[0], hi = (uint32_t)(buf[0] >> 32);
 #pragma unroll
-    for (int i = 0; i < 16; ++i) stage[i * 64 + lane] = r[i];
-    __syncthreads();
-    if (c + 1 < nchunks) {
-      const u32x4* nx = src + (c + 1) * kChunk * 4;
+    for (int d = 0; d + 1 < kDepth; ++d) buf[d] = buf[d + 1];
+    buf[kDepth - 1] = b + kDepth < full ? cn[8 * (64 * (b + kDepth) + lane) + k] : 0;
 #pragma unroll
-      for (int i = 0; i < 16; ++i) r[i] = __builtin_nontemporal_load(&nx[i * 64 + lane]);
-    }
-    const uint64_t* st = reinterpret_cast<const uint64_t*>(stage);
-#pragma unroll 8
-    for (uint32_t u = 0; u < kChunk; ++u) {
-      const uint64_t c0 = st[8 * u + 2 * q], c1 = st[8 * u + 2 * q + 1];
-      a0 = xxh3_scr(a0, c0, scr0);
-      a1 = xxh3_scr(a1, c1, scr1);
-    }
-    __syncthreads();
+    for (int t = 0; t < 64; ++t)
+      step((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)lo, t) |
+           ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)hi, t) << 32));
   }
-  n = nchunks * kChunk;
-  for (; n + 4 <= nb; n += 4) {  // contributions of four KiB blocks in flight per step
-    uint64_t c[8];
+  {
+    const uint64_t n0 = full * 64;
+    const uint64_t cl = n0 + lane < m ? cn[8 * (n0 + lane) + k] : 0;
+    const uint32_t lo = (uint32_t)cl, hi = (uint32_t)(cl >> 32);
+    for (uint32_t t = 0; n0 + t < m; ++t)
+      step((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)lo, (int)t) |
+           ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)hi, (int)t) << 32));
+  }
+  step(0);  // the last block's scramble, nothing added after it
+  return y;
+}
+
+// K2: 8 single-wave workgroups; workgroup k carries accumulator k over this
+// update's KiB blocks.
+__global__ __launch_bounds__(64) void xxh3_stream_chain_kernel(Xxh3Stream* __restrict__ st, uint64_t len,
+                                                                const uint64_t* __restrict__ contrib) {
+  const uint32_t k = blockIdx.x;
+  const uint64_t nb = stream_blocks(st->pending, len);
+  if (!nb) return;
+  const uint64_t x = xxh3_chain_wave(contrib, nb, k, st->acc[k], kLongSecret.acc[16 + k]);
+  if (threadIdx.x == 0) st->acc[k] = x;
+}
+
+// K3: the new pending bytes (and the 64 before them) into the state: all
+// reads first, a barrier, then the writes (the new history may come from the
+// old pending bytes).
+__global__ __launch_bounds__(512) void xxh3_stream_buffer_kernel(Xxh3Stream* __restrict__ st,
+                                                                 const uint8_t* __restrict__ data, uint64_t len) {
+  const uint32_t tid = threadIdx.x;
+  const uint32_t pend = st->pending;
+  const uint64_t nb = stream_blocks(pend, len);
+  const uint64_t t = (uint64_t)pend + len;
+  uint8_t v[3] = {0, 0, 0};
+  uint32_t cnt, dst0;
+  uint64_t src0;
+  if (nb) {  // hist || buf = (pending || data)[1024 nb - 64, t)
+    src0 = nb * 1024 - 64;
+    cnt = (uint32_t)(t - src0);
+    dst0 = 0;
+  } else {   // append to the pending bytes
+    src0 = pend;
+    cnt = (uint32_t)len;
+    dst0 = 64 + pend;
+  }
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      c[2 * u] = contrib[8 * (n + u) + 2 * q];
-      c[2 * u + 1] = contrib[8 * (n + u) + 2 * q + 1];
+  for (uint32_t r = 0; r < 3; ++r) {
+    const uint32_t i = tid + 512 * r;
+    if (i < cnt) {
+      const uint64_t x = src0 + i;
+      v[r] = x < pend ? st->buf[x] : data[x - pend];
     }
+  }
+  __syncthreads();
 #pragma unroll
-    for (int u = 0; u < 4; ++u) {
-      a0 = xxh3_scr(a0, c[2 * u], scr0);
-      a1 = xxh3_scr(a1, c[2 * u + 1], scr1);
-    }
+  for (uint32_t r = 0; r < 3; ++r) {
+    const uint32_t i = tid + 512 * r;
+    if (i < cnt) st->hist[dst0 + i] = v[r];  // (hist[64 + j] is buf[j])
   }
-  for (; n < nb; ++n) {
-    a0 = xxh3_scr(a0, contrib[8 * n + 2 * q], scr0);
-    a1 = xxh3_scr(a1, contrib[8 * n + 2 * q + 1], scr1);
-  }
-  {  // tail stripes of the last (partial) KiB block, then the last stripe (secret + 121)
-    const uint64_t tail0 = nb * 1024;
-    const uint32_t nb_stripes = (uint32_t)(((len - 1) - tail0) / 64);
-    uint64_t c0 = 0, c1 = 0;
-    if ((uint32_t)s < nb_stripes) {
-      const uint64_t a = (uint64_t)(uintptr_t)(data + tail0);
-      const Win16 w = read_win16(reinterpret_cast<const uint8_t*>(a & ~15ULL), (uint32_t)(a & 15) + 16 * lane);
-      stripe_part(w, k0, k1, c0, c1);
-    }
-    if (lane < 4) {
-      const uint64_t a = (uint64_t)(uintptr_t)(data + len - 64);
-      const Win16 w = read_win16(reinterpret_cast<const uint8_t*>(a & ~15ULL), (uint32_t)(a & 15) + 16 * lane);
-      stripe_part(w, ls->last[2 * q], ls->last[2 * q + 1], c0, c1);
-    }
-    a0 += quad_group_sum64(c0);
-    a1 += quad_group_sum64(c1);
-  }
-  uint64_t tlo = mul_fold64(a0 ^ ls->mlo[2 * q], a1 ^ ls->mlo[2 * q + 1]);
-  uint64_t thi = mul_fold64(a0 ^ ls->mhi[2 * q], a1 ^ ls->mhi[2 * q + 1]);
-  tlo += shfl_xor64(tlo, 1);
-  thi += shfl_xor64(thi, 1);
-  tlo += shfl_xor64(tlo, 2);
-  thi += shfl_xor64(thi, 2);
-  if (lane == 0) {
-    out[0] = xxh3_avalanche(len * P64_1 + tlo);
-    out[1] = xxh3_avalanche(~(len * P64_2) + thi);
+  if (tid == 0) {
+    st->pending = nb ? (uint32_t)(t - nb * 1024) : (uint32_t)t;
+    st->total += len;
   }
 }
 
-size_t xxh3_file_workspace_size(uint64_t len) { return len > 240 ? ((len - 1) / 1024) * 64 + 256 : 256; }
+// digest128 (Xxh3Default::digest128): the tail stripes of the pending bytes,
+// the last stripe (64 bytes ending at the input's end: hist || buf), the
+// merge and the avalanche.  One wave; the state is not modified.
+__global__ __launch_bounds__(64) void xxh3_stream_digest_kernel(const Xxh3Stream* __restrict__ st,
+                                                                uint64_t* __restrict__ out) {
+  const int lane = threadIdx.x & 63;
+  const int q = lane & 3, s = lane >> 2;
+  const LongSecret* ls = &kLongSecret;
+  const uint8_t* sb = reinterpret_cast<const uint8_t*>(st);
+  const uint64_t len = st->total;
+  const uint32_t pend = st->pending;
+  const uint32_t buf = (uint32_t)offsetof(Xxh3Stream, buf);
+  uint64_t lo, hi;
+  if (len <= 240) {  // short paths: every byte is still pending
+    xxh3_128_wave(sb, buf, (uint32_t)len, ls, lo, hi);
+  } else {
+    uint64_t a0 = st->acc[2 * q], a1 = st->acc[2 * q + 1];
+    const uint32_t nb_stripes = (pend - 1) / 64;
+    uint64_t c0 = 0, c1 = 0;
+    if ((uint32_t)s < nb_stripes)
+      stripe_part(read_win16(sb, buf + 16 * lane), ls->acc[s + 2 * q], ls->acc[s + 2 * q + 1], c0, c1);
+    if (lane < 4) stripe_part(read_win16(sb, buf + pend - 64 + 16 * lane), ls->last[2 * q], ls->last[2 * q + 1], c0, c1);
+    a0 += quad_group_sum64(c0);
+    a1 += quad_group_sum64(c1);
+    uint64_t tlo = mul_fold64(a0 ^ ls->mlo[2 * q], a1 ^ ls->mlo[2 * q + 1]);
+    uint64_t thi = mul_fold64(a0 ^ ls->mhi[2 * q], a1 ^ ls->mhi[2 * q + 1]);
+    tlo += shfl_xor64(tlo, 1);
+    thi += shfl_xor64(thi, 1);
+    tlo += shfl_xor64(tlo, 2);
+    thi += shfl_xor64(thi, 2);
+    lo = xxh3_avalanche(len * P64_1 + tlo);
+    hi = xxh3_avalanche(~(len * P64_2) + thi);
+  }
+  if (lane == 0) {
+    out[0] = lo;
+    out[1] = hi;
+  }
+}
 
-hipError_t launch_xxh3_128_file(const uint8_t* data, uint64_t len, uint64_t* out, void* ws, hipStream_t st) {
-  if (len <= 240) {  // short paths: one wave
-    hipLaunchKernelGGL(xxh3_file_short_kernel, dim3(1), dim3(64), 0, st, data, len, out);
-    return hipGetLastError();
-  }
-  const uint64_t nb = (len - 1) / 1024;
-  uint64_t* contrib = (uint64_t*)ws;
-  if (nb) {
-    const uint64_t wgs = (nb + 3) / 4;
-    hipLaunchKernelGGL(xxh3_file_contrib_kernel, dim3((uint32_t)(wgs < 65536 ? wgs : 65536)), dim3(256), 0, st, data,
-                       nb, contrib);
-  }
-  hipLaunchKernelGGL(xxh3_file_finish_kernel, dim3(1), dim3(64), 0, st, data, len, contrib, out);
+constexpr uint32_t kChainLds = 96 * 1024;
+
+size_t xxh3_stream_workspace_size(uint64_t len) { return 64 * (len / 1024 + 2) + 256; }
+
+hipError_t launch_xxh3_stream_update(Xxh3Stream* st, const uint8_t* data, uint64_t len, uint64_t* contrib,
+                                     hipStream_t s) {
+  if (len == 0) return hipSuccess;
+  const uint64_t kmax = (len + 1023) / 1024 + 1;  // blocks of pending (<= 1024) || data, at most
+  const uint64_t wgs = (kmax + 3) / 4;
+  hipLaunchKernelGGL(xxh3_stream_contrib_kernel, dim3((uint32_t)(wgs < 65536 ? wgs : 65536)), dim3(256), 0, s, st,
+                     data, len, contrib);
+  // (an unused 96 KiB LDS request: one chain workgroup per CU, no two chains share a SIMD)
+  static uint64_t attr_done = 0;
+  hipError_t e = set_lds_attr((const void*)xxh3_stream_chain_kernel, kChainLds, &attr_done);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(xxh3_stream_chain_kernel, dim3(8), dim3(64), kChainLds, s, st, len, contrib);
+  hipLaunchKernelGGL(xxh3_stream_buffer_kernel, dim3(1), dim3(512), 0, s, st, data, len);
+  return hipGetLastError();
+}
+
+size_t xxh3_file_workspace_size(uint64_t len) { return sizeof(Xxh3Stream) + xxh3_stream_workspace_size(len); }
+
+// One-shot whole-file checksum: a stream in the workspace, one update, digest.
+hipError_t launch_xxh3_128_file(const uint8_t* data, uint64_t len, uint64_t* out, void* ws, hipStream_t s) {
+  Xxh3Stream* st = (Xxh3Stream*)ws;
+  uint64_t* contrib = (uint64_t*)((uint8_t*)ws + sizeof(Xxh3Stream));
+  hipLaunchKernelGGL(xxh3_stream_init_kernel, dim3(1), dim3(64), 0, s, st);
+  hipError_t e = launch_xxh3_stream_update(st, data, len, contrib, s);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL(xxh3_stream_digest_kernel, dim3(1), dim3(64), 0, s, st, out);
   return hipGetLastError();
 }
 
@@ -187,7 +311,35 @@ extern "C" size_t lsm_xxh3_128_file_workspace_size(uint64_t len) { return lsmgpu
 extern "C" int lsm_xxh3_128_file(const uint8_t* d_data, uint64_t len, uint64_t* d_out, void* d_workspace,
                                  size_t workspace_bytes, void* stream) {
   if (!d_out || (len && !d_data)) return LSM_BAD_ARG;
-  if (len > 240 && (!d_workspace || workspace_bytes < lsmgpu::xxh3_file_workspace_size(len))) return LSM_BAD_ARG;
+  if (!d_workspace || ((uintptr_t)d_workspace & 15) || workspace_bytes < lsmgpu::xxh3_file_workspace_size(len))
+    return LSM_BAD_ARG;
   const hipError_t e = lsmgpu::launch_xxh3_128_file(d_data, len, d_out, d_workspace, (hipStream_t)stream);
   return lsmgpu::hip_status(e, "lsm_xxh3_128_file");
+}
+
+extern "C" size_t lsm_xxh3_128_stream_state_size(void) { return sizeof(lsmgpu::Xxh3Stream); }
+
+extern "C" int lsm_xxh3_128_stream_init(void* d_state, void* stream) {
+  if (!d_state || ((uintptr_t)d_state & 15)) return LSM_BAD_ARG;
+  hipLaunchKernelGGL(lsmgpu::xxh3_stream_init_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream,
+                     (lsmgpu::Xxh3Stream*)d_state);
+  return lsmgpu::hip_status(hipGetLastError(), "lsm_xxh3_128_stream_init");
+}
+
+extern "C" size_t lsm_xxh3_128_stream_workspace_size(uint64_t len) { return lsmgpu::xxh3_stream_workspace_size(len); }
+
+extern "C" int lsm_xxh3_128_stream_update(void* d_state, const uint8_t* d_data, uint64_t len, void* d_workspace,
+                                          size_t workspace_bytes, void* stream) {
+  if (!d_state || ((uintptr_t)d_state & 15) || (len && !d_data)) return LSM_BAD_ARG;
+  if (len && (!d_workspace || workspace_bytes < lsmgpu::xxh3_stream_workspace_size(len))) return LSM_BAD_ARG;
+  const hipError_t e = lsmgpu::launch_xxh3_stream_update((lsmgpu::Xxh3Stream*)d_state, d_data, len,
+                                                         (uint64_t*)d_workspace, (hipStream_t)stream);
+  return lsmgpu::hip_status(e, "lsm_xxh3_128_stream_update");
+}
+
+extern "C" int lsm_xxh3_128_stream_digest(const void* d_state, uint64_t* d_out, void* stream) {
+  if (!d_state || ((uintptr_t)d_state & 15) || !d_out) return LSM_BAD_ARG;
+  hipLaunchKernelGGL(lsmgpu::xxh3_stream_digest_kernel, dim3(1), dim3(64), 0, (hipStream_t)stream,
+                     (const lsmgpu::Xxh3Stream*)d_state, d_out);
+  return lsmgpu::hip_status(hipGetLastError(), "lsm_xxh3_128_stream_digest");
 }

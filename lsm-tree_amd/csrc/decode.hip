@@ -42,8 +42,10 @@ namespace lsmgpu {
 constexpr uint32_t kMaxGroup = LSM_DEC_MAX_GROUP;  // blocks per staged group
 // Internal status: the block needs the general path (index block, a record
 // shape the straight-line parsers do not take, a block larger than the
-// stage).  The main kernel lists it; decode_deferred_kernel re-decodes it
-// from HBM with the LEB cursor and writes the final status.
+// stage).  The group kernel lists it for decode_big_kernel, which hands on
+// what it cannot take (index blocks, rare shapes, blocks beyond its stage) to
+// decode_deferred_staged_kernel, the general path with the LEB cursor; that
+// one writes the final status.
 constexpr int32_t ST_DEFER = 0x7F;
 constexpr uint32_t kStagePad = 256;  // readable LDS bytes past the span (fast parsers read <= 138)
 
@@ -583,14 +585,6 @@ __device__ __forceinline__ void defer_blocks_wave(const DecodeParams& P, bool pr
   base = (uint32_t)__shfl((int)base, (int)__builtin_ctzll(m));
   const uint32_t rank = (uint32_t)__builtin_popcountll(m & ((1ULL << lane) - 1));
   if (pred) gstore(P.defer_list, base + rank, b);
-}
-
-// General path for the deferred blocks: one wave per block, straight from
-// HBM, Cursor fallback for every record shape (decode_block_direct).
-__global__ __launch_bounds__(kWave) void decode_deferred_kernel(DecodeParams P) {
-  __shared__ BlockMeta meta[1];
-  const uint32_t n = gload(P.defer_count, 0);
-  for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) decode_block_direct(P, gload(P.defer_list, i), meta);
 }
 
 // Deferred blocks up to kBigStage bytes (the 16..64 KiB data blocks larger

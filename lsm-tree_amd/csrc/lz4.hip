@@ -148,7 +148,7 @@ struct Lz4Block {
 
 // Header + payload checksum (Block::from_reader, mod.rs:92-102); wave-uniform.
 // frame = 0 (payload only) or kHdrLen (lsm_lz4_decompress_framed: the payload
-// follows a frame header written by lz4_frame_headers_kernel).
+// follows a frame header written by lz4_write_frame_header).
 __device__ __forceinline__ int32_t lz4_check_block(const uint8_t* blocks, const uint64_t* block_off, const uint64_t* out_off,
                                    uint8_t* out, uint32_t i, uint32_t frame, Lz4Block& b) {
   const uint64_t o = block_off[i], e = block_off[i + 1];
@@ -203,6 +203,36 @@ __device__ __forceinline__ int32_t lz4_stage_and_decode(const Lz4Block& b, uint3
   return ST_OK;
 }
 
+// Frame header of lsm_lz4_decompress_framed for block i (one lane): the
+// stored header with data_length = uncompressed_length and the header checksum
+// recomputed over the new first 29 bytes (header.rs:83-109), so the frame is a
+// well-formed uncompressed block whose payload checksum field still names the
+// stored bytes (decoded with LSM_DECODE_PAYLOAD_VERIFIED).  Written only once
+// the block's decompression has succeeded; a block that failed (payload
+// checksum, Error::Decompress, length mismatch) gets an all-zero frame header
+// instead, so a decode of the frames reports BAD_MAGIC for it on its own even
+// if the caller never merges the decompress statuses.  Blocks whose plan gave
+// no frame (failed header) have nothing to write.
+__device__ __forceinline__ void lz4_write_frame_header(const uint8_t* blocks, const uint64_t* block_off, uint32_t i,
+                                                       uint8_t* out, const uint64_t* out_off, bool ok) {
+  const uint64_t fo = out_off[i];
+  if (out_off[i + 1] - fo < kHdrLen) return;
+  uint32_t h[12] = {0};  // 29 header bytes + the readers' 12-byte over-read
+  uint8_t* hp = reinterpret_cast<uint8_t*>(h);
+  if (ok) {
+    const uint64_t o = block_off[i];
+    const uint8_t* base = blocks + (o & ~15ULL);
+    const uint32_t hb = (uint32_t)(o & 15);
+    for (uint32_t j = 0; j < 21; ++j) hp[j] = base[hb + j];  // magic, type, stored checksum
+    const uint32_t ul = read_u32_unaligned(base, hb + 25);
+    for (uint32_t j = 0; j < 4; ++j) hp[21 + j] = hp[25 + j] = (uint8_t)(ul >> (8 * j));
+    uint64_t lo, hi;
+    xxh3_128_short(29, BaseReader8{hp, 0}, BaseReader64{hp, 0}, lo, hi);
+    for (uint32_t j = 0; j < 4; ++j) hp[29 + j] = (uint8_t)(lo >> (8 * j));
+  }
+  for (uint32_t j = 0; j < kHdrLen; ++j) out[fo + j] = hp[j];
+}
+
 constexpr uint32_t kSmallIn = 5120, kSmallOut = 5120;  // 40 KiB per 4-wave workgroup: 4 per CU
 constexpr uint32_t kLargeIn = 72 * 1024, kLargeOut = 80 * 1024;
 
@@ -224,7 +254,10 @@ __global__ __launch_bounds__(256) void lz4_small_kernel(const uint8_t* __restric
     else
       st = lz4_stage_and_decode<kSmallIn, kSmallOut>(b, s_in[wv], s_out[wv], lane);
   }
-  if (lane == 0) status[i] = st;
+  if (lane == 0) {
+    if (frame && st != kLz4Deferred) lz4_write_frame_header(blocks, block_off, i, out, out_off, st == ST_OK);
+    status[i] = st;
+  }
 }
 
 __global__ __launch_bounds__(64) void lz4_large_kernel(const uint8_t* __restrict__ blocks,
@@ -250,7 +283,10 @@ __global__ __launch_bounds__(64) void lz4_large_kernel(const uint8_t* __restrict
         st = got == (int64_t)b.raw_len ? ST_OK : LSM_DECOMPRESS;
       }
     }
-    if (lane == 0) status[i] = st;
+    if (lane == 0) {
+      if (frame) lz4_write_frame_header(blocks, block_off, i, out, out_off, st == ST_OK);
+      status[i] = st;
+    }
   }
 }
 
@@ -280,34 +316,6 @@ __global__ __launch_bounds__(256) void lz4_plan_kernel(const uint8_t* __restrict
     len = len > max_raw ? 0 : len + frame;
   }
   raw[i] = len;
-}
-
-// Frame headers of lsm_lz4_decompress_framed (lane per block): the stored
-// header with data_length = uncompressed_length and the header checksum
-// recomputed over the new first 29 bytes (header.rs:83-109), so the frame is a
-// well-formed uncompressed block whose payload checksum field still names the
-// stored bytes (decoded with LSM_DECODE_PAYLOAD_VERIFIED).  Blocks whose plan
-// gave no frame (failed header) are skipped.
-__global__ __launch_bounds__(256) void lz4_frame_headers_kernel(const uint8_t* __restrict__ blocks,
-                                                                const uint64_t* __restrict__ block_off, uint32_t n,
-                                                                uint8_t* __restrict__ out,
-                                                                const uint64_t* __restrict__ out_off) {
-  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-  if (i >= n) return;
-  const uint64_t fo = out_off[i];
-  if (out_off[i + 1] - fo < kHdrLen) return;
-  const uint64_t o = block_off[i];
-  const uint8_t* base = blocks + (o & ~15ULL);
-  const uint32_t hb = (uint32_t)(o & 15);
-  uint32_t h[12] = {0};  // 29 header bytes + the readers' 12-byte over-read
-  uint8_t* hp = reinterpret_cast<uint8_t*>(h);
-  for (uint32_t j = 0; j < 21; ++j) hp[j] = base[hb + j];           // magic, type, stored checksum
-  const uint32_t ul = read_u32_unaligned(base, hb + 25);
-  for (uint32_t j = 0; j < 4; ++j) hp[21 + j] = hp[25 + j] = (uint8_t)(ul >> (8 * j));
-  uint64_t lo, hi;
-  xxh3_128_short(29, BaseReader8{hp, 0}, BaseReader64{hp, 0}, lo, hi);
-  for (uint32_t j = 0; j < 4; ++j) hp[29 + j] = (uint8_t)(lo >> (8 * j));
-  for (uint32_t j = 0; j < kHdrLen; ++j) out[fo + j] = hp[j];
 }
 
 struct Lz4OffOut {
@@ -365,9 +373,6 @@ static int lz4_decompress(const uint8_t* d_blocks, const uint64_t* d_block_off, 
   uint32_t* list = count + 4;
   hipError_t e = hipMemsetAsync(count, 0, 4, st);
   if (e != hipSuccess) return hip_status(e, "lsm_lz4_decompress_blocks");
-  if (frame)
-    hipLaunchKernelGGL(lz4_frame_headers_kernel, dim3((n_blocks + 255) / 256), dim3(256), 0, st, d_blocks, d_block_off,
-                       n_blocks, d_out, d_out_off);
   hipLaunchKernelGGL(lz4_small_kernel, dim3((n_blocks + 3) / 4), dim3(256), 0, st, d_blocks, d_block_off, n_blocks,
                      d_out, d_out_off, d_status, frame);
   hipLaunchKernelGGL(lz4_collect_deferred, dim3((n_blocks + 255) / 256), dim3(256), 0, st, d_status, n_blocks, list,

@@ -111,6 +111,17 @@ def lib():
         L.lsm_xxh3_128_file_workspace_size.argtypes = [C.c_uint64]
         L.lsm_xxh3_128_file.restype = C.c_int
         L.lsm_xxh3_128_file.argtypes = [C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]
+        L.lsm_xxh3_128_stream_state_size.restype = C.c_size_t
+        L.lsm_xxh3_128_stream_state_size.argtypes = []
+        L.lsm_xxh3_128_stream_workspace_size.restype = C.c_size_t
+        L.lsm_xxh3_128_stream_workspace_size.argtypes = [C.c_uint64]
+        L.lsm_xxh3_128_stream_init.restype = C.c_int
+        L.lsm_xxh3_128_stream_init.argtypes = [C.c_void_p, C.c_void_p]
+        L.lsm_xxh3_128_stream_update.restype = C.c_int
+        L.lsm_xxh3_128_stream_update.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_void_p, C.c_size_t,
+                                                 C.c_void_p]
+        L.lsm_xxh3_128_stream_digest.restype = C.c_int
+        L.lsm_xxh3_128_stream_digest.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
         L.lsm_point_read_blocks.restype = C.c_int
         L.lsm_point_read_blocks.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p,
                                             C.c_void_p, C.c_uint32, C.POINTER(LsmPointResult), C.c_void_p,
@@ -174,7 +185,9 @@ EXPORTED_SYMBOLS = ["lsm_abi_version", "lsm_status_name", "lsm_last_error", "lsm
                     "lsm_bloom_build", "lsm_bloom_contains", "lsm_lz4_workspace_size", "lsm_lz4_decompress_blocks",
                     "lsm_lz4_plan_workspace_size", "lsm_lz4_plan_output", "lsm_seek_blocks", "lsm_lz4_plan_framed",
                     "lsm_lz4_decompress_framed", "lsm_scan_workspace_size", "lsm_scan_table",
-                    "lsm_materialize_workspace_size", "lsm_materialize_plan", "lsm_materialize_keys"]
+                    "lsm_materialize_workspace_size", "lsm_materialize_plan", "lsm_materialize_keys",
+                    "lsm_xxh3_128_stream_state_size", "lsm_xxh3_128_stream_workspace_size",
+                    "lsm_xxh3_128_stream_init", "lsm_xxh3_128_stream_update", "lsm_xxh3_128_stream_digest"]
 
 
 def _check(rc, what):
@@ -379,6 +392,45 @@ def xxh3_128_file(data, length=None, offset=0, stream=None):
     return lo, hi
 
 
+class ChecksummedWriter:
+    """The running whole-file checksum of an SST writer (ChecksummedWriter,
+    src/checksum.rs:59-96) with its state in device memory: write(data) feeds
+    the next bytes (ChecksummedWriter::write, checksum.rs:92-95),
+    checksum() is Xxh3Default::digest128 of everything written so far, as
+    (low, high) Python ints (synchronises; the state is kept, writes may go on).
+    Any split of the file into writes gives the one-shot xxh3_128."""
+
+    def __init__(self, device=None, stream=None):
+        torch = _torch()
+        self.device = torch.device("cuda") if device is None else torch.device(device)
+        self.stream = stream
+        self.state = torch.empty(lib().lsm_xxh3_128_stream_state_size(), dtype=torch.uint8, device=self.device)
+        self._ws = torch.empty(0, dtype=torch.uint8, device=self.device)
+        self.bytes_written = 0
+        _check(lib().lsm_xxh3_128_stream_init(_ptr(self.state), _stream(stream)), "lsm_xxh3_128_stream_init")
+
+    def write(self, data, length=None, offset=0):
+        """Feed data[offset .. offset + length) (uint8 cuda tensor, readable 16 B past the end)."""
+        torch = _torch()
+        length = data.numel() - offset if length is None else length
+        need = lib().lsm_xxh3_128_stream_workspace_size(length)
+        if self._ws.numel() < need:
+            self._ws = torch.empty(need, dtype=torch.uint8, device=self.device)
+        _check(lib().lsm_xxh3_128_stream_update(_ptr(self.state), C.c_void_p(data.data_ptr() + offset), length,
+                                                _ptr(self._ws), self._ws.numel(), _stream(self.stream)),
+               "lsm_xxh3_128_stream_update")
+        self.bytes_written += length
+        return length
+
+    def checksum(self):
+        torch = _torch()
+        out = torch.zeros(2, dtype=torch.int64, device=self.device)
+        _check(lib().lsm_xxh3_128_stream_digest(_ptr(self.state), _ptr(out), _stream(self.stream)),
+               "lsm_xxh3_128_stream_digest")
+        lo, hi = (int(x) & (2 ** 64 - 1) for x in out.cpu().tolist())
+        return lo, hi
+
+
 BLOOM_BITS_PER_KEY, BLOOM_FP_RATE, BLOOM_BAD_FILTER = 0, 1, 0xFF
 
 
@@ -421,8 +473,13 @@ def bloom_contains(filt, hashes, stream=None):
     return out[:hashes.numel()]
 
 
-# the largest uncompressed block the default writer makes is 4 MiB (writer/mod.rs:195-198)
-LZ4_MAX_BLOCK = 1 << 26
+# Default cap on a header's uncompressed_length (the plan sizes the output from
+# verified headers only, but a crafted header per block could still ask for
+# this much): the writer's largest data-block target is 4 MiB
+# (writer/mod.rs:195-198) and a block overshoots its target by its last item
+# (mod.rs:284-290), so 4 MiB + 64 KiB covers tables of items < 64 KiB; pass a
+# larger max_block_bytes for tables with larger items.
+LZ4_MAX_BLOCK = (4 << 20) + (64 << 10)
 
 
 def lz4_decompress_blocks(blocks, block_off, n_blocks=None, max_block_bytes=LZ4_MAX_BLOCK, stream=None):
@@ -458,7 +515,9 @@ def decode_lz4_blocks(blocks, block_off, n_blocks=None, expect_type=-1, item_cap
     lsm_decode_blocks_tuned(frames, LSM_DECODE_PAYLOAD_VERIFIED).  Returns the decode
     output dict (payload-relative offsets into each frame's payload) plus "frames",
     "frame_off" and "status" = the decompress status where it is not OK, else the
-    decode status."""
+    decode status ("decode_status": the decode's own statuses: a block whose
+    decompression failed has an all-zero frame header, so it is BAD_MAGIC there
+    even without the merge)."""
     torch = _torch()
     n = block_off.numel() - 1 if n_blocks is None else n_blocks
     dev = blocks.device
@@ -480,6 +539,7 @@ def decode_lz4_blocks(blocks, block_off, n_blocks=None, expect_type=-1, item_cap
     out = d.alloc_outputs(item_cap, n, fields)
     d.decode(frames, frame_off, n, out, item_cap, expect_type,
              tuning=(0, 0, 0, DECODE_PAYLOAD_VERIFIED), stream=stream)
+    out["decode_status"] = out["status"].clone()  # (what a caller sees without the merge below)
     out["status"] = torch.where(zst[:max(n, 1)] != 0, zst[:max(n, 1)], out["status"])
     out["frames"], out["frame_off"] = frames, frame_off
     return out

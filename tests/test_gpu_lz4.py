@@ -161,6 +161,13 @@ def test_lz4_chained_parse(gpu):
     want = [OK] * len(blocks)
     want[3], want[7], want[9] = CKSUM, DECOMPRESS, 7
     assert st.tolist() == want
+    # without the status merge: a block whose decompression failed still reports an
+    # error from the decode alone (its frame header is all zero: BAD_MAGIC), never OK
+    dst = out["decode_status"].cpu().numpy()[:len(blocks)]
+    assert dst[3] == BAD_MAGIC and dst[7] == BAD_MAGIC and dst[9] == 7
+    fr = out["frames"].cpu().numpy()
+    fo = out["frame_off"].cpu().numpy()
+    assert not fr[fo[3]:fo[3] + 33].any() and not fr[fo[7]:fo[7] + 33].any()
     starts = out["item_start"].cpu().numpy().view(np.uint32)
     frames = out["frames"].cpu().numpy()
     foff = out["frame_off"].cpu().numpy()
