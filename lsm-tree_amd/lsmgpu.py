@@ -664,44 +664,118 @@ def _dev_items(items, i0, i1, device):
     return d
 
 
+def _pinned(arr):
+    """A host numpy array copied into page-locked memory (torch tensor; the copy
+    runs in numpy, which releases the GIL for it)."""
+    import numpy as np
+    torch = _torch()
+    a = np.ascontiguousarray(arr)
+    t = torch.empty(a.nbytes, dtype=torch.uint8, pin_memory=True)
+    if a.nbytes:
+        np.copyto(t.numpy(), a.view(np.uint8).reshape(-1))
+    return t
+
+
+def _run_shards(jobs, worker):
+    """One host thread per shard (each drives its own device and stream; the
+    library calls and torch copies release the GIL), with a barrier for the one
+    exchange step.  worker(k, job, barrier) -> result; a failing shard aborts
+    the barrier so no other shard waits forever, and its exception is raised."""
+    import threading
+    from concurrent.futures import ThreadPoolExecutor
+    if not jobs:
+        return []
+    barrier = threading.Barrier(len(jobs))
+
+    def run(k):
+        try:
+            return worker(k, jobs[k], barrier)
+        except BaseException:
+            barrier.abort()
+            raise
+    with ThreadPoolExecutor(max_workers=len(jobs)) as ex:
+        futs = [ex.submit(run, k) for k in range(len(jobs))]
+        return [f.result() for f in futs]
+
+
 def encode_sharded(items, starts, devices, restart_interval=16, hash_ratio=0.0, block_type=BLOCK_DATA):
     """Single-process multi-device encode:
     the blocks of a host write buffer (pyoracle.Items layout, starts [n+1]) are
-    split into len(devices) contiguous shards at block cuts (shard_items), each
-    shard is copied to its device and encoded there on that device's current
-    stream (all shards in flight together: the library keeps per-device state
-    only for its LDS attributes), and the one exchange step is the host
-    exclusive scan of the shards' byte totals, which places every shard at its
-    offset in one packed buffer.  Returns (packed bytes, block_off [n+1],
-    status [n]) as host numpy arrays, equal to a single-device encode."""
+    split into len(devices) contiguous shards at block cuts (shard_items).  One
+    host thread per shard: it stages the shard's items in pinned memory, copies
+    them to its device on its own stream, encodes there and reads back the
+    shard's block offsets; the one exchange step is the exclusive scan of the
+    shards' byte totals (a barrier across the threads), after which every
+    thread copies its blocks asynchronously into its place in one pinned packed
+    buffer.  Shards overlap end to end (no blocking copy serialises them).
+    Returns (packed bytes, block_off [n+1], status [n]) as host numpy arrays,
+    equal to a single-device encode."""
     import numpy as np
     torch = _torch()
     starts = np.asarray(starts, dtype=np.int64)
     n_blocks = len(starts) - 1
     bounds = shard_items(starts, items.key_off, items.val_off, len(devices))
-    pend = []
-    for r, dev in enumerate(devices):
-        b0, b1 = bounds[r], bounds[r + 1]
-        if b1 == b0:
-            continue
+    jobs = [(dev, bounds[r], bounds[r + 1]) for r, dev in enumerate(devices) if bounds[r + 1] > bounds[r]]
+    totals = [0] * len(jobs)
+    shared = {}
+
+    def worker(k, job, barrier):
+        dev, b0, b1 = job
+        dev = torch.device("cuda", dev) if isinstance(dev, int) else torch.device(dev)
+        torch.cuda.set_device(dev)
         i0, i1 = int(starts[b0]), int(starts[b1])
-        with torch.cuda.device(dev):
-            d_items = _dev_items(items, i0, i1, dev)
-            d_starts = torch.from_numpy((starts[b0:b1 + 1] - i0).astype(np.int32)).to(dev)
-            enc = Encoder(dev).encode(d_items, d_starts, b1 - b0, restart_interval, hash_ratio, block_type)
-        pend.append((b0, b1, dev, enc))
-    parts, offs, stats, base = [], [np.zeros(1, np.uint64)], [], 0
-    for b0, b1, dev, enc in pend:  # exchange: exclusive scan of the shard totals
-        with torch.cuda.device(dev):
-            torch.cuda.current_stream(dev).synchronize()
-            off = enc["block_off"][:b1 - b0 + 1].cpu().numpy().view(np.uint64)
-            parts.append(enc["buf"][:int(off[-1])].cpu().numpy())
-            stats.append(enc["status"][:b1 - b0].cpu().numpy())
-        offs.append(off[1:] + np.uint64(base))
-        base += int(off[-1])
-    packed = np.concatenate(parts) if parts else np.zeros(0, np.uint8)
-    status = np.concatenate(stats) if stats else np.zeros(0, np.int32)
-    block_off = np.concatenate(offs)
+        k0, k1 = int(items.key_off[i0]), int(items.key_off[i1])
+        v0, v1 = int(items.val_off[i0]), int(items.val_off[i1])
+        host = {"keys": _pinned(items.keys[k0:k1]), "vals": _pinned(items.vals[v0:v1]),
+                "key_off": _pinned((items.key_off[i0:i1 + 1] - np.uint64(k0)).astype(np.int64)),
+                "val_off": _pinned((items.val_off[i0:i1 + 1] - np.uint64(v0)).astype(np.int64)),
+                "seqno": _pinned(items.seqno[i0:i1]), "vtype": _pinned(items.vtype[i0:i1]),
+                "starts": _pinned((starts[b0:b1 + 1] - i0).astype(np.int32))}
+        if items.handle_off is not None:
+            host["handle_off"] = _pinned(items.handle_off[i0:i1])
+            host["handle_size"] = _pinned(items.handle_size[i0:i1])
+        st = torch.cuda.Stream(dev)
+        nb = b1 - b0
+        with torch.cuda.stream(st):
+            d = {}
+            for name, dt in (("keys", torch.uint8), ("vals", torch.uint8), ("key_off", torch.int64),
+                             ("val_off", torch.int64), ("seqno", torch.int64), ("vtype", torch.uint8),
+                             ("handle_off", torch.int64), ("handle_size", torch.int32)):
+                if name not in host:
+                    continue
+                h = host[name].view(dt)
+                if name in ("keys", "vals"):
+                    t = padded_bytes(h.numel(), dev)
+                    t[:h.numel()].copy_(h, non_blocking=True)
+                else:
+                    t = torch.empty(h.numel(), dtype=dt, device=dev)
+                    t.copy_(h, non_blocking=True)
+                d[name] = t
+            d_starts = torch.empty(nb + 1, dtype=torch.int32, device=dev)
+            d_starts.copy_(host["starts"].view(torch.int32), non_blocking=True)
+            enc = Encoder(dev).encode(d, d_starts, nb, restart_interval, hash_ratio, block_type, stream=st)
+            off_h = torch.empty(nb + 1, dtype=torch.int64, pin_memory=True)
+            st_h = torch.empty(nb, dtype=torch.int32, pin_memory=True)
+            off_h.copy_(enc["block_off"][:nb + 1], non_blocking=True)
+            st_h.copy_(enc["status"][:nb], non_blocking=True)
+        st.synchronize()
+        totals[k] = int(off_h[-1])
+        barrier.wait()  # exchange: every shard's byte total is known
+        if k == 0:
+            shared["packed"] = torch.empty(sum(totals), dtype=torch.uint8, pin_memory=True)
+        barrier.wait()
+        base = sum(totals[:k])
+        with torch.cuda.stream(st):
+            if totals[k]:
+                shared["packed"][base:base + totals[k]].copy_(enc["buf"][:totals[k]], non_blocking=True)
+        st.synchronize()
+        off = off_h.numpy().view(np.uint64)
+        return off[1:] + np.uint64(base), st_h.numpy().copy()
+
+    res = _run_shards(jobs, worker)
+    packed = shared["packed"].numpy() if jobs else np.zeros(0, np.uint8)
+    block_off = np.concatenate([np.zeros(1, np.uint64)] + [r[0] for r in res])
+    status = np.concatenate([r[1] for r in res]) if res else np.zeros(0, np.int32)
     assert len(block_off) == n_blocks + 1
     return packed, block_off, status
 
@@ -709,11 +783,13 @@ def encode_sharded(items, starts, devices, restart_interval=16, hash_ratio=0.0, 
 def decode_sharded(blocks, block_off, devices, expect_type=-1, fields=None):
     """Single-process multi-device decode: the on-disk blocks
     of a host buffer (e.g. an mmap'd SST's data section; block_off [n+1]) are
-    split into len(devices) byte-balanced contiguous shards (shard_blocks),
-    each shard is copied to its device and decoded there, all in flight
-    together; the parsed rows are gathered in block order, item_start rebased
-    by the exclusive scan of the shards' item totals.  Returns host numpy
-    arrays: every requested field, item_start [n+1] and status [n]."""
+    split into len(devices) byte-balanced contiguous shards (shard_blocks).  One
+    host thread per shard stages its bytes in pinned memory, copies them to its
+    device on its own stream and decodes there; after the exchange step (the
+    exclusive scan of the shards' item totals, a barrier across the threads)
+    each thread copies its rows asynchronously into one pinned gather buffer
+    per field, item_start rebased.  Returns host numpy arrays: every requested
+    field, item_start [n+1] and status [n]."""
     import numpy as np
     torch = _torch()
     boff = np.asarray(block_off, dtype=np.uint64)
@@ -722,35 +798,52 @@ def decode_sharded(blocks, block_off, devices, expect_type=-1, fields=None):
     n_blocks = len(boff) - 1
     bounds = shard_blocks(boff, len(devices))
     fields = fields or [f for f, _ in PARSED_FIELDS]
-    pend = []
-    for r, dev in enumerate(devices):
-        b0, b1 = bounds[r], bounds[r + 1]
-        if b1 == b0:
-            continue
+    jobs = [(dev, bounds[r], bounds[r + 1]) for r, dev in enumerate(devices) if bounds[r + 1] > bounds[r]]
+    counts = [0] * len(jobs)
+    shared = {}
+
+    def worker(k, job, barrier):
+        dev, b0, b1 = job
+        dev = torch.device("cuda", dev) if isinstance(dev, int) else torch.device(dev)
+        torch.cuda.set_device(dev)
         o0, o1 = int(boff[b0]), int(boff[b1])
-        with torch.cuda.device(dev):
-            d_blocks = to_device_bytes(data[o0:o1], dev)
-            d_off = torch.from_numpy((boff[b0:b1 + 1] - np.uint64(o0)).astype(np.int64)).to(dev)
-            cap = (o1 - o0) // 3 + 1
+        nb = b1 - b0
+        hb = _pinned(data[o0:o1])
+        ho = _pinned((boff[b0:b1 + 1] - np.uint64(o0)).astype(np.int64))
+        st = torch.cuda.Stream(dev)
+        cap = (o1 - o0) // 3 + 1
+        with torch.cuda.stream(st):
+            d_blocks = padded_bytes(o1 - o0, dev)
+            d_blocks[:o1 - o0].copy_(hb, non_blocking=True)
+            d_off = torch.empty(nb + 1, dtype=torch.int64, device=dev)
+            d_off.copy_(ho.view(torch.int64), non_blocking=True)
             dec = Decoder(dev)
-            out = dec.alloc_outputs(cap, b1 - b0, fields)
-            dec.decode(d_blocks, d_off, b1 - b0, out, cap, expect_type)
-        pend.append((b0, b1, dev, out, d_blocks, d_off))
-    res = {f: [] for f in fields}
-    starts, stats, base = [np.zeros(1, np.int64)], [], 0
-    for b0, b1, dev, out, _, _ in pend:
-        with torch.cuda.device(dev):
-            torch.cuda.current_stream(dev).synchronize()
-            ist = out["item_start"][:b1 - b0 + 1].cpu().numpy().astype(np.int64)
-            n = int(ist[-1])
-            for f in fields:
-                res[f].append(out[f][:n].cpu().numpy())
-            stats.append(out["status"][:b1 - b0].cpu().numpy())
-        starts.append(ist[1:] + base)
-        base += n
-    for f in fields:
-        res[f] = np.concatenate(res[f]) if res[f] else np.zeros(0)
-    res["item_start"] = np.concatenate(starts)
-    res["status"] = np.concatenate(stats) if stats else np.zeros(0, np.int32)
+            out = dec.alloc_outputs(cap, nb, fields)
+            dec.decode(d_blocks, d_off, nb, out, cap, expect_type, stream=st)
+            ist_h = torch.empty(nb + 1, dtype=torch.int32, pin_memory=True)
+            st_h = torch.empty(nb, dtype=torch.int32, pin_memory=True)
+            ist_h.copy_(out["item_start"][:nb + 1], non_blocking=True)
+            st_h.copy_(out["status"][:nb], non_blocking=True)
+        st.synchronize()
+        ist = ist_h.numpy().view(np.uint32).astype(np.int64)
+        counts[k] = int(ist[-1])
+        barrier.wait()  # exchange: every shard's item total is known
+        if k == 0:
+            tot = sum(counts)
+            shared.update({f: torch.empty(max(tot, 1), dtype=out[f].dtype, pin_memory=True) for f in fields})
+        barrier.wait()
+        base = sum(counts[:k])
+        with torch.cuda.stream(st):
+            if counts[k]:
+                for f in fields:
+                    shared[f][base:base + counts[k]].copy_(out[f][:counts[k]], non_blocking=True)
+        st.synchronize()
+        return ist[1:] + base, st_h.numpy().copy()
+
+    res_sh = _run_shards(jobs, worker)
+    total = sum(counts)
+    res = {f: (shared[f][:total].numpy() if jobs else np.zeros(0)) for f in fields}
+    res["item_start"] = np.concatenate([np.zeros(1, np.int64)] + [r[0] for r in res_sh])
+    res["status"] = np.concatenate([r[1] for r in res_sh]) if res_sh else np.zeros(0, np.int32)
     assert len(res["item_start"]) == n_blocks + 1
     return res

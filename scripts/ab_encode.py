@@ -1,0 +1,89 @@
+#!/usr/bin/env python3
+"""A/B timing of library variants on the encode (and decode) bench workloads.
+
+usage: scripts/ab_encode.py LIB1 LIB2 ... [--rounds 3]
+Each round runs every library in its own child process (interleaved, rule 24 of
+the HIP guide); a child times lsm_encode_blocks on configs[1] (1 M x 4 KiB) and
+configs[3] (256 K x 16 KiB prefix keys) and prints the xxh3_128 of the encoded
+bytes, so variants can be compared for identical output.
+"""
+import json
+import os
+import subprocess
+import sys
+from pathlib import Path
+
+ROOT = Path(__file__).resolve().parent.parent
+
+
+def child(reps, which):
+    for p in (ROOT, ROOT / "lsm-tree_amd", ROOT / "oracle", ROOT / "tests"):
+        sys.path.insert(0, str(p))
+    import torch
+    import bench
+    import lsmgpu
+    torch.cuda.set_device(0)
+    res = {}
+    shapes = {"c1": dict(n_blocks=1 << 20), "c3": dict(n_blocks=262144, items_per_block=56, key_len=40, val_len=256,
+                                                      kind="prefix"),
+              "r1": dict(n_blocks=1 << 20, kind="random")}
+    for name in which.split(","):
+        items, starts, n = bench.make_workload(torch, lsmgpu, **shapes[name])
+        nb = shapes[name]["n_blocks"]
+        enc_ctx = lsmgpu.Encoder()
+        enc = enc_ctx.encode(items, starts, nb)
+        torch.cuda.synchronize()
+        total = int(enc["block_off"][nb].item())
+        bad = int((enc["status"][:nb] != 0).sum())
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(reps):
+            enc_ctx.encode(items, starts, nb, out=enc)
+        e1.record()
+        torch.cuda.synchronize()
+        ms = e0.elapsed_time(e1) / reps
+        ck = lsmgpu.xxh3_128_file(enc["buf"], total)
+        res[name] = {"ms": round(ms, 4), "bytes": total, "bad": bad, "ck": f"{ck[1]:016x}{ck[0]:016x}"}
+        del items, enc
+        torch.cuda.empty_cache()
+    print(json.dumps(res), flush=True)
+
+
+def main():
+    if sys.argv[1] == "--child":
+        child(int(sys.argv[2]), sys.argv[3])
+        return
+    libs, rounds, which, reps = [], 3, "c1,c3", 10
+    a = sys.argv[1:]
+    while a:
+        x = a.pop(0)
+        if x == "--rounds":
+            rounds = int(a.pop(0))
+        elif x == "--which":
+            which = a.pop(0)
+        elif x == "--reps":
+            reps = int(a.pop(0))
+        else:
+            libs.append(x)
+    out = {l: [] for l in libs}
+    for r in range(rounds):
+        for l in libs:
+            env = dict(os.environ, LSMGPU_LIB=str(Path(l).resolve()))
+            p = subprocess.run([sys.executable, __file__, "--child", str(reps), which], env=env, capture_output=True,
+                               text=True, timeout=300)
+            if p.returncode != 0:
+                print(l, "FAILED", p.stderr[-2000:], flush=True)
+                sys.exit(p.returncode)
+            d = json.loads(p.stdout.strip().splitlines()[-1])
+            out[l].append(d)
+            print(f"round {r} {Path(l).name:28s} " + "  ".join(f"{k} {v['ms']:.4f} ms bad {v['bad']} ck {v['ck'][:12]}"
+                                                          for k, v in d.items()), flush=True)
+    print("median:")
+    for l in libs:
+        ks = out[l][0].keys()
+        print(f"  {Path(l).name:28s} " + "  ".join(
+            f"{k} {sorted(x[k]['ms'] for x in out[l])[len(out[l]) // 2]:.4f} ms" for k in ks))
+
+
+if __name__ == "__main__":
+    main()
