@@ -442,6 +442,39 @@ def bench_config5(torch, lsmgpu, steps, rank, world, dist, dev, threads, total_b
             "oracle_checked_blocks_per_rank": {"encode": checked, "decode": nb}}
 
 
+def bench_large_blocks(torch, lsmgpu, threads, steps=5):
+    """Data blocks above the general path's 72 KiB stage (the writer's data_block_size
+    goes up to 4 MiB, writer/mod.rs:193-198): 240 x 1 MiB and 60 x 4 MiB blocks of
+    16 B counter keys / 64 B values, encoded on the device (E3), decoded through
+    the stage in 64 KiB chunks (decode_chunked); every block checked against the
+    oracle (encoded bytes and decoded fields)."""
+    res = {}
+    for name, nb, ipb in (("1MiB", 240, 13107), ("4MiB", 60, 52429)):
+        items, starts, n = make_workload(torch, lsmgpu, nb, items_per_block=ipb, seed=0x5EED0007)
+        enc_ctx = lsmgpu.Encoder()
+        enc = enc_ctx.encode(items, starts, nb)
+        torch.cuda.synchronize()
+        total = int(enc["block_off"][nb].item())
+        e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+        e0.record()
+        for _ in range(3):
+            enc_ctx.encode(items, starts, nb, out=enc)
+        e1.record()
+        torch.cuda.synchronize()
+        enc_ms = e0.elapsed_time(e1) / 3
+        dec_ms, out = time_decode(torch, lsmgpu, enc["buf"], enc["block_off"], nb, n, steps)
+        ref_buf, ref_off = check_encode_all(torch, items, starts, enc, nb, n, threads)
+        check_decode_all(out, ref_buf, ref_off, nb, threads)
+        res[name] = {"blocks": nb, "bytes": total, "encode_ms": round(enc_ms, 3),
+                     "encode_GiB_per_s": round(total / (enc_ms * 1e-3) / 2 ** 30, 2), "decode_ms": round(dec_ms, 3),
+                     "decode_GiB_per_s": round(total / (dec_ms * 1e-3) / 2 ** 30, 2), "oracle_checked_blocks": nb}
+        del items, enc, out, ref_buf
+        torch.cuda.empty_cache()
+    res["note"] = ("encode: one wave per block straight in HBM (encode_large_kernel); decode: 4-wave workgroup per "
+                   "block through a 72 KiB stage in 64 KiB chunks (XXH3 chain carried across chunks)")
+    return res
+
+
 def bench_point_read(torch, lsmgpu, items, enc, nb, n_items, n_queries=1 << 20, reps=5):
     """Batched DataBlock::point_read: random existing keys of the config 2 batch,
     snapshot = max; every query must hit its own item."""
@@ -1099,6 +1132,8 @@ def main():
         if world == 1:
             extra["config4"] = bench_config4(torch, lsmgpu, max(3, args.steps // 4), rank, threads)
         extra["config5"] = bench_config5(torch, lsmgpu, max(3, args.steps // 4), rank, world, dist, red_dev, threads)
+        if world == 1:
+            extra["large_blocks"] = bench_large_blocks(torch, lsmgpu, threads)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu and ref_buf is not None:

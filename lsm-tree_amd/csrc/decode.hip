@@ -465,14 +465,13 @@ __device__ __forceinline__ void phase_b(const DecodeParams& P, const uint8_t* im
   }
 }
 
-// Interval walk straight from a span (direct path); emit(j, fields).
+// Records of restart interval r, [start, stop) payload-relative (the binary
+// index's entries r, r + 1), parsed from `base`; emit(j, fields).
 template <class Emit>
-__device__ __forceinline__ bool walk_interval(const uint8_t* base, uint32_t p0, const BlockMeta& m, uint32_t r,
-                                              Emit emit) {
-  const TrailerInfo t = trailer_of(m);
+__device__ __forceinline__ bool walk_interval_at(const uint8_t* base, uint32_t p0, const BlockMeta& m,
+                                                 const TrailerInfo& t, uint32_t r, uint32_t start, uint32_t stop,
+                                                 Emit emit) {
   const bool last = r + 1 == t.bin_len;
-  const uint32_t start = bin_get(base, p0, t, r);
-  const uint32_t stop = last ? t.rec_end : bin_get(base, p0, t, r + 1);
   const uint32_t count = last ? t.item_count - r * t.ri : t.ri;
   if (start > t.rec_end || stop > t.rec_end || (r == 0 && start != 0)) return false;
   uint32_t base_key = 0, pos = start;
@@ -485,6 +484,17 @@ __device__ __forceinline__ bool walk_interval(const uint8_t* base, uint32_t p0, 
     pos = next;
   }
   return pos == stop;
+}
+
+// Interval walk straight from a span (direct path); emit(j, fields).
+template <class Emit>
+__device__ __forceinline__ bool walk_interval(const uint8_t* base, uint32_t p0, const BlockMeta& m, uint32_t r,
+                                              Emit emit) {
+  const TrailerInfo t = trailer_of(m);
+  const bool last = r + 1 == t.bin_len;
+  const uint32_t start = bin_get(base, p0, t, r);
+  const uint32_t stop = last ? t.rec_end : bin_get(base, p0, t, r + 1);
+  return walk_interval_at(base, p0, m, t, r, start, stop, emit);
 }
 
 // One block straight from HBM (blocks larger than the LDS stage).
@@ -600,22 +610,25 @@ constexpr uint32_t kBigStage = 72 * 1024;
 constexpr uint32_t kBigContrib = 256;                        // LDS: contributions, 64 B per KiB
 constexpr uint32_t kBigStageOff = kBigContrib + (kBigStage / 1024 + 1) * 64;
 
-// An index block larger than the stage (a full block index: ~25 B per data
-// block, hundreds of KiB for a 64 MiB table), on all four waves of the
-// general-path workgroup, through the stage in 64 KiB chunks.  Index blocks
-// have restart interval 1, so every record starts at its binary-index entry
-// and the records are independent: per chunk, each thread parses the records
-// (its intervals r = tid, tid + 256, ...) that start in the chunk, from LDS;
-// all waves compute the per-KiB XXH3 contributions of the chunk's KiB blocks
-// and wave 0 carries the serial chain across chunks.  Same results as the
-// interval walk of decode_block_direct (walk_interval), which still takes an
-// interval whose record count is not 1 (malformed trailers).
-constexpr uint32_t kIndexChunk = 64 * 1024;
-static_assert(kIndexChunk + 1024 + 256 <= kBigStage, "chunk + one KiB unit + a record header");
+// A data or index block larger than the stage (a full block index: ~25 B
+// per data block, hundreds of KiB for a 64 MiB table; a data block of the
+// writer's up-to-4-MiB targets, writer/mod.rs:193-198), on all four waves of
+// the general-path workgroup, through the stage in 64 KiB chunks (staged with
+// 7.5 KiB of overlap past the chunk).  Per chunk: all waves compute the
+// per-KiB XXH3 contributions of the chunk's KiB blocks, wave 0 carries the
+// serial chain across chunks; each thread parses the restart intervals
+// (r = tid, tid + 256, ...) that start in the chunk from LDS when the whole
+// interval (+ the parsers' read-ahead) is staged, else walks it from HBM.  The
+// interval starts come from the binary index in HBM (the block's tail is not
+// in the chunk).  Same results as the interval walk of decode_block_direct.
+constexpr uint32_t kChunkBytes = 64 * 1024;
+constexpr uint32_t kChunkOverlap = 7 * 1024 + 512;
+constexpr uint32_t kChunkReadAhead = 192;  // parsers read at most this far past a record start window
+static_assert(kChunkBytes + kChunkOverlap + 256 <= kBigStage, "chunk + overlap + pad");
 
-__device__ __forceinline__ void decode_index_chunked(const DecodeParams& P, uint32_t b, const uint8_t* gbase,
-                                                     uint32_t span, BlockMeta* meta, uint32_t* cks_bad,
-                                                     uint64_t* contrib, uint8_t* stage) {
+__device__ __forceinline__ void decode_chunked(const DecodeParams& P, uint32_t b, const uint8_t* gbase,
+                                               uint32_t span, BlockMeta* meta, uint32_t* cks_bad,
+                                               uint64_t* contrib, uint8_t* stage) {
   const uint32_t tid = threadIdx.x;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(tid / kWave);
   const int lane = tid & (kWave - 1);
@@ -631,14 +644,15 @@ __device__ __forceinline__ void decode_index_chunked(const DecodeParams& P, uint
   xxh3_acc_init(lane & 3, a0, a1);
   const uint64_t scr0 = kLongSecret.acc[16 + 2 * (lane & 3)], scr1 = kLongSecret.acc[16 + 2 * (lane & 3) + 1];
   const uint32_t nint = t.bin_len;
+  auto emit = [&](uint32_t j, const ItemFields& f) { emit_global(P.out, item_base + j, f, P.seqno_add); };
   uint32_t r = tid;
   uint32_t s_cur = r < nint ? bin_get(gbase, p0, t, r) : 0xFFFFFFFFu;
   bool ok = true;
-  for (uint32_t cs = 0; cs < span; cs += kIndexChunk) {
-    const uint32_t ce = min(cs + kIndexChunk, span);
-    const uint32_t ss = min(ce + 1024 + 256, span);  // staged: [cs, ss)
+  for (uint32_t cs = 0; cs < span; cs += kChunkBytes) {
+    const uint32_t ce = min(cs + kChunkBytes, span);
+    const uint32_t ss = min(ce + kChunkOverlap, span);  // staged: [cs, ss)
     {
-      const uint32_t chunks = (ss - cs) >> 4;
+      const uint32_t chunks = (ss - cs + 15) >> 4;
       const uint8_t* src = gbase + cs + 16 * lane;
       for (uint32_t c = wave; c * kWave < chunks; c += kBigWaves)
         if (c * kWave + lane < chunks)
@@ -652,25 +666,12 @@ __device__ __forceinline__ void decode_index_chunked(const DecodeParams& P, uint
     const uint32_t n1 = min(nbk, ce > p0 ? (ce - p0 + 1023) / 1024 : 0u);
     if (hash && n1 > n0)
       xxh3_kib_contribs(sbase, p0 + 1024 * n0, (n1 - n0) * 1024 + 1, &kLongSecret, contrib, wave, kBigWaves);
-    // the records that start in this chunk
+    // the intervals that start in this chunk
     while (r < nint && p0 + s_cur < ce) {
       const bool last = r + 1 == nint;
       const uint32_t stop = last ? t.rec_end : bin_get(gbase, p0, t, r + 1);
-      const uint32_t count = last ? t.item_count - r : 1;
-      if (s_cur > t.rec_end || stop > t.rec_end || (r == 0 && s_cur != 0)) {
-        ok = false;
-      } else if (count != 1) {
-        ok &= walk_interval(gbase, p0, m, r, [&](uint32_t j, const ItemFields& f) {
-          emit_global(P.out, item_base + j, f, P.seqno_add);
-        });
-      } else {
-        ItemFields f;
-        uint32_t next;
-        if (parse_record(sbase, p0, s_cur, t, 1, true, 0, f, next) && next == stop)
-          emit_global(P.out, item_base + r, f, P.seqno_add);
-        else
-          ok = false;
-      }
+      const bool staged = p0 + s_cur >= cs && stop <= t.rec_end && (p0 + stop + kChunkReadAhead <= ss || ss == span);
+      ok &= walk_interval_at(staged ? sbase : gbase, p0, m, t, r, s_cur, stop, emit);
       r += kThreads;
       s_cur = r < nint ? bin_get(gbase, p0, t, r) : 0xFFFFFFFFu;
     }
@@ -722,9 +723,9 @@ __global__ __launch_bounds__(kBigWaves * kWave) void decode_deferred_staged_kern
         *cks_bad = 0;
       }
       lds_barrier();
-      if (meta[1].st == ST_OK && meta[1].type == 1) {  // index blocks (a full index of a large table)
-        decode_index_chunked(P, b, gbase, (uint32_t)(span1 - span0), meta, cks_bad, contrib, stage);
-      } else if (wave == 0) {  // anything else: one wave straight from HBM
+      if (meta[0].st == ST_OK && meta[1].st == ST_OK) {  // data / index / meta blocks: chunked through the stage
+        decode_chunked(P, b, gbase, (uint32_t)(span1 - span0), meta, cks_bad, contrib, stage);
+      } else if (wave == 0) {  // a failing header or trailer: one wave (statuses in oracle order)
         decode_block_direct(P, b, meta);
       }
       lds_barrier();
