@@ -449,7 +449,8 @@ def bench_large_blocks(torch, lsmgpu, threads, steps=5):
     the stage in 64 KiB chunks (decode_chunked); every block checked against the
     oracle (encoded bytes and decoded fields)."""
     res = {}
-    for name, nb, ipb in (("1MiB", 240, 13107), ("4MiB", 60, 52429)):
+    for name, nb, ipb, bs in (("1MiB", 240, 13108, 1 << 20), ("4MiB", 60, 52429, 4 << 20)):
+        check_cut_rule(lsmgpu, ipb, 16, 64, bs)  # = the writer's cut at that data_block_size
         items, starts, n = make_workload(torch, lsmgpu, nb, items_per_block=ipb, seed=0x5EED0007)
         enc_ctx = lsmgpu.Encoder()
         enc = enc_ctx.encode(items, starts, nb)
