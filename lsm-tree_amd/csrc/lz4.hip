@@ -39,7 +39,9 @@ __device__ __forceinline__ uint64_t lds_read8(const uint32_t* w, uint32_t p) {
   const uint32_t lo = s ? alignbyte(d1, d0, s) : d0, hi = s ? alignbyte(d2, d1, s) : d1;
   // wave-uniform by construction (every lane reads the same bytes): move it to
   // SGPRs so the walk's bounds checks and loops are scalar branches
-  return (uint64_t)__builtin_amdgcn_readfirstlane(lo) | ((uint64_t)__builtin_amdgcn_readfirstlane(hi) << 32);
+  // (readfirstlane returns int: widen through uint32_t, or bit 31 of lo would sign-fill the high word)
+  return (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(lo) |
+         ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane(hi) << 32);
 }
 
 __device__ __forceinline__ uint32_t lds_read1(const uint8_t* in, uint32_t p) {

@@ -80,7 +80,9 @@ __global__ __launch_bounds__(kMatWaves * 64) void materialize_kernel(MatParams P
     const uint8_t* pre = payload + (live ? P.key_off[head] : 0);
     const uint8_t* suf = payload + (live ? P.key_off[i] : 0);
     // the step's output span [o0, o1) (contiguous: the keys of items c .. c + 63 in order)
-    const uint64_t o0 = __builtin_amdgcn_readfirstlane((uint32_t)o) | ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(o >> 32)) << 32);
+    // (readfirstlane returns int: widened through uint32_t, so an offset with bit 31 set is not sign-filled)
+    const uint64_t o0 = (uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)o) |
+                        ((uint64_t)(uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)(o >> 32)) << 32);
     const uint64_t last = min(e, c + 64) - 1 - c;
     const uint64_t oe = o + pl + kl;  // this key's end
     const uint32_t oe_lo = (uint32_t)__builtin_amdgcn_readlane((int)(uint32_t)oe, (int)last);

@@ -78,3 +78,30 @@ def test_scan_then_materialize(gpu, oracle):
     want = [items.keys[int(items.key_off[i]):int(items.key_off[i + 1])].tobytes() for i in range(items.n)]
     assert len(ko) == items.n + 1
     assert [kb[ko[i]:ko[i + 1]] for i in range(items.n)] == want
+
+
+def test_materialize_output_past_2gib(gpu):
+    """A key arena larger than 2 GiB (1000-byte keys: 992-byte shared prefix +
+    8-byte counter, restart interval 16): output offsets with bit 31 set must
+    not be sign-extended when a wave broadcasts them (the v_readfirstlane int
+    result is widened through uint32_t).  Every materialized key equals the
+    encoder's input key."""
+    import sys
+    from pathlib import Path
+    import torch
+    sys.path.insert(0, str(Path(__file__).resolve().parent.parent))
+    import bench
+    n_blocks = 520000  # 5 items of 1000 + 4 bytes per 4 KiB block: 2.6 M keys, 2.6 GB materialized
+    items, starts, n = bench.make_workload(torch, gpu, n_blocks, items_per_block=5, key_len=1000, val_len=4,
+                                           seed=77, kind="prefix")
+    bench.check_cut_rule(gpu, 5, 1000, 4)
+    enc = gpu.Encoder().encode(items, starts, n_blocks)
+    torch.cuda.synchronize()
+    assert int((enc["status"][:n_blocks] != 0).sum()) == 0
+    out = gpu.decode_blocks(enc["buf"], enc["block_off"], n_blocks, item_cap=n)
+    keys, key_off = gpu.materialize_keys(enc["buf"], enc["block_off"], n_blocks, out, n)
+    torch.cuda.synchronize()
+    assert int((out["status"][:n_blocks] != 0).sum()) == 0
+    assert int(key_off[n].item()) == n * 1000 and n * 1000 > (1 << 31) + (1 << 28)
+    assert torch.equal(key_off[:n + 1], torch.arange(n + 1, device=key_off.device, dtype=key_off.dtype) * 1000)
+    assert torch.equal(keys[:n * 1000], items["keys"][:n * 1000])
