@@ -1099,8 +1099,21 @@ def main():
     dec_ms = timed(lambda: dec_ctx.decode(enc["buf"], enc["block_off"], nb, out, n_items), reps)
     kdec_ms = timed(lambda: dec_ctx.decode(enc["buf"], enc["block_off"], nb, out, n_items,
                                            tuning=(0, 0, 0, lsmgpu.DECODE_ITEM_START_VALID)), reps)
+    # the compact 19 B/item layout (lsm_decode_blocks16), same blocks, checked against the 32-bit output
+    out16 = dec_ctx.alloc_outputs(n_items, nb, compact=True)
+    dec_ctx.decode(enc["buf"], enc["block_off"], nb, out16, n_items, compact=True)
+    torch.cuda.synchronize()
+    assert int((out16["status"][:nb] != 0).sum()) == 0, "compact decode: a block failed"
+    for f in ("key_off", "val_off", "val_len"):
+        assert torch.equal(out[f][:n_items].to(torch.int64), out16[f][:n_items].to(torch.int64) & 0xFFFF), f
+    for f in ("seqno", "key_len", "prefix_len", "vtype"):
+        assert torch.equal(out[f][:n_items], out16[f][:n_items]), f
+    kdec16_ms = timed(lambda: dec_ctx.decode(enc["buf"], enc["block_off"], nb, out16, n_items, compact=True,
+                                             tuning=(0, 0, 0, lsmgpu.DECODE_ITEM_START_VALID)), reps)
+    del out16
     ceil = ceilings(torch) if rank == 0 else None
     dec_alg = total_bytes + n_items * PARSED_BYTES_PER_ITEM + nb * PER_BLOCK_OUT
+    dec16_alg = total_bytes + n_items * 19 + nb * PER_BLOCK_OUT
     key_val = int(items["key_off"][n_items].item()) + int(items["val_off"][n_items].item())
     enc_alg = key_val + n_items * ENC_IN_PER_ITEM + 4 * (nb + 1) + total_bytes + 8 * (nb + 1) + 4 * nb
     r_dec = roofline_entry("decode_blocks_kernel (item_start precomputed)", dec_alg, kdec_ms, ceil,
@@ -1170,6 +1183,11 @@ def main():
             "decode": {"ms": round(dec_ms, 4), "GiB_per_s": round(total_bytes / (dec_ms * 1e-3) / 2 ** 30, 3),
                        "kernel_ms": round(kdec_ms, 4),
                        "note": "whole lsm_decode_blocks call (trailer counts + scan + decode kernel)"},
+            "decode_compact": {"kernel_ms": round(kdec16_ms, 4), "alg_bytes": dec16_alg,
+                               "GBps_alg": round(dec16_alg / (kdec16_ms * 1e-3) / 1e9, 1),
+                               "read_only_frac": round(total_bytes / (kdec16_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4),
+                               "note": "lsm_decode_blocks16 (19 B/item: u16 payload offsets / lengths), item_start "
+                                       "precomputed; every field equal to the 32-bit decode's"},
             "round_trip_traffic_GiB_per_s": round(2 * value, 3),
             **extra,
             "host_inclusive": hostinc or None,

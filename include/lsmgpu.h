@@ -50,7 +50,7 @@
 extern "C" {
 #endif
 
-#define LSM_ABI_VERSION 3
+#define LSM_ABI_VERSION 4
 #define LSM_HEADER_LEN 33  /* Header::serialized_len(), header.rs:64-76 */
 #define LSM_TRAILER_LEN 31 /* TRAILER_SIZE, trailer.rs:14-23 */
 /* d_blocks must be 16-byte aligned and readable for LSM_INPUT_PADDING bytes
@@ -117,6 +117,21 @@ typedef struct lsm_parsed_items {
     uint64_t* handle_off;
 } lsm_parsed_items;
 
+/* Compact decode output (lsm_decode_blocks16): the same fields with 16-bit
+ * payload offsets and lengths, 19 bytes per item instead of 25.  Only data and
+ * meta blocks whose payload is at most 65535 bytes (every 4 / 16 KiB-target
+ * block) are decoded into it; index blocks and larger payloads get
+ * LSM_UNSUPPORTED (after the header and checksum checks, before the trailer). */
+typedef struct lsm_parsed_items16 {
+    uint64_t* seqno;
+    uint16_t* key_off;
+    uint16_t* val_off;
+    uint16_t* val_len;
+    uint16_t* key_len;
+    uint16_t* prefix_len;
+    uint8_t* vtype;
+} lsm_parsed_items16;
+
 typedef struct lsm_block_params {
     uint8_t restart_interval; /* data_block_restart_interval (config default 16); forced 1 for index */
     uint8_t block_type;       /* LSM_BLOCK_DATA / LSM_BLOCK_INDEX / LSM_BLOCK_META */
@@ -180,6 +195,14 @@ int lsm_decode_blocks_tuned(const uint8_t* d_blocks, const uint64_t* d_block_off
                             int32_t expect_type, const lsm_parsed_items* d_out, uint64_t item_cap,
                             uint32_t* d_item_start, int32_t* d_status, void* d_workspace,
                             size_t workspace_bytes, const lsm_decode_tuning* tuning, void* stream);
+/* lsm_decode_blocks_tuned into the compact 19 B/item layout (lsm_parsed_items16;
+ * tuning may be NULL).  Same statuses, plus LSM_UNSUPPORTED for index blocks
+ * and payloads over 65535 bytes.  Replaces the same decoder.rs:442-483 /
+ * data_block/mod.rs:272-316 walk as lsm_decode_blocks. */
+int lsm_decode_blocks16(const uint8_t* d_blocks, const uint64_t* d_block_off, uint32_t n_blocks,
+                        int32_t expect_type, const lsm_parsed_items16* d_out, uint64_t item_cap,
+                        uint32_t* d_item_start, int32_t* d_status, void* d_workspace, size_t workspace_bytes,
+                        const lsm_decode_tuning* tuning, void* stream);
 
 /* ---- encode ---------------------------------------------------------------
  * Encodes n_blocks blocks; block b holds items [d_block_item_start[b],

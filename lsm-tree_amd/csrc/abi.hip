@@ -63,17 +63,18 @@ int lsm_set_device(int device) {
 
 size_t lsm_decode_workspace_size(uint32_t n_blocks) { return lsmgpu::decode_workspace_size(n_blocks); }
 
-int lsm_decode_blocks_tuned(const uint8_t* d_blocks, const uint64_t* d_block_off, uint32_t n_blocks,
-                            int32_t expect_type, const lsm_parsed_items* d_out, uint64_t item_cap,
-                            uint32_t* d_item_start, int32_t* d_status, void* d_workspace,
-                            size_t workspace_bytes, const lsm_decode_tuning* tuning, void* stream) {
+static int decode_blocks_common(const uint8_t* d_blocks, const uint64_t* d_block_off, uint32_t n_blocks,
+                                int32_t expect_type, const lsm_parsed_items* d_out, bool compact, uint64_t item_cap,
+                                uint32_t* d_item_start, int32_t* d_status, void* d_workspace,
+                                size_t workspace_bytes, const lsm_decode_tuning* tuning, void* stream) {
   if (n_blocks == 0) return LSM_OK;
   if (!d_blocks || !d_block_off || !d_out || !d_item_start || !d_status) return LSM_BAD_ARG;
   if (((uintptr_t)d_blocks & 15) != 0) return LSM_BAD_ARG;
   if (expect_type < -1 || expect_type > 3) return LSM_BAD_ARG;
   if (item_cap > 0xFFFFFFFFULL) item_cap = 0xFFFFFFFFULL;
   if (!d_workspace || workspace_bytes < lsmgpu::decode_workspace_size(n_blocks)) return LSM_BAD_ARG;
-  lsmgpu::DecodeParams P;
+  lsmgpu::DecodeParams P{};
+  P.compact = compact ? 1u : 0u;
   P.blocks = d_blocks;
   P.block_off = d_block_off;
   P.n_blocks = n_blocks;
@@ -98,6 +99,33 @@ int lsm_decode_blocks_tuned(const uint8_t* d_blocks, const uint64_t* d_block_off
   if (lsmgpu::decode_lds_bytes(P.stage_bytes, P.tile_items, P.blocks_per_wave) > 160 * 1024) return LSM_BAD_ARG;
   hipError_t e = lsmgpu::launch_decode(P, d_workspace, (hipStream_t)stream);
   return e == hipSuccess ? LSM_OK : set_hip_error(e, "lsm_decode_blocks");
+}
+
+int lsm_decode_blocks_tuned(const uint8_t* d_blocks, const uint64_t* d_block_off, uint32_t n_blocks,
+                            int32_t expect_type, const lsm_parsed_items* d_out, uint64_t item_cap,
+                            uint32_t* d_item_start, int32_t* d_status, void* d_workspace,
+                            size_t workspace_bytes, const lsm_decode_tuning* tuning, void* stream) {
+  return decode_blocks_common(d_blocks, d_block_off, n_blocks, expect_type, d_out, false, item_cap, d_item_start,
+                              d_status, d_workspace, workspace_bytes, tuning, stream);
+}
+
+int lsm_decode_blocks16(const uint8_t* d_blocks, const uint64_t* d_block_off, uint32_t n_blocks,
+                        int32_t expect_type, const lsm_parsed_items16* d_out, uint64_t item_cap,
+                        uint32_t* d_item_start, int32_t* d_status, void* d_workspace, size_t workspace_bytes,
+                        const lsm_decode_tuning* tuning, void* stream) {
+  if (!d_out) return n_blocks ? LSM_BAD_ARG : LSM_OK;
+  // the same kernels, with the three payload-position arrays stored as u16
+  lsm_parsed_items o{};
+  o.seqno = d_out->seqno;
+  o.key_off = reinterpret_cast<uint32_t*>(d_out->key_off);
+  o.val_off = reinterpret_cast<uint32_t*>(d_out->val_off);
+  o.val_len = reinterpret_cast<uint32_t*>(d_out->val_len);
+  o.key_len = d_out->key_len;
+  o.prefix_len = d_out->prefix_len;
+  o.vtype = d_out->vtype;
+  o.handle_off = nullptr;
+  return decode_blocks_common(d_blocks, d_block_off, n_blocks, expect_type, &o, true, item_cap, d_item_start,
+                              d_status, d_workspace, workspace_bytes, tuning, stream);
 }
 
 int lsm_decode_blocks(const uint8_t* d_blocks, const uint64_t* d_block_off, uint32_t n_blocks,

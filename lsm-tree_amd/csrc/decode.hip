@@ -124,12 +124,21 @@ __device__ __forceinline__ void lds_barrier() {
   __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup", "local");
 }
 
+// compact (lsm_decode_blocks16): key_off / val_off / val_len are uint16_t
+// arrays; every block that reaches a store has a payload <= 65535 bytes
+// (meta_trailer), so the payload-relative values fit.
 __device__ __forceinline__ void emit_global(const lsm_parsed_items& o, uint64_t i, const ItemFields& f,
-                                            uint64_t seqno_add) {
+                                            uint64_t seqno_add, bool compact) {
   if (o.seqno) gstore(o.seqno, i, f.seqno + seqno_add);
-  if (o.key_off) gstore(o.key_off, i, f.key_off);
-  if (o.val_off) gstore(o.val_off, i, f.val_off);
-  if (o.val_len) gstore(o.val_len, i, f.val_len);
+  if (compact) {
+    if (o.key_off) gstore(reinterpret_cast<uint16_t*>(o.key_off), i, (uint16_t)f.key_off);
+    if (o.val_off) gstore(reinterpret_cast<uint16_t*>(o.val_off), i, (uint16_t)f.val_off);
+    if (o.val_len) gstore(reinterpret_cast<uint16_t*>(o.val_len), i, (uint16_t)f.val_len);
+  } else {
+    if (o.key_off) gstore(o.key_off, i, f.key_off);
+    if (o.val_off) gstore(o.val_off, i, f.val_off);
+    if (o.val_len) gstore(o.val_len, i, f.val_len);
+  }
   if (o.key_len) gstore(o.key_len, i, f.key_len);
   if (o.prefix_len) gstore(o.prefix_len, i, f.prefix_len);
   if (o.vtype) gstore(o.vtype, i, f.vtype);
@@ -167,12 +176,17 @@ __device__ __forceinline__ void meta_header_fields(const uint8_t* base, uint32_t
 }
 
 // After the payload checksum: data_length, expected type, trailer structure.
-__device__ __forceinline__ void meta_trailer(const uint8_t* base, int32_t expect_type, uint32_t cap, BlockMeta& m) {
+// compact output (lsm_decode_blocks16): index blocks (u64 handle offsets) and
+// payloads over 65535 bytes cannot be stored in 16 bits: LSM_UNSUPPORTED,
+// decided here, after every header check and before the trailer is read.
+__device__ __forceinline__ void meta_trailer(const uint8_t* base, int32_t expect_type, uint32_t cap, BlockMeta& m,
+                                             bool compact) {
   if (m.st != ST_OK) return;
   const uint32_t plen = m.len - kHdrLen;
   if (m.item_count != plen) { m.st = ST_TRUNCATED; return; }   // data_length vs handle
   if (expect_type >= 0 && (int32_t)m.type != expect_type) { m.st = ST_TYPE_MISMATCH; return; }
   if (m.type == 2) { m.st = ST_UNSUPPORTED; return; }          // filter blocks are not KV blocks
+  if (compact && (m.type == 1 || plen > 0xFFFFu)) { m.st = ST_UNSUPPORTED; return; }
   TrailerInfo t;
   int32_t st = read_trailer(base, m.hb + kHdrLen, plen, t);
   if (st == ST_OK && m.type == 1 && t.ri != 1) st = ST_PARSE;   // index blocks: restart interval 1
@@ -414,26 +428,33 @@ __host__ __device__ __forceinline__ bool all_fields(const lsm_parsed_items& o) {
   return o.seqno && o.key_off && o.val_off && o.val_len && o.key_len && o.prefix_len && o.vtype;
 }
 
+template <bool kCompact>
 __device__ __forceinline__ void store_fields(const DecodeParams& P, bool all_fields, uint64_t gi,
                                              const ItemFields& f) {
   if (all_fields) {  // every output array present: no per-field null checks
     gstore(P.out.seqno, gi, f.seqno + P.seqno_add);
-    gstore(P.out.key_off, gi, f.key_off);
-    gstore(P.out.val_off, gi, f.val_off);
-    gstore(P.out.val_len, gi, f.val_len);
+    if (kCompact) {  // 19 B/item: 16-bit payload offsets and lengths
+      gstore(reinterpret_cast<uint16_t*>(P.out.key_off), gi, (uint16_t)f.key_off);
+      gstore(reinterpret_cast<uint16_t*>(P.out.val_off), gi, (uint16_t)f.val_off);
+      gstore(reinterpret_cast<uint16_t*>(P.out.val_len), gi, (uint16_t)f.val_len);
+    } else {
+      gstore(P.out.key_off, gi, f.key_off);
+      gstore(P.out.val_off, gi, f.val_off);
+      gstore(P.out.val_len, gi, f.val_len);
+    }
     gstore(P.out.key_len, gi, f.key_len);
     gstore(P.out.prefix_len, gi, f.prefix_len);
     gstore(P.out.vtype, gi, f.vtype);
     if (P.out.handle_off) gstore(P.out.handle_off, gi, f.handle_off);
   } else {
-    emit_global(P.out, gi, f, P.seqno_add);
+    emit_global(P.out, gi, f, P.seqno_add, kCompact);
   }
 }
 
 // Phase B: thread = record.  Full parse + validation of every descriptor
 // (the oracle's parse_data_item checks, and the record must end exactly at
 // the descriptor's end), then coalesced stores of all fields.
-template <bool kAllFields, bool kWide = false>
+template <bool kAllFields, bool kCompact, bool kWide = false>
 __device__ __forceinline__ void phase_b(const DecodeParams& P, const uint8_t* img, BlockMeta* meta,
                                         const uint64_t* rec, uint32_t n_items, uint32_t g_item0, uint32_t tid,
                                         uint32_t nthr) {
@@ -459,7 +480,7 @@ __device__ __forceinline__ void phase_b(const DecodeParams& P, const uint8_t* im
     const uint32_t n1 = (uint32_t)(d >> RL::kN1Shift) & 7, n2 = (uint32_t)(d >> RL::kN2Shift) & 3;
     const int rc = n1 ? parse_data_shape(img, p0, a, end, restart, base_key, n1, n2, f, next)
                       : parse_data_fast(img, p0, a, end, restart, base_key, f, next);
-    if (rc > 0 && store) store_fields(P, all_fields, gi, f);
+    if (rc > 0 && store) store_fields<kCompact>(P, all_fields, gi, f);
     if (rc == 0) meta[j].st = ST_DEFER;  // wins over PARSE
     else if (rc < 0 || next != want) atomicCAS(&meta[j].st, ST_OK, ST_PARSE);
   }
@@ -514,14 +535,14 @@ __device__ __forceinline__ void decode_block_direct(const DecodeParams& P, uint3
     if (lane == 0 && (lo != meta[0].ck_lo || hi != meta[0].ck_hi)) meta[0].st = ST_CKSUM;
   }
   wave_sync();
-  if (lane == 0) meta_trailer(base, P.expect_type, cap, meta[0]);
+  if (lane == 0) meta_trailer(base, P.expect_type, cap, meta[0], P.compact);
   wave_sync();
   const BlockMeta m = meta[0];
   if (m.st == ST_OK) {
     bool ok = true;
     for (uint32_t r = lane; r < m.bin_len; r += kWave) {
       ok &= walk_interval(base, hb + kHdrLen, m, r,
-                          [&](uint32_t j, const ItemFields& f) { emit_global(P.out, item_base + j, f, P.seqno_add); });
+                          [&](uint32_t j, const ItemFields& f) { emit_global(P.out, item_base + j, f, P.seqno_add, P.compact); });
     }
     if (!ok) atomicCAS(&meta[0].st, ST_OK, ST_PARSE);
   }
@@ -644,7 +665,7 @@ __device__ __forceinline__ void decode_chunked(const DecodeParams& P, uint32_t b
   xxh3_acc_init(lane & 3, a0, a1);
   const uint64_t scr0 = kLongSecret.acc[16 + 2 * (lane & 3)], scr1 = kLongSecret.acc[16 + 2 * (lane & 3) + 1];
   const uint32_t nint = t.bin_len;
-  auto emit = [&](uint32_t j, const ItemFields& f) { emit_global(P.out, item_base + j, f, P.seqno_add); };
+  auto emit = [&](uint32_t j, const ItemFields& f) { emit_global(P.out, item_base + j, f, P.seqno_add, P.compact); };
   uint32_t r = tid;
   uint32_t s_cur = r < nint ? bin_get(gbase, p0, t, r) : 0xFFFFFFFFu;
   bool ok = true;
@@ -719,7 +740,7 @@ __global__ __launch_bounds__(kBigWaves * kWave) void decode_deferred_staged_kern
       if (tid == 0) {
         meta_header(gbase, (uint32_t)(off - span0), end >= off ? end - off : 0, meta[0]);
         meta[1] = meta[0];
-        meta_trailer(gbase, P.expect_type, cap, meta[1]);
+        meta_trailer(gbase, P.expect_type, cap, meta[1], P.compact);
         *cks_bad = 0;
       }
       lds_barrier();
@@ -745,7 +766,7 @@ __global__ __launch_bounds__(kBigWaves * kWave) void decode_deferred_staged_kern
     if (tid == 0) {
       meta_header(stage, hb, end >= off ? end - off : 0, meta[0]);
       meta[1] = meta[0];
-      meta_trailer(stage, P.expect_type, cap, meta[1]);
+      meta_trailer(stage, P.expect_type, cap, meta[1], P.compact);
       *cks_bad = 0;
     }
     lds_barrier();
@@ -767,7 +788,7 @@ __global__ __launch_bounds__(kBigWaves * kWave) void decode_deferred_staged_kern
         bool ok = true;
         for (uint32_t r = tid - kWave; r < m.bin_len; r += (kBigWaves - 1) * kWave) {
           ok &= walk_interval(stage, hb + kHdrLen, m, r,
-                              [&](uint32_t j, const ItemFields& f) { emit_global(P.out, item_base + j, f, P.seqno_add); });
+                              [&](uint32_t j, const ItemFields& f) { emit_global(P.out, item_base + j, f, P.seqno_add, P.compact); });
         }
         if (!ok) atomicCAS(&meta[1].st, ST_OK, ST_PARSE);
       }
@@ -863,7 +884,7 @@ __device__ unsigned long long g_dec_phase[32];
 #define DEC_ROLE(i)
 #endif
 
-template <bool kAllFields>
+template <bool kAllFields, bool kCompact>
 __global__ __launch_bounds__(kBigGWaves * kWave) void decode_big_kernel(DecodeParams P) {
 #ifdef LSM_DIAG
   uint64_t t_last = __builtin_amdgcn_s_memtime(), ph[8] = {};
@@ -948,7 +969,7 @@ __global__ __launch_bounds__(kBigGWaves * kWave) void decode_big_kernel(DecodePa
           m.hdr_st = m.st;
           m.ck_bad = 0;
           m.hck_bad = 0;
-          meta_trailer(stage, P.expect_type, n_items, m);
+          meta_trailer(stage, P.expect_type, n_items, m, P.compact);
           if (m.st == ST_OK && m.type == 1) m.st = ST_DEFER;  // index blocks: general path
           m.chain0 = 0;
           meta[0] = m;
@@ -970,7 +991,7 @@ __global__ __launch_bounds__(kBigGWaves * kWave) void decode_big_kernel(DecodePa
       }
       // phase B on waves 0 .. kBigGWaves - 2, under the chain
       if (!(kDiagBuild && (P.flags & kDiagSkipPhaseB)))
-        phase_b<kAllFields, true>(P, stage, meta, rec, n_items, X.it0, tid, (kBigGWaves - 1) * kWave);
+        phase_b<kAllFields, kCompact, true>(P, stage, meta, rec, n_items, X.it0, tid, (kBigGWaves - 1) * kWave);
     }
     lds_barrier();
     DEC_PHASE(4);
@@ -1028,7 +1049,7 @@ constexpr uint32_t kGroupWaves = LSM_DEC_WAVES;
 constexpr int kPrioA = LSM_PRIO_A;  // s_setprio of the phase-A wave
 constexpr int kPrioH = LSM_PRIO_H;  // s_setprio of a wave hashing one whole block
 
-template <bool kAllFields>
+template <bool kAllFields, bool kCompact>
 __global__ __launch_bounds__(kGroupWaves * kWave) __attribute__((amdgpu_waves_per_eu(LSM_DEC_WPE))) void decode_blocks_kernel(DecodeParams P) {
   // LDS: [meta: G x 80 B][rec: u64 per item + 1 scratch][owner: u8 per item][staged bytes + pad][secret]
 #ifdef LSM_DIAG
@@ -1113,7 +1134,7 @@ __global__ __launch_bounds__(kGroupWaves * kWave) __attribute__((amdgpu_waves_pe
         m.hdr_st = m.st;
         m.ck_bad = 0;
         m.hck_bad = 0;
-        meta_trailer(stage, P.expect_type, G.it1_j - G.it0_j, m);
+        meta_trailer(stage, P.expect_type, G.it1_j - G.it0_j, m, P.compact);
         if (m.st == ST_OK && m.type == 1) m.st = ST_DEFER;  // index blocks: general path
         chains = m.st == ST_OK ? m.bin_len : 0;
       }
@@ -1177,7 +1198,7 @@ __global__ __launch_bounds__(kGroupWaves * kWave) __attribute__((amdgpu_waves_pe
     DEC_PHASE(2);
     // ---- 4. phase B: thread = record; full parse + validation; coalesced stores
     if (!(kDiagBuild && (P.flags & (kDiagSkipParse | kDiagSkipPhaseB))))
-      phase_b<kAllFields>(P, stage, meta, rec, G.n_items, G.g_item0, threadIdx.x, blockDim.x);
+      phase_b<kAllFields, kCompact>(P, stage, meta, rec, G.n_items, G.g_item0, threadIdx.x, blockDim.x);
     lds_barrier();
     DEC_PHASE(3);
     if (wave == 0) {
@@ -1271,17 +1292,22 @@ hipError_t launch_decode(const DecodeParams& P0, void* ws, hipStream_t st) {
   }
   const uint32_t lds = decode_lds_bytes(P.stage_bytes, P.tile_items, P.blocks_per_wave);
   const bool all = all_fields(P.out);
+  // kernel variants: every field present or not, 32- or 16-bit offsets
+  const int variant = (all ? 1 : 0) | (P.compact ? 2 : 0);
+  const void* const group_k[4] = {(const void*)decode_blocks_kernel<false, false>,
+                                  (const void*)decode_blocks_kernel<true, false>,
+                                  (const void*)decode_blocks_kernel<false, true>,
+                                  (const void*)decode_blocks_kernel<true, true>};
+  const void* const big_k[4] = {(const void*)decode_big_kernel<false, false>, (const void*)decode_big_kernel<true, false>,
+                                (const void*)decode_big_kernel<false, true>, (const void*)decode_big_kernel<true, true>};
   if (lds > 64 * 1024) {
-    static uint64_t done_all = 0, done_some = 0;
-    e = all ? set_lds_attr((const void*)decode_blocks_kernel<true>, 160 * 1024, &done_all)
-            : set_lds_attr((const void*)decode_blocks_kernel<false>, 160 * 1024, &done_some);
-    if (e != hipSuccess) return e;
+    static uint64_t done[4] = {};
+    if ((e = set_lds_attr(group_k[variant], 160 * 1024, &done[variant])) != hipSuccess) return e;
   }
   const uint32_t grid = (P.n_blocks + P.blocks_per_wave - 1) / P.blocks_per_wave;
-  if (all)
-    hipLaunchKernelGGL((decode_blocks_kernel<true>), dim3(grid), dim3(kGroupWaves * kWave), lds, st, P);
-  else
-    hipLaunchKernelGGL((decode_blocks_kernel<false>), dim3(grid), dim3(kGroupWaves * kWave), lds, st, P);
+  void* args[] = {&P};
+  if ((e = hipLaunchKernel(group_k[variant], dim3(grid), dim3(kGroupWaves * kWave), args, lds, st)) != hipSuccess)
+    return e;
   // listed blocks: the big-block kernel (two workgroups per CU), then the
   // general path for what it hands on (its list read as defer_count / defer_list)
   static int cu_count[64] = {};  // per device (benign race: every writer stores the same count)
@@ -1294,14 +1320,10 @@ hipError_t launch_decode(const DecodeParams& P0, void* ws, hipStream_t st) {
   }
   const uint32_t bgrid = min(P.n_blocks, (uint32_t)n_cu * kBigGPerCU);
   if (bgrid) {
-    static uint64_t done_bg_all = 0, done_bg_some = 0;
-    e = all ? set_lds_attr((const void*)decode_big_kernel<true>, kBigGLds, &done_bg_all)
-            : set_lds_attr((const void*)decode_big_kernel<false>, kBigGLds, &done_bg_some);
-    if (e != hipSuccess) return e;
-    if (all)
-      hipLaunchKernelGGL((decode_big_kernel<true>), dim3(bgrid), dim3(kBigGWaves * kWave), kBigGLds, st, P);
-    else
-      hipLaunchKernelGGL((decode_big_kernel<false>), dim3(bgrid), dim3(kBigGWaves * kWave), kBigGLds, st, P);
+    static uint64_t done_bg[4] = {};
+    if ((e = set_lds_attr(big_k[variant], kBigGLds, &done_bg[variant])) != hipSuccess) return e;
+    if ((e = hipLaunchKernel(big_k[variant], dim3(bgrid), dim3(kBigGWaves * kWave), args, kBigGLds, st)) != hipSuccess)
+      return e;
   }
   const uint32_t dgrid = P.n_blocks < 1024 ? P.n_blocks : 1024;
   if (dgrid) {

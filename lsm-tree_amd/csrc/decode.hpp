@@ -44,6 +44,7 @@ struct DecodeParams {
   uint32_t* defer2_count;  // workspace: blocks decode_big_kernel hands on to the general path
   uint32_t* defer2_list;
   uint64_t seqno_add;     // added to every decoded seqno (Scanner's global_seqno, scanner.rs:84)
+  uint32_t compact;       // lsm_decode_blocks16: out.key_off / val_off / val_len are uint16_t arrays
 };
 
 // Diagnostic builds (-DLSM_DIAG, `make variant`) honour ablation bits in

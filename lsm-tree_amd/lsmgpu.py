@@ -36,6 +36,11 @@ class LsmParsed(C.Structure):
                 ("handle_off", C.c_void_p)]
 
 
+class LsmParsed16(C.Structure):
+    _fields_ = [("seqno", C.c_void_p), ("key_off", C.c_void_p), ("val_off", C.c_void_p), ("val_len", C.c_void_p),
+                ("key_len", C.c_void_p), ("prefix_len", C.c_void_p), ("vtype", C.c_void_p)]
+
+
 class LsmBlockParams(C.Structure):
     _fields_ = [("restart_interval", C.c_uint8), ("block_type", C.c_uint8), ("compression", C.c_uint8),
                 ("reserved", C.c_uint8), ("hash_ratio", C.c_float)]
@@ -56,7 +61,7 @@ class LsmTableScan(C.Structure):
                 ("global_seqno", C.c_uint64), ("block_count", C.c_uint64)]
 
 
-ABI_VERSION = 3
+ABI_VERSION = 4
 DECODE_ITEM_START_VALID = 1
 DECODE_PAYLOAD_VERIFIED = 2
 
@@ -95,6 +100,10 @@ def lib():
         L.lsm_decode_blocks_tuned.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_int32, C.POINTER(LsmParsed),
                                               C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t,
                                               C.POINTER(LsmDecodeTuning), C.c_void_p]
+        L.lsm_decode_blocks16.restype = C.c_int
+        L.lsm_decode_blocks16.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_int32, C.POINTER(LsmParsed16),
+                                          C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t,
+                                          C.POINTER(LsmDecodeTuning), C.c_void_p]
         L.lsm_encode_bound.restype = C.c_uint64
         L.lsm_encode_bound.argtypes = [C.c_uint64, C.c_uint32, C.c_uint64, C.c_uint64, C.POINTER(LsmBlockParams)]
         L.lsm_encode_workspace_size.restype = C.c_size_t
@@ -178,7 +187,8 @@ def lib():
 
 
 EXPORTED_SYMBOLS = ["lsm_abi_version", "lsm_status_name", "lsm_last_error", "lsm_device_count", "lsm_set_device",
-                    "lsm_decode_workspace_size", "lsm_decode_blocks", "lsm_decode_blocks_tuned", "lsm_encode_bound",
+                    "lsm_decode_workspace_size", "lsm_decode_blocks", "lsm_decode_blocks_tuned", "lsm_decode_blocks16",
+                    "lsm_encode_bound",
                     "lsm_encode_workspace_size", "lsm_encode_blocks", "lsm_cut_blocks", "lsm_xxh3_128_batch",
                     "lsm_point_read_blocks", "lsm_xxh3_128_file_workspace_size", "lsm_xxh3_128_file",
                     "lsm_bloom_calculate_m", "lsm_bloom_shape", "lsm_bloom_filter_size", "lsm_hash64_keys",
@@ -232,6 +242,9 @@ def to_device_bytes(data, device="cuda"):
 
 PARSED_FIELDS = (("seqno", "int64"), ("key_off", "int32"), ("val_off", "int32"), ("val_len", "int32"),
                  ("key_len", "int16"), ("prefix_len", "int16"), ("vtype", "uint8"), ("handle_off", "int64"))
+# lsm_parsed_items16: 16-bit payload offsets and lengths, 19 B/item (no handle_off)
+PARSED16_FIELDS = (("seqno", "int64"), ("key_off", "int16"), ("val_off", "int16"), ("val_len", "int16"),
+                   ("key_len", "int16"), ("prefix_len", "int16"), ("vtype", "uint8"))
 
 
 class Decoder:
@@ -248,22 +261,39 @@ class Decoder:
             self.ws = torch.empty(max(need, 256), dtype=torch.uint8, device=self.device)
         return self.ws
 
-    def alloc_outputs(self, item_cap, n_blocks, fields=None):
+    def alloc_outputs(self, item_cap, n_blocks, fields=None, compact=False):
         torch = _torch()
-        fields = fields or [f for f, _ in PARSED_FIELDS]
+        spec = PARSED16_FIELDS if compact else PARSED_FIELDS
+        fields = fields or [f for f, _ in spec]
         out = {}
-        for f, dt in PARSED_FIELDS:
+        for f, dt in spec:
             if f in fields:
                 out[f] = torch.empty(max(item_cap, 1), dtype=getattr(torch, dt), device=self.device)
         out["item_start"] = torch.empty(n_blocks + 1, dtype=torch.int32, device=self.device)
         out["status"] = torch.empty(max(n_blocks, 1), dtype=torch.int32, device=self.device)
         return out
 
-    def decode(self, blocks, block_off, n_blocks, out, item_cap, expect_type=-1, tuning=None, stream=None):
-        """Enqueue lsm_decode_blocks. blocks: uint8 cuda (padded); block_off: int64 cuda [n+1]."""
+    def decode(self, blocks, block_off, n_blocks, out, item_cap, expect_type=-1, tuning=None, stream=None,
+               compact=False):
+        """Enqueue lsm_decode_blocks (compact: lsm_decode_blocks16 into 16-bit
+        offset arrays from alloc_outputs(..., compact=True)).  blocks: uint8 cuda
+        (padded); block_off: int64 cuda [n+1]."""
         if tuning is None and os.environ.get("LSMGPU_DECODE_TUNING"):  # diagnostic override
             tuning = tuple(int(x, 0) for x in os.environ["LSMGPU_DECODE_TUNING"].split(","))
         ws = self.workspace(n_blocks)
+        if compact:
+            ps = LsmParsed16()
+            for f, dt in PARSED16_FIELDS:
+                if f in out and out[f].element_size() != C.sizeof(C.c_uint64 if dt == "int64" else
+                                                                  C.c_uint16 if dt == "int16" else C.c_uint8):
+                    raise LsmError(f"compact decode: field {f} must be {dt}")
+                setattr(ps, f, out[f].data_ptr() if f in out else None)
+            t = C.byref(LsmDecodeTuning(*tuning)) if tuning is not None else None
+            rc = lib().lsm_decode_blocks16(_ptr(blocks), _ptr(block_off), n_blocks, expect_type, C.byref(ps),
+                                           item_cap, _ptr(out["item_start"]), _ptr(out["status"]), _ptr(ws),
+                                           ws.numel(), t, _stream(stream))
+            _check(rc, "lsm_decode_blocks16")
+            return out
         ps = LsmParsed()
         for f, _ in PARSED_FIELDS:
             setattr(ps, f, out[f].data_ptr() if f in out else None)
@@ -280,14 +310,16 @@ class Decoder:
         return out
 
 
-def decode_blocks(blocks, block_off, n_blocks=None, expect_type=-1, item_cap=None, fields=None, tuning=None):
-    """Convenience: decode device blocks, returns dict of device tensors."""
+def decode_blocks(blocks, block_off, n_blocks=None, expect_type=-1, item_cap=None, fields=None, tuning=None,
+                  compact=False):
+    """Convenience: decode device blocks, returns dict of device tensors
+    (compact: the 19 B/item lsm_parsed_items16 layout)."""
     n_blocks = (block_off.numel() - 1) if n_blocks is None else n_blocks
     if item_cap is None:
         item_cap = blocks.numel() // 3 + 1
     d = Decoder(blocks.device)
-    out = d.alloc_outputs(item_cap, n_blocks, fields)
-    return d.decode(blocks, block_off, n_blocks, out, item_cap, expect_type, tuning)
+    out = d.alloc_outputs(item_cap, n_blocks, fields, compact)
+    return d.decode(blocks, block_off, n_blocks, out, item_cap, expect_type, tuning, compact=compact)
 
 
 class Encoder:
