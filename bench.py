@@ -471,7 +471,7 @@ def bench_large_blocks(torch, lsmgpu, threads, steps=5):
                      "decode_GiB_per_s": round(total / (dec_ms * 1e-3) / 2 ** 30, 2), "oracle_checked_blocks": nb}
         del items, enc, out, ref_buf
         torch.cuda.empty_cache()
-    res["note"] = ("encode: one wave per block straight in HBM (encode_large_kernel); decode: 4-wave workgroup per "
+    res["note"] = ("encode: plan workgroups of ~16 Ki items, then one 8-wave workgroup per block straight in HBM (encode_large_kernel: record per thread at its E1 offset, per-KiB XXH3 contributions on every wave, chain on one); decode: 4-wave workgroup per "
                    "block through a 72 KiB stage in 64 KiB chunks (XXH3 chain carried across chunks)")
     return res
 

@@ -25,6 +25,8 @@
 
 #include <math.h>
 
+#include <algorithm>
+
 #include "block_format.hpp"
 #include "decode.hpp"
 #include "encode.hpp"
@@ -105,6 +107,7 @@ struct EncodeParams {
   float ratio;
   uint32_t type;
   uint32_t diag;  // lsm_block_params.reserved: diagnostic ablations (0 in normal use)
+  uint32_t plan_bpw;  // blocks per plan workgroup (<= kPlanBlocks), see plan_blocks_per_wg
   uint8_t* out;
   uint64_t out_cap;
   uint64_t* block_off;
@@ -730,8 +733,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LSM_PLAN_WP
   __shared__ uint32_t mono;
   __shared__ unsigned long long kos[kPlanChunk + 1];  // key offsets of the chunk's items (+ the next)
   const uint32_t tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
-  const uint32_t b0 = blockIdx.x * kPlanBlocks;
-  const uint32_t nb = min(kPlanBlocks, P.n_blocks - b0);
+  const uint32_t b0 = blockIdx.x * P.plan_bpw;
+  const uint32_t nb = min(P.plan_bpw, P.n_blocks - b0);
   if (tid <= nb) bst[tid] = P.starts[b0 + tid];
   if (tid < nb) {
     bfirst[tid] = bend[tid] = lhead[tid] = 0;
@@ -860,7 +863,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LSM_PLAN_WP
         const bool head = jj == ridx * ri;
         const uint64_t roff = exq[q] - bfirst[jq[q]];
         const uint32_t x = head ? ridx : m[q].sh;
-        P.erec[i0 + q] = (uint32_t)min(roff, (uint64_t)0x7FFF) | (head ? kErecHead : 0u) | (min(x, 0xFFFFu) << 16);
+        // blocks of more than kGItems items are never group-class: their items
+        // keep the whole 32-bit record offset, for E3
+        P.erec[i0 + q] = bst[jq[q] + 1] - bst[jq[q]] > kGItems ? (uint32_t)min(roff, (uint64_t)0xFFFFFFFFu)
+                                     : (uint32_t)min(roff, (uint64_t)0x7FFF) | (head ? kErecHead : 0u) |
+                                           (min(x, 0xFFFFu) << 16);
       }
     }
     carry += ptot;
@@ -1497,9 +1504,24 @@ __global__ __launch_bounds__(kWave) void encode_write_list_kernel(EncodeParams P
 }
 
 // ----------------------------------------------------- E3: HBM write pass
-__global__ __launch_bounds__(64) void encode_large_kernel(EncodeParams P) {
+// Blocks larger than the list kernels' 96 KiB image (data blocks up to the
+// writer's 4 MiB target, writer/mod.rs:193-198), one 8-wave workgroup per
+// block, straight in HBM:
+//   records  thread = item, at the record offset E1 left in erec (blocks of
+//            more than kGItems items) or from a workgroup scan (fewer items);
+//            the shared prefix is recomputed from the keys
+//   hash     hash-index votes in LDS passes of kE3HashChunk buckets
+//   tail     marker, trailer (wave 0)
+//   xxh3     of the bytes just written: per 64 KiB, every wave reduces KiB
+//            blocks into LDS contributions, then wave 0 carries the scramble
+//            chain (as decode_chunked), the tail merge and the header.
+constexpr uint32_t kE3Waves = 8, kE3Threads = kE3Waves * kWave;
+__global__ __launch_bounds__(kE3Threads) void encode_large_kernel(EncodeParams P) {
   __shared__ uint32_t hlo[kE3HashChunk], hhi[kE3HashChunk];
-  const int lane = threadIdx.x;
+  __shared__ uint64_t contrib[8 * 64];
+  __shared__ uint32_t psum[kE3Waves];
+  const uint32_t tid = threadIdx.x, lane = tid & (kWave - 1);
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid / kWave);
   const uint32_t count = P.list_count[0];
   for (uint32_t li = blockIdx.x; li < count; li += gridDim.x) {
     const uint32_t b = P.lists[li];
@@ -1508,7 +1530,7 @@ __global__ __launch_bounds__(64) void encode_large_kernel(EncodeParams P) {
     const uint32_t step = pl.step_flags & 0xFF;
     const uint64_t dst_off = P.block_off[b], dst_end = P.block_off[b + 1];
     if (dst_end > P.out_cap) {
-      if (lane == 0) P.status[b] = ST_OVERFLOW;
+      if (tid == 0) P.status[b] = ST_OVERFLOW;
       continue;
     }
     const uint32_t s = P.starts[b], e = P.starts[b + 1], n = e - s;
@@ -1520,33 +1542,41 @@ __global__ __launch_bounds__(64) void encode_large_kernel(EncodeParams P) {
     const uint32_t pad = (uint32_t)(dabs & 15);
     const uint32_t p0 = pad + kHdrLen;
     const uint32_t bin_off = pl.recs + 1;
-    uint32_t carry = 0;
-    for (uint32_t c = 0; c < n; c += kWave) {
-      const uint32_t j = c + lane;
+    const bool scan = n <= kGItems;  // (uniform) else erec holds each record's offset
+    for (uint32_t j = tid; j < (scan ? kE3Threads : n); j += kE3Threads) {
       const bool head = j % ri == 0;
       ItemMeta m;
-      RecordCopy rc;
-      uint32_t rec = 0;
+      uint32_t roff = 0;
       if (j < n) {
         bool bad = false;
         m = load_item_lcp(P, s, j, ri, bad);
-        rec = (uint32_t)item_record_len(P, m, head);
+        if (!scan) roff = P.erec[s + j];
       }
-      const uint32_t incl = wave_incl_scan_u32(rec);
-      const uint32_t roff = carry + incl - rec;
+      if (scan) {  // n <= kGItems <= kE3Threads: one pass
+        const uint32_t rec = j < n ? (uint32_t)item_record_len(P, m, head) : 0u;
+        const uint32_t incl = wave_incl_scan_u32(rec);
+        if (lane == kWave - 1) psum[wave] = incl;
+        __syncthreads();
+        uint32_t base = 0;
+        for (uint32_t w = 0; w < wave; ++w) base += psum[w];
+        roff = base + incl - rec;
+      }
       if (j < n) {
+        RecordCopy rc;
         rc.issue(P, m, head, p0 + roff);
         rc.store(P, m, head, img);
-        if (j % ri == 0) store_le(img, p0 + bin_off + (j / ri) * step, roff, step);
+        if (head) store_le(img, p0 + bin_off + (j / ri) * step, roff, step);
       }
-      carry += wave_bcast_u32(incl, 63);
     }
     const uint32_t hash_off = pl.hash_w ? bin_off + pl.bin_len * step : 0;
     for (uint32_t base = 0; base < pl.hash_w; base += kE3HashChunk) {
       const uint32_t lim = min(kE3HashChunk, pl.hash_w - base);
-      for (uint32_t k = lane; k < lim; k += kWave) { hlo[k] = 0xFFFFFFFFu; hhi[k] = 0; }
+      for (uint32_t k = tid; k < lim; k += kE3Threads) {
+        hlo[k] = 0xFFFFFFFFu;
+        hhi[k] = 0;
+      }
       __syncthreads();
-      for (uint32_t j = lane; j < n; j += kWave) {
+      for (uint32_t j = tid; j < n; j += kE3Threads) {
         const uint64_t i = (uint64_t)s + j;
         const uint64_t ko = P.it.key_off[i];
         const uint32_t bk = key_bucket(P, ko, (uint32_t)(P.it.key_off[i + 1] - ko), pl.hash_w);
@@ -1556,17 +1586,41 @@ __global__ __launch_bounds__(64) void encode_large_kernel(EncodeParams P) {
         }
       }
       __syncthreads();
-      for (uint32_t k = lane; k < lim; k += kWave) img[p0 + hash_off + base + k] = (uint8_t)bucket_byte(hlo[k], hhi[k]);
+      for (uint32_t k = tid; k < lim; k += kE3Threads) img[p0 + hash_off + base + k] = (uint8_t)bucket_byte(hlo[k], hhi[k]);
       __syncthreads();
     }
-    if (lane == 0) img[p0 + pl.recs] = kTrailerMarker;
-    write_trailer_bytes(img, p0 + plen - kTrailerLen, ri, step, pl.bin_len, bin_off, pl.hash_w, hash_off, n);
-    __threadfence();  // make this wave's HBM writes visible to its own re-reads below
+    if (wave == 0) {
+      if (lane == 0) img[p0 + pl.recs] = kTrailerMarker;
+      write_trailer_bytes(img, p0 + plen - kTrailerLen, ri, step, pl.bin_len, bin_off, pl.hash_w, hash_off, n);
+    }
+    __threadfence();  // the block's bytes, for the re-reads below
     __syncthreads();
-    uint64_t ck_lo, ck_hi;
-    xxh3_128_wave(img, p0, plen, &kLongSecret, ck_lo, ck_hi);
-    write_header_bytes(img, pad, P.type, ck_lo, ck_hi, plen);
-    if (lane == 0) P.status[b] = ST_OK;
+    uint64_t lo = 0, hi = 0;
+    if (plen > 240) {
+      const int q = lane & 3;
+      uint64_t a0, a1;
+      xxh3_acc_init(q, a0, a1);
+      const uint64_t scr0 = kLongSecret.acc[16 + 2 * q], scr1 = kLongSecret.acc[16 + 2 * q + 1];
+      const uint32_t nbk = (plen - 1) / 1024;
+      for (uint32_t n0 = 0; n0 < nbk; n0 += 64) {
+        const uint32_t n1 = min(nbk, n0 + 64);
+        xxh3_kib_contribs(img, p0 + 1024 * n0, (n1 - n0) * 1024 + 1, &kLongSecret, contrib, wave, kE3Waves);
+        __syncthreads();
+        if (wave == 0)
+          for (uint32_t k = 0; k < n1 - n0; ++k) {
+            a0 = xxh3_scr(a0, contrib[8 * k + 2 * q], scr0);
+            a1 = xxh3_scr(a1, contrib[8 * k + 2 * q + 1], scr1);
+          }
+        __syncthreads();
+      }
+      if (wave == 0) xxh3_wave_tail_merge(img, p0, plen, &kLongSecret, a0, a1, lo, hi);
+    } else if (wave == 0) {
+      xxh3_128_wave(img, p0, plen, &kLongSecret, lo, hi);
+    }
+    if (wave == 0) {
+      write_header_bytes(img, pad, P.type, lo, hi, plen);
+      if (lane == 0) P.status[b] = ST_OK;
+    }
     __syncthreads();
   }
 }
@@ -1595,6 +1649,16 @@ static unsigned long long* diag_phase_buffer() {
 #endif
 
 static size_t al256(size_t x) { return (x + 255) / 256 * 256; }
+
+// A plan workgroup walks its blocks' items serially (chunks of 512), so it
+// owns about 16 Ki items: kPlanBlocks blocks of the 4 KiB shapes, down to one
+// block each for 1-4 MiB data blocks (which gave a single workgroup 3 M items
+// and a 27 ms plan for 60 blocks of 4 MiB).
+static uint32_t plan_blocks_per_wg(uint64_t n_items, uint32_t n_blocks) {
+  const uint64_t avg = n_blocks ? (n_items + n_blocks - 1) / n_blocks : 1;
+  const uint64_t bpw = (16384 + avg - 1) / (avg ? avg : 1);
+  return (uint32_t)std::min<uint64_t>(kPlanBlocks, std::max<uint64_t>(1, bpw));
+}
 
 size_t encode_workspace_size(uint64_t n_items, uint32_t n_blocks) {
   return 2 * al256(((size_t)n_blocks + 1) * 8) + al256((size_t)n_blocks * 8) +
@@ -1641,7 +1705,8 @@ hipError_t launch_encode(const lsm_items& items, const uint32_t* starts, uint32_
   uint64_t* tiles = (uint64_t*)w; w += al256(scan_tiles(n_blocks) * 8);
   P.erec = (uint32_t*)w;
   hipError_t e;
-  const dim3 pgrid((n_blocks + kPlanBlocks - 1) / kPlanBlocks);
+  P.plan_bpw = plan_blocks_per_wg(items.n_items, n_blocks);
+  const dim3 pgrid((n_blocks + P.plan_bpw - 1) / P.plan_bpw);
   if (P.type == 1)
     hipLaunchKernelGGL(encode_plan_kernel<true>, pgrid, dim3(256), 0, st, P);
   else
@@ -1660,7 +1725,7 @@ hipError_t launch_encode(const lsm_items& items, const uint32_t* starts, uint32_
     hipLaunchKernelGGL((encode_group_kernel<false, false>), ggrid, gblock, 0, st, P);
   hipLaunchKernelGGL(encode_write_list_kernel, dim3(2048), dim3(kWave), kImgMedium, st, P, kPlanMedium);
   hipLaunchKernelGGL(encode_write_list_kernel, dim3(512), dim3(kWave), kImgBig, st, P, kPlanBig);
-  hipLaunchKernelGGL(encode_large_kernel, dim3(1024), dim3(64), 0, st, P);
+  hipLaunchKernelGGL(encode_large_kernel, dim3(512), dim3(kE3Threads), 0, st, P);
   return hipGetLastError();
 }
 

@@ -62,3 +62,22 @@ def test_large_data_blocks_corrupted(gpu):
     parsed, item_start, status = pyoracle.decode_blocks(buf2, off2)
     assert (status[:2] == 0).all() and status[2] == 4 and (status[3:] != 0).all(), status
     compare_decode(g, parsed, item_start, status)
+
+
+@pytest.mark.parametrize("ratio", [0.0, 1.33])
+def test_large_blocks_few_items(gpu, ratio):
+    """Blocks beyond the 96 KiB list image with at most 256 items (long values):
+    E3 takes their record offsets from its own workgroup scan (E1 keeps full
+    32-bit offsets only for blocks of more than 256 items); long seqnos and
+    value lengths give multi-byte varints."""
+    items = counter_items(400, key_len=24, val_len=3000, seqno=(1 << 40) + 5, seed=11, tomb_frac=0.1)
+    starts = np.array([0, 40, 290, 400], np.uint32)  # ~110 KiB, ~680 KiB (250 items), ~300 KiB
+    ref_buf, ref_off = pyoracle.encode_blocks(items, starts, restart_interval=16, hash_ratio=ratio)
+    sizes = np.diff(ref_off.astype(np.int64))
+    assert (sizes > 96 * 1024).all(), sizes
+    buf, off, st = _gpu_encode(gpu, items, starts, 16, ratio)
+    assert (st == 0).all() and (off == ref_off).all() and buf.tobytes() == ref_buf.tobytes()
+    g = gpu_decode(gpu, buf, off)
+    parsed, item_start, status = pyoracle.decode_blocks(buf, off)
+    assert (status == 0).all()
+    compare_decode(g, parsed, item_start, status)
