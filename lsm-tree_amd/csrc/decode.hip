@@ -863,7 +863,7 @@ __device__ __forceinline__ BigBlk big_blk(const DecodeParams& P, uint32_t li) {
   return x;
 }
 
-#ifdef LSM_DIAG
+#if defined(LSM_DIAG) && !defined(LSM_DIAG_NOTIME)
 // Diagnostic builds: per-phase s_memtime totals of wave 0 of every big-block
 // workgroup (read by lsm_diag_decode_phases).
 __device__ unsigned long long g_dec_phase[32];
@@ -886,7 +886,7 @@ __device__ unsigned long long g_dec_phase[32];
 
 template <bool kAllFields, bool kCompact>
 __global__ __launch_bounds__(kBigGWaves * kWave) void decode_big_kernel(DecodeParams P) {
-#ifdef LSM_DIAG
+#if defined(LSM_DIAG) && !defined(LSM_DIAG_NOTIME)
   uint64_t t_last = __builtin_amdgcn_s_memtime(), ph[8] = {};
   uint32_t nblk = 0;
 #endif
@@ -1010,12 +1010,12 @@ __global__ __launch_bounds__(kBigGWaves * kWave) void decode_big_kernel(DecodePa
     DEC_PHASE(5);
     if (Xn.fits) issue_dma(Xn, stages);
     DEC_PHASE(6);
-#ifdef LSM_DIAG
+#if defined(LSM_DIAG) && !defined(LSM_DIAG_NOTIME)
     ++nblk;
 #endif
     X = Xn;
   }
-#ifdef LSM_DIAG
+#if defined(LSM_DIAG) && !defined(LSM_DIAG_NOTIME)
   if (tid == 0) {
     for (int i = 0; i < 8; ++i) atomicAdd(&g_dec_phase[i], (unsigned long long)ph[i]);
     atomicAdd(&g_dec_phase[15], (unsigned long long)nblk);
@@ -1052,7 +1052,7 @@ constexpr int kPrioH = LSM_PRIO_H;  // s_setprio of a wave hashing one whole blo
 template <bool kAllFields, bool kCompact>
 __global__ __launch_bounds__(kGroupWaves * kWave) __attribute__((amdgpu_waves_per_eu(LSM_DEC_WPE))) void decode_blocks_kernel(DecodeParams P) {
   // LDS: [meta: G x 80 B][rec: u64 per item + 1 scratch][owner: u8 per item][staged bytes + pad][secret]
-#ifdef LSM_DIAG
+#if defined(LSM_DIAG) && !defined(LSM_DIAG_NOTIME)
   uint64_t t_last = __builtin_amdgcn_s_memtime(), ph[16] = {};
 #endif
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
@@ -1215,13 +1215,13 @@ __global__ __launch_bounds__(kGroupWaves * kWave) __attribute__((amdgpu_waves_pe
     }
     if (Gn.k) issue_dma(Gn, img);  // refill the stage after phase B
     DEC_PHASE(4);
-#ifdef LSM_DIAG
+#if defined(LSM_DIAG) && !defined(LSM_DIAG_NOTIME)
     ph[5] += 1;
     ph[6] += k;
 #endif
     G = Gn;
   }
-#ifdef LSM_DIAG
+#if defined(LSM_DIAG) && !defined(LSM_DIAG_NOTIME)
   if (lane == 0) {
     for (int i = 0; i < 16; ++i)
       if ((i >= 8 || wave == 0) && ph[i]) atomicAdd(&g_dec_phase[16 + i], (unsigned long long)ph[i]);
@@ -1340,7 +1340,7 @@ hipError_t launch_decode(const DecodeParams& P0, void* ws, hipStream_t st) {
 
 }  // namespace lsmgpu
 
-#ifdef LSM_DIAG
+#if defined(LSM_DIAG) && !defined(LSM_DIAG_NOTIME)
 // Diagnostic builds only: copy out and clear the big-block kernel's phase totals.
 // Entries 16..31 are the group kernel's (wave 0 per group, role timers summed over waves).
 extern "C" int lsm_diag_decode_phases(uint64_t* out32) {
