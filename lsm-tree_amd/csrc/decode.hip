@@ -1095,7 +1095,7 @@ __global__ __launch_bounds__(kGroupWaves * kWave) __attribute__((amdgpu_waves_pe
   };
   // LDS-DMA of a group's span (wave w moves 1-KiB pieces w, w + 4, ...).
   auto issue_dma = [&](const Group& g, uint8_t* dst) {
-    const uint32_t chunks = (uint32_t)((g.span1 - g.span0) >> 4);
+    const uint32_t chunks = (kDiagBuild && (P.flags & kDiagSkipDma)) ? 0u : (uint32_t)((g.span1 - g.span0) >> 4);
     const uint8_t* src = P.blocks + g.span0 + 16 * lane;
     for (uint32_t i = wave; i * kWave < chunks; i += kGroupWaves) {
       if (i * kWave + lane < chunks)
@@ -1125,7 +1125,7 @@ __global__ __launch_bounds__(kGroupWaves * kWave) __attribute__((amdgpu_waves_pe
     DEC_PHASE(0);
     const Group Gn = next_group(b + k);
     // ---- 2. wave 0: headers, trailers, restart-interval numbering; owner[c] = block of interval c
-    if (wave == 0) {
+    if (wave == 0 && !(kDiagBuild && (P.flags & kDiagSkipHeader))) {
       uint32_t chains = 0;
       BlockMeta m;
       if ((uint32_t)lane < k) {

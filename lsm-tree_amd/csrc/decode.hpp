@@ -56,7 +56,10 @@ constexpr bool kDiagBuild = true;
 constexpr bool kDiagBuild = false;
 #endif
 constexpr uint32_t kDiagSkipHash = 0x100, kDiagSkipParse = 0x200, kDiagSkipStore = 0x400, kDiagSkipPhaseB = 0x800;
-constexpr uint32_t kDecodeDiagMask = kDiagSkipHash | kDiagSkipParse | kDiagSkipStore | kDiagSkipPhaseB;
+// (group kernel, stage-only profiling: outputs and statuses invalid) no header / trailer wave; no stage DMA
+constexpr uint32_t kDiagSkipHeader = 0x1000, kDiagSkipDma = 0x2000;
+constexpr uint32_t kDecodeDiagMask =
+    kDiagSkipHash | kDiagSkipParse | kDiagSkipStore | kDiagSkipPhaseB | kDiagSkipHeader | kDiagSkipDma;
 
 // The > 64 KiB dynamic-LDS attribute acts on the CURRENT device: set it once
 // per device (a process may drive several GPUs, one host thread per device).

@@ -905,6 +905,232 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LSM_PLAN_WP
   }
 }
 
+// ------------------------------------- E1 for data blocks: wave-level runs
+// The outputs of encode_plan_kernel<false> without workgroup barriers in the
+// item loop: the workgroup's blocks are split among its four waves by item
+// count (whole blocks each), and every wave walks its own items in steps of
+// 128 (two consecutive items per lane).  Record offsets come from a wave scan
+// plus a carry (a block never spans two waves); the shared prefix with the
+// restart head (encoder.rs:140-143, util.rs:125-130) takes the head's key
+// offset from the step's LDS copy, or for a head before the step from the
+// carried last head; and the next step's item fields are loaded while this
+// step's key windows are in flight.
+constexpr uint32_t kPWStep = 2 * kWave;
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void encode_plan_wave_kernel(EncodeParams P) {
+  __shared__ uint32_t bst[kPlanBlocks + 1];
+  __shared__ unsigned long long bfirst[kPlanBlocks], bend[kPlanBlocks], lhead[kPlanBlocks];
+  __shared__ unsigned long long kos[4][kPWStep];
+  __shared__ uint32_t kls[4][kPWStep];
+  __shared__ uint32_t badf[kPlanBlocks];
+  __shared__ uint32_t wcut[5];
+  __shared__ uint32_t mono;
+  const uint32_t tid = threadIdx.x, lane = tid & (kWave - 1);
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid / kWave);
+  const uint32_t b0 = blockIdx.x * P.plan_bpw;
+  const uint32_t nb = min(P.plan_bpw, P.n_blocks - b0);
+  if (tid <= nb) bst[tid] = P.starts[b0 + tid];
+  if (tid < nb) {
+    bfirst[tid] = bend[tid] = lhead[tid] = 0;
+    badf[tid] = 0;
+  }
+  if (tid == 0) mono = 1;
+  __syncthreads();
+  if (tid < nb && bst[tid + 1] < bst[tid]) mono = 0;  // (benign race: every writer stores 0)
+  if (tid <= 4) {  // wave t's first block: the first at or after a quarter of the items
+    const uint32_t target = bst[0] + (uint32_t)(((uint64_t)(bst[nb] - bst[0]) * tid) / 4);
+    uint32_t lo = 0, hi = nb;  // first j with bst[j] >= target (bst[nb] >= target)
+    while (lo < hi) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (bst[mid] >= target) hi = mid;
+      else lo = mid + 1;
+    }
+    wcut[tid] = tid == 4 ? nb : lo;
+  }
+  __syncthreads();
+  const uint32_t ri = P.ri;
+  const uint32_t jlo = __builtin_amdgcn_readfirstlane(wcut[wave]);
+  const uint32_t jhi = __builtin_amdgcn_readfirstlane(mono ? wcut[wave + 1] : wcut[wave]);
+  const uint32_t ia = __builtin_amdgcn_readfirstlane(bst[jlo]);
+  const uint32_t ie = __builtin_amdgcn_readfirstlane(bst[jhi]);
+  unsigned long long* wkos = kos[wave];
+  uint32_t* wkls = kls[wave];
+  // a lane's two consecutive items: key / value offsets [t, t + 3), seqnos and types [t, t + 2)
+  struct StepRaw {
+    uint64_t ko[3], vo[3], seq[2];
+    uint32_t vt[2];
+  };
+  auto load_step = [&](uint32_t base, StepRaw& r) {
+    // (items past the run are clamped to its last one and ignored; offsets index up to ie)
+    const uint32_t n = ie - base, t = min(2 * lane, n - 1), t1 = min(t + 1, n - 1);
+    auto at64 = [&](const uint64_t* a, uint32_t k) {
+      return *reinterpret_cast<const uint64_t*>(reinterpret_cast<const uint8_t*>(a + base) + 8u * k);
+    };
+    r.ko[0] = at64(P.it.key_off, t);
+    r.ko[1] = at64(P.it.key_off, t + 1);
+    r.ko[2] = at64(P.it.key_off, min(t + 2, n));
+    r.vo[0] = at64(P.it.val_off, t);
+    r.vo[1] = at64(P.it.val_off, t + 1);
+    r.vo[2] = at64(P.it.val_off, min(t + 2, n));
+    r.seq[0] = at64(P.it.seqno, t);
+    r.seq[1] = at64(P.it.seqno, t1);
+    r.vt[0] = (P.it.vtype + base)[t];
+    r.vt[1] = (P.it.vtype + base)[t1];
+  };
+  StepRaw raw, nxt;
+  if (ia < ie) load_step(ia, raw);
+  uint64_t carry = 0;     // record bytes of this wave's items before the step
+  uint64_t hk_ko = 0;     // the last restart head of the previous step: key offset, key length
+  uint32_t hk_kl = 0;
+  for (uint32_t base = ia; base < ie; base += kPWStep) {
+    if (base + kPWStep < ie) load_step(base + kPWStep, nxt);  // in flight under this step
+    const uint32_t t0 = 2 * lane;
+    ItemMeta m[2];
+    uint32_t jq[2], jjq[2];
+    bool ok[2];
+    uint32_t j = jlo;
+    {
+      uint32_t lo = jlo, hi = jhi;  // block j: bst[j] <= base + t0 < bst[j + 1]
+      const uint32_t i0 = min(base + t0, ie - 1);
+      while (hi - lo > 1) {
+        const uint32_t mid = (lo + hi) >> 1;
+        if (bst[mid] <= i0) lo = mid;
+        else hi = mid;
+      }
+      j = lo;
+    }
+#pragma unroll
+    for (uint32_t q = 0; q < 2; ++q) {
+      const uint32_t i = base + t0 + q;
+      ok[q] = i < ie;
+      while (j + 1 < jhi && bst[j + 1] <= i) ++j;
+      jq[q] = j;
+      jjq[q] = ok[q] ? i - bst[j] : 0;
+      bool bad = false;
+      RawItem r;
+      r.ko = raw.ko[q];
+      r.ko1 = raw.ko[q + 1];
+      r.vo = raw.vo[q];
+      r.vo1 = raw.vo[q + 1];
+      r.seq = raw.seq[q];
+      r.vt = raw.vt[q];
+      r.e = 0;
+      m[q] = cook_item<false>(r, bad);
+      if (ok[q] && bad) atomicOr(&badf[j], 1u);
+      wkos[t0 + q] = m[q].ko;
+      wkls[t0 + q] = m[q].klen;
+    }
+    wave_lds_sync();
+    // ---- shared prefix with the restart head: both keys' first 16 bytes in flight together
+    Win16 wa[2], wb[2];
+    uint32_t nq[2];
+    uint64_t hq[2];
+#pragma unroll
+    for (uint32_t q = 0; q < 2; ++q) {
+      nq[q] = 0;
+      hq[q] = 0;
+      if (ok[q] && jjq[q] % ri != 0) {
+        const uint32_t h = base + t0 + q - jjq[q] % ri;
+        const bool in = h >= base;
+        const uint64_t hko = in ? (uint64_t)wkos[h - base] : hk_ko;
+        const uint32_t hkl = in ? wkls[h - base] : hk_kl;
+        nq[q] = min(hkl, m[q].klen);
+        hq[q] = hko;
+        wa[q] = gwin16(P.it.keys + hko);
+        wb[q] = gwin16(P.it.keys + m[q].ko);
+      }
+    }
+#pragma unroll
+    for (uint32_t q = 0; q < 2; ++q) {
+      if (!nq[q]) continue;
+      const uint64_t x0 = wa[q].lo ^ wb[q].lo, x1 = wa[q].hi ^ wb[q].hi;
+      const uint32_t n = nq[q];
+      uint32_t sh;
+      if (x0) sh = min(n, (uint32_t)(__builtin_ctzll(x0) >> 3));
+      else if (x1) sh = min(n, 8 + (uint32_t)(__builtin_ctzll(x1) >> 3));
+      else sh = n <= 16 ? n : lcp_tail(P.it.keys, hq[q], m[q].ko, n);
+      m[q].sh = sh;
+    }
+    // ---- record lengths, wave scan (a block never spans two waves)
+    uint64_t rec[2];
+#pragma unroll
+    for (uint32_t q = 0; q < 2; ++q) rec[q] = ok[q] ? item_record_len(P, m[q], jjq[q] % ri == 0) : 0;
+    const uint64_t tsum = rec[0] + rec[1];
+    const uint64_t incl = wave_incl_scan_u64(tsum);
+    uint64_t ex = carry + incl - tsum;
+    uint64_t exq[2];
+#pragma unroll
+    for (uint32_t q = 0; q < 2; ++q) {
+      exq[q] = ex;
+      if (ok[q]) {
+        const uint32_t jb = jq[q], jj = jjq[q], ridx = jj / ri;
+        const uint32_t n = bst[jb + 1] - bst[jb];
+        if (jj == 0) bfirst[jb] = ex;
+        if (jj + 1 == n) bend[jb] = ex + rec[q];
+        if (jj == ridx * ri && ridx == (n - 1) / ri) lhead[jb] = ex;
+      }
+      ex += rec[q];
+    }
+    wave_lds_sync();
+#pragma unroll
+    for (uint32_t q = 0; q < 2; ++q) {
+      if (ok[q]) {
+        const uint32_t jj = jjq[q], ridx = jj / ri;
+        const bool head = jj == ridx * ri;
+        const uint64_t roff = exq[q] - bfirst[jq[q]];
+        const uint32_t x = head ? ridx : m[q].sh;
+        // blocks of more than kGItems items are never group-class: their items
+        // keep the whole 32-bit record offset, for E3
+        P.erec[(uint64_t)base + t0 + q] =
+            bst[jq[q] + 1] - bst[jq[q]] > kGItems
+                ? (uint32_t)min(roff, (uint64_t)0xFFFFFFFFu)
+                : (uint32_t)min(roff, (uint64_t)0x7FFF) | (head ? kErecHead : 0u) | (min(x, 0xFFFFu) << 16);
+      }
+    }
+    carry += wave_bcast_u64(incl, kWave - 1);
+    {  // the restart head of the step's last item, for the next step's first items
+      const uint32_t last = min(ie, base + kPWStep) - 1, ll = (last - base) >> 1, lq = (last - base) & 1;
+      const uint32_t jjl = __builtin_amdgcn_readlane((int)(lq ? jjq[1] : jjq[0]), (int)ll);
+      const uint32_t h = last - jjl % ri;
+      if (h >= base) {
+        hk_ko = wkos[h - base];
+        hk_kl = wkls[h - base];
+      }
+    }
+    wave_lds_sync();  // (the next step rewrites kos / kls)
+    raw = nxt;
+  }
+  __syncthreads();
+  if (tid >= nb) return;
+  const uint32_t b = b0 + tid, s = bst[tid], e = bst[tid + 1];
+  bool bad = !mono || e <= s || badf[tid];
+  const uint32_t n = bad ? 0 : e - s;
+  const uint64_t recs = bad ? 0 : bend[tid] - bfirst[tid], last_head = bad ? 0 : lhead[tid] - bfirst[tid];
+  const uint32_t bin_len = n ? (n + ri - 1) / ri : 0;
+  const uint32_t step = last_head <= 0xFFFF ? 2 : 4;
+  const uint32_t buckets = bucket_count(n, P.ratio);
+  const uint32_t hash_w = (buckets > 0 && bin_len <= kHashMaxPointers) ? buckets : 0;
+  const uint64_t total = kHdrLen + recs + 1 + (uint64_t)bin_len * step + hash_w + kTrailerLen;
+  if (recs > 0xFFFFFFF0ULL || total > 0xFFFFFF00ULL) bad = true;
+  const uint64_t ks = P.it.key_off[s], ke = P.it.key_off[e];
+  const uint64_t vs = P.it.val_off[s], ve = P.it.val_off[e];
+  uint32_t flags = 0;
+  if (bad) {
+    flags = kPlanBad;
+    P.status[b] = ST_BAD_ARG;
+  } else if (!group_fits(n, ke - ks, ve - vs, total, hash_w)) {
+    const uint64_t need = e2_need(total, hash_w);
+    flags = need <= kImgMedium ? kPlanMedium : need <= kImgBig ? kPlanBig : kPlanHuge;
+  }
+  P.plans[b] = BlockPlan{(uint32_t)recs, bin_len, hash_w, step | (flags << 8)};
+  P.sizes[b] = (bad ? 0 : total) | ((flags & (kPlanMedium | kPlanBig | kPlanHuge)) ? kListedOne : 0);
+  P.kspan[b] = ks;
+  P.vspan[b] = vs;
+  if (b + 1 == P.n_blocks) {
+    P.kspan[b + 1] = ke;
+    P.vspan[b + 1] = ve;
+  }
+}
+
 // ------------------------------------------------ E2: group write kernel
 // One 4-wave workgroup owns kGRun consecutive blocks and writes them in
 // GROUPS: the longest run of consecutive group-class blocks whose items,
@@ -1710,7 +1936,11 @@ hipError_t launch_encode(const lsm_items& items, const uint32_t* starts, uint32_
   if (P.type == 1)
     hipLaunchKernelGGL(encode_plan_kernel<true>, pgrid, dim3(256), 0, st, P);
   else
+#ifdef LSM_PLAN_V1
     hipLaunchKernelGGL(encode_plan_kernel<false>, pgrid, dim3(256), 0, st, P);
+#else
+    hipLaunchKernelGGL(encode_plan_wave_kernel, pgrid, dim3(256), 0, st, P);
+#endif
   if ((e = launch_excl_scan(P.sizes, n_blocks, tiles,
                             EncodeOffOut{block_off, P.sizes, P.lists, P.list_count, n_blocks}, st)) != hipSuccess)
     return e;

@@ -18,7 +18,8 @@ import torch  # noqa: E402
 import bench  # noqa: E402
 import lsmgpu  # noqa: E402
 
-VARIANTS = [("full", 0), ("no-parse", 0x200), ("stage-only", 0x700), ("no-hash", 0x100), ("phaseA-only", 0x800)]
+VARIANTS = [("full", 0), ("no-parse", 0x200), ("stage-only", 0x700), ("no-hash", 0x100), ("phaseA-only", 0x800),
+            ("stage-no-header", 0x1700), ("no-header-no-dma", 0x3700)]
 
 
 def main():
