@@ -704,6 +704,29 @@ __device__ __forceinline__ Win16 gwin16(const uint8_t* p) {
   return r;
 }
 
+// gwin16 that skips the second 16-B load when p is 16-byte aligned
+__device__ __forceinline__ Win16 gwin16a(const uint8_t* p) {
+  const uint64_t a = (uint64_t)(uintptr_t)p;
+  const u32x4* w = reinterpret_cast<const u32x4*>(a & ~15ULL);
+  const uint32_t s = (uint32_t)(a & 15);
+  const u32x4 x = w[0];
+  u32x4 y = {0, 0, 0, 0};
+  if (s) y = w[1];
+  uint64_t w0 = (uint64_t)x.x | ((uint64_t)x.y << 32), w1 = (uint64_t)x.z | ((uint64_t)x.w << 32);
+  uint64_t w2 = (uint64_t)y.x | ((uint64_t)y.y << 32);
+  const uint64_t w3 = (uint64_t)y.z | ((uint64_t)y.w << 32);
+  if (s & 8) {
+    w0 = w1;
+    w1 = w2;
+    w2 = w3;
+  }
+  const uint32_t sh = (s & 7) * 8;
+  Win16 r;
+  r.lo = sh ? (w0 >> sh) | (w1 << (64 - sh)) : w0;
+  r.hi = sh ? (w1 >> sh) | (w2 << (64 - sh)) : w1;
+  return r;
+}
+
 // Shared prefix past an equal first 16 bytes: 16 bytes per step (rare: long
 // common key prefixes; kept narrow so the common path's registers stay low).
 #ifdef LSM_LCP_INLINE
@@ -915,12 +938,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LSM_PLAN_WP
 // offset from the step's LDS copy, or for a head before the step from the
 // carried last head; and the next step's item fields are loaded while this
 // step's key windows are in flight.
-constexpr uint32_t kPWStep = 2 * kWave;
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void encode_plan_wave_kernel(EncodeParams P) {
+#ifndef LSM_PW_PER
+#define LSM_PW_PER 2
+#endif
+constexpr uint32_t kPW = LSM_PW_PER;  // consecutive items per lane
+constexpr uint32_t kPWStep = kPW * kWave;
+#ifndef LSM_PW_WPE
+#define LSM_PW_WPE 4
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LSM_PW_WPE))) void encode_plan_wave_kernel(EncodeParams P) {
   __shared__ uint32_t bst[kPlanBlocks + 1];
   __shared__ unsigned long long bfirst[kPlanBlocks], bend[kPlanBlocks], lhead[kPlanBlocks];
   __shared__ unsigned long long kos[4][kPWStep];
   __shared__ uint32_t kls[4][kPWStep];
+  __shared__ Win16 kwin[4][kPWStep];  // each item's first 16 key bytes
   __shared__ uint32_t badf[kPlanBlocks];
   __shared__ uint32_t wcut[5];
   __shared__ uint32_t mono;
@@ -954,39 +985,41 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
   const uint32_t ie = __builtin_amdgcn_readfirstlane(bst[jhi]);
   unsigned long long* wkos = kos[wave];
   uint32_t* wkls = kls[wave];
+  Win16* wkwin = kwin[wave];
   // a lane's two consecutive items: key / value offsets [t, t + 3), seqnos and types [t, t + 2)
   struct StepRaw {
-    uint64_t ko[3], vo[3], seq[2];
-    uint32_t vt[2];
+    uint64_t ko[kPW + 1], vo[kPW + 1], seq[kPW];
+    uint32_t vt[kPW];
   };
   auto load_step = [&](uint32_t base, StepRaw& r) {
     // (items past the run are clamped to its last one and ignored; offsets index up to ie)
-    const uint32_t n = ie - base, t = min(2 * lane, n - 1), t1 = min(t + 1, n - 1);
+    const uint32_t n = ie - base, t = min(kPW * lane, n - 1);
     auto at64 = [&](const uint64_t* a, uint32_t k) {
       return *reinterpret_cast<const uint64_t*>(reinterpret_cast<const uint8_t*>(a + base) + 8u * k);
     };
-    r.ko[0] = at64(P.it.key_off, t);
-    r.ko[1] = at64(P.it.key_off, t + 1);
-    r.ko[2] = at64(P.it.key_off, min(t + 2, n));
-    r.vo[0] = at64(P.it.val_off, t);
-    r.vo[1] = at64(P.it.val_off, t + 1);
-    r.vo[2] = at64(P.it.val_off, min(t + 2, n));
-    r.seq[0] = at64(P.it.seqno, t);
-    r.seq[1] = at64(P.it.seqno, t1);
-    r.vt[0] = (P.it.vtype + base)[t];
-    r.vt[1] = (P.it.vtype + base)[t1];
+#pragma unroll
+    for (uint32_t q = 0; q <= kPW; ++q) {
+      r.ko[q] = at64(P.it.key_off, min(t + q, n));
+      r.vo[q] = at64(P.it.val_off, min(t + q, n));
+    }
+#pragma unroll
+    for (uint32_t q = 0; q < kPW; ++q) {
+      r.seq[q] = at64(P.it.seqno, min(t + q, n - 1));
+      r.vt[q] = (P.it.vtype + base)[min(t + q, n - 1)];
+    }
   };
   StepRaw raw, nxt;
   if (ia < ie) load_step(ia, raw);
   uint64_t carry = 0;     // record bytes of this wave's items before the step
   uint64_t hk_ko = 0;     // the last restart head of the previous step: key offset, key length
   uint32_t hk_kl = 0;
+  Win16 hk_win{0, 0};
   for (uint32_t base = ia; base < ie; base += kPWStep) {
     if (base + kPWStep < ie) load_step(base + kPWStep, nxt);  // in flight under this step
-    const uint32_t t0 = 2 * lane;
-    ItemMeta m[2];
-    uint32_t jq[2], jjq[2];
-    bool ok[2];
+    const uint32_t t0 = kPW * lane;
+    ItemMeta m[kPW];
+    uint32_t jq[kPW], jjq[kPW];
+    bool ok[kPW];
     uint32_t j = jlo;
     {
       uint32_t lo = jlo, hi = jhi;  // block j: bst[j] <= base + t0 < bst[j + 1]
@@ -999,7 +1032,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
       j = lo;
     }
 #pragma unroll
-    for (uint32_t q = 0; q < 2; ++q) {
+    for (uint32_t q = 0; q < kPW; ++q) {
       const uint32_t i = base + t0 + q;
       ok[q] = i < ie;
       while (j + 1 < jhi && bst[j + 1] <= i) ++j;
@@ -1019,15 +1052,21 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
       wkos[t0 + q] = m[q].ko;
       wkls[t0 + q] = m[q].klen;
     }
-    wave_lds_sync();
-    // ---- shared prefix with the restart head: both keys' first 16 bytes in flight together
-    Win16 wa[2], wb[2];
-    uint32_t nq[2];
-    uint64_t hq[2];
+    // ---- shared prefix with the restart head: every item loads its own first 16
+    // key bytes once; the others of its interval read the head's from LDS
+    Win16 wa[kPW], wb[kPW];
 #pragma unroll
-    for (uint32_t q = 0; q < 2; ++q) {
+    for (uint32_t q = 0; q < kPW; ++q) wb[q] = gwin16a(P.it.keys + m[q].ko);
+#pragma unroll
+    for (uint32_t q = 0; q < kPW; ++q) wkwin[t0 + q] = wb[q];
+    wave_lds_sync();
+    uint32_t nq[kPW];
+    uint64_t hq[kPW];
+#pragma unroll
+    for (uint32_t q = 0; q < kPW; ++q) {
       nq[q] = 0;
       hq[q] = 0;
+      wa[q] = wb[q];
       if (ok[q] && jjq[q] % ri != 0) {
         const uint32_t h = base + t0 + q - jjq[q] % ri;
         const bool in = h >= base;
@@ -1035,12 +1074,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
         const uint32_t hkl = in ? wkls[h - base] : hk_kl;
         nq[q] = min(hkl, m[q].klen);
         hq[q] = hko;
-        wa[q] = gwin16(P.it.keys + hko);
-        wb[q] = gwin16(P.it.keys + m[q].ko);
+        wa[q] = in ? wkwin[h - base] : hk_win;
       }
     }
 #pragma unroll
-    for (uint32_t q = 0; q < 2; ++q) {
+    for (uint32_t q = 0; q < kPW; ++q) {
       if (!nq[q]) continue;
       const uint64_t x0 = wa[q].lo ^ wb[q].lo, x1 = wa[q].hi ^ wb[q].hi;
       const uint32_t n = nq[q];
@@ -1051,15 +1089,17 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
       m[q].sh = sh;
     }
     // ---- record lengths, wave scan (a block never spans two waves)
-    uint64_t rec[2];
+    uint64_t rec[kPW], tsum = 0;
 #pragma unroll
-    for (uint32_t q = 0; q < 2; ++q) rec[q] = ok[q] ? item_record_len(P, m[q], jjq[q] % ri == 0) : 0;
-    const uint64_t tsum = rec[0] + rec[1];
+    for (uint32_t q = 0; q < kPW; ++q) {
+      rec[q] = ok[q] ? item_record_len(P, m[q], jjq[q] % ri == 0) : 0;
+      tsum += rec[q];
+    }
     const uint64_t incl = wave_incl_scan_u64(tsum);
     uint64_t ex = carry + incl - tsum;
-    uint64_t exq[2];
+    uint64_t exq[kPW];
 #pragma unroll
-    for (uint32_t q = 0; q < 2; ++q) {
+    for (uint32_t q = 0; q < kPW; ++q) {
       exq[q] = ex;
       if (ok[q]) {
         const uint32_t jb = jq[q], jj = jjq[q], ridx = jj / ri;
@@ -1072,7 +1112,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
     }
     wave_lds_sync();
 #pragma unroll
-    for (uint32_t q = 0; q < 2; ++q) {
+    for (uint32_t q = 0; q < kPW; ++q) {
       if (ok[q]) {
         const uint32_t jj = jjq[q], ridx = jj / ri;
         const bool head = jj == ridx * ri;
@@ -1088,12 +1128,16 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
     }
     carry += wave_bcast_u64(incl, kWave - 1);
     {  // the restart head of the step's last item, for the next step's first items
-      const uint32_t last = min(ie, base + kPWStep) - 1, ll = (last - base) >> 1, lq = (last - base) & 1;
-      const uint32_t jjl = __builtin_amdgcn_readlane((int)(lq ? jjq[1] : jjq[0]), (int)ll);
+      const uint32_t last = min(ie, base + kPWStep) - 1, ll = (last - base) / kPW, lq = (last - base) % kPW;
+      uint32_t jsel = jjq[0];
+#pragma unroll
+      for (uint32_t q = 1; q < kPW; ++q) jsel = lq == q ? jjq[q] : jsel;
+      const uint32_t jjl = __builtin_amdgcn_readlane((int)jsel, (int)ll);
       const uint32_t h = last - jjl % ri;
       if (h >= base) {
         hk_ko = wkos[h - base];
         hk_kl = wkls[h - base];
+        hk_win = wkwin[h - base];
       }
     }
     wave_lds_sync();  // (the next step rewrites kos / kls)
