@@ -1512,6 +1512,10 @@ __global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(LSM_G
     m.sh = head ? 0u : m.e >> 16;
     // ---- item t: its record into the image (one thread per item, or for
     // groups of few items tpi threads per item splitting the value copy)
+    // Two writers on purpose: the split one (tsh > 0) also covers tsh = 0, but as
+    // the only writer it measured 0.6 % slower on configs[1] and 0.5 % on
+    // configs[3] (3.237 vs 3.218 ms, 3.131 vs 3.115 ms; profiles/r03_encode_experiments.txt).
+    // A fix in one must be made in both.
     if (tsh == 0) {
     if (live && !(kDiagBuild && (P.diag & 9))) {
       const GBlk& B = L.blk[j];
