@@ -1119,7 +1119,7 @@ def main():
     r_dec = roofline_entry("decode_blocks_kernel (item_start precomputed)", dec_alg, kdec_ms, ceil,
                            "decode_blocks_kernel", nb)
     r_dec["read_only_frac"] = round(total_bytes / (kdec_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
-    r_enc = roofline_entry("lsm_encode_blocks (encode_plan_kernel + scan + encode_group_kernel)", enc_alg, enc_ms,
+    r_enc = roofline_entry("lsm_encode_blocks (encode_plan_wave_kernel + scan + encode_group_kernel)", enc_alg, enc_ms,
                            ceil, "lsm_encode_blocks", nb)
     dominant = r_enc if enc_ms >= kdec_ms else r_dec
 

@@ -15,7 +15,7 @@ for P in "$P1" "$P2" "$P3"; do
   timeout -k 10 120 rocprofv3 --pmc $P --output-format csv -d $OUT/e$i -o pmc -- python3 scripts/prof_encode.py --reps 2 > $OUT/e$i.log 2>&1
   timeout -k 10 120 rocprofv3 --pmc $P --output-format csv -d $OUT/d$i -o pmc -- python3 scripts/prof_decode.py --variants full --reps 2 --blocks 1048576 > $OUT/d$i.log 2>&1
 done
-for k in encode_group_kernel encode_plan_kernel; do echo "== $k"; python3 scripts/pmc_kernel.py $OUT/ $k 1048576 | grep -v "^$"; done > $OUT/summary.txt
+for k in encode_group_kernel encode_plan; do echo "== $k"; python3 scripts/pmc_kernel.py $OUT/ $k 1048576 | grep -v "^$"; done > $OUT/summary.txt
 echo "== decode_blocks_kernel" >> $OUT/summary.txt
 for i in 1 2 3; do python3 scripts/pmc_kernel.py $OUT/d$i decode_blocks_kernel 1048576; done >> $OUT/summary.txt
 cat $OUT/summary.txt

@@ -57,7 +57,7 @@ def main():
                                          "FETCH_SIZE x2 (gfx950 wide-read correction); WRITE_SIZE raw (1-8 B/lane "
                                          "SoA stores, uncalibrated)")}
     if len(a) >= 8:
-        names = ["encode_plan_kernel", "scan_tile", "encode_group_kernel", "encode_write_list", "encode_large"]
+        names = ["encode_plan", "scan_tile", "encode_group_kernel", "encode_write_list", "encode_large"]
         f, n = per_dispatch(a[5], "FETCH_SIZE", names, True)
         w, _ = per_dispatch(a[6], "WRITE_SIZE", names, True)
         out["lsm_encode_blocks"] = entry("lsm_encode_blocks", f, w, n, dblocks, int(a[7]),
