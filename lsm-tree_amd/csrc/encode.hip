@@ -1983,12 +1983,14 @@ hipError_t launch_encode(const lsm_items& items, const uint32_t* starts, uint32_
   const dim3 pgrid((n_blocks + P.plan_bpw - 1) / P.plan_bpw);
   if (P.type == 1)
     hipLaunchKernelGGL(encode_plan_kernel<true>, pgrid, dim3(256), 0, st, P);
-  else
-#ifdef LSM_PLAN_V1
-    hipLaunchKernelGGL(encode_plan_kernel<false>, pgrid, dim3(256), 0, st, P);
-#else
+#ifndef LSM_PLAN_V1
+  // (the wave kernel gives each wave whole blocks: with a few blocks of many items
+  // per workgroup most waves would idle, so those batches keep the workgroup walk)
+  else if (P.plan_bpw >= 16)
     hipLaunchKernelGGL(encode_plan_wave_kernel, pgrid, dim3(256), 0, st, P);
 #endif
+  else
+    hipLaunchKernelGGL(encode_plan_kernel<false>, pgrid, dim3(256), 0, st, P);
   if ((e = launch_excl_scan(P.sizes, n_blocks, tiles,
                             EncodeOffOut{block_off, P.sizes, P.lists, P.list_count, n_blocks}, st)) != hipSuccess)
     return e;
