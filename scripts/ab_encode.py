@@ -26,7 +26,12 @@ def child(reps, which):
     res = {}
     shapes = {"c1": dict(n_blocks=1 << 20), "c3": dict(n_blocks=262144, items_per_block=56, key_len=40, val_len=256,
                                                       kind="prefix"),
-              "r1": dict(n_blocks=1 << 20, kind="random")}
+              "r1": dict(n_blocks=1 << 20, kind="random"),
+              # the configs[4] data-block classes (bench.C5_SEGMENTS, ~1.4 GB each)
+              "k16c": dict(n_blocks=97817, items_per_block=205), "k16r": dict(n_blocks=82754, items_per_block=205,
+                                                                           kind="random"),
+              "k64c": dict(n_blocks=24552, items_per_block=820), "k64r": dict(n_blocks=20682, items_per_block=820,
+                                                                           kind="random")}
     for name in which.split(","):
         items, starts, n = bench.make_workload(torch, lsmgpu, **shapes[name])
         nb = shapes[name]["n_blocks"]
