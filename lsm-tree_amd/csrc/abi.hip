@@ -93,7 +93,7 @@ static int decode_blocks_common(const uint8_t* d_blocks, const uint64_t* d_block
   P.stage_bytes = pick(tuning ? tuning->stage_bytes : 0, lsmgpu::kDefaultStageBytes);
   P.tile_items = pick(tuning ? tuning->tile_items : 0, lsmgpu::kDefaultTileItems);
   P.seqno_add = 0;
-  if (P.tile_items > 8192 || P.stage_bytes < 256 || P.stage_bytes > 65536 || P.blocks_per_wave > 63)
+  if (P.tile_items > 8192 || P.stage_bytes < 256 || P.stage_bytes > (lsmgpu::kDefaultStageBytes >= 65536 ? 131072u : 65536u) || P.blocks_per_wave > 63)
     return LSM_BAD_ARG;
   P.stage_bytes = (P.stage_bytes + 15) & ~15u;
   if (lsmgpu::decode_lds_bytes(P.stage_bytes, P.tile_items, P.blocks_per_wave) > 160 * 1024) return LSM_BAD_ARG;

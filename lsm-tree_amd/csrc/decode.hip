@@ -1048,6 +1048,8 @@ constexpr uint32_t kGroupWaves = LSM_DEC_WAVES;
 #endif
 constexpr int kPrioA = LSM_PRIO_A;  // s_setprio of the phase-A wave
 constexpr int kPrioH = LSM_PRIO_H;  // s_setprio of a wave hashing one whole block
+// 17-bit record descriptors for stages of 64 KiB and more (two 8-wave workgroups per CU)
+constexpr bool kDecWide = kDefaultStageBytes >= 65536;
 
 template <bool kAllFields, bool kCompact>
 __global__ __launch_bounds__(kGroupWaves * kWave) __attribute__((amdgpu_waves_per_eu(LSM_DEC_WPE))) void decode_blocks_kernel(DecodeParams P) {
@@ -1157,7 +1159,7 @@ __global__ __launch_bounds__(kGroupWaves * kWave) __attribute__((amdgpu_waves_pe
       const bool hash = !(kDiagBuild && (P.flags & kDiagSkipHash)) && !(P.flags & LSM_DECODE_PAYLOAD_VERIFIED);
       if (role < nA) {
         if (kPrioA) __builtin_amdgcn_s_setprio(kPrioA);  // the serial walk is the group's critical path
-        phase_a(stage, meta, owner, rec, role * kWave, nA * kWave, total, P.tile_items);
+        phase_a<kDecWide>(stage, meta, owner, rec, role * kWave, nA * kWave, total, P.tile_items);
         if (kPrioA) __builtin_amdgcn_s_setprio(0);
         DEC_ROLE(8);
       } else if (hash && k <= kGroupWaves - nA) {
@@ -1198,7 +1200,7 @@ __global__ __launch_bounds__(kGroupWaves * kWave) __attribute__((amdgpu_waves_pe
     DEC_PHASE(2);
     // ---- 4. phase B: thread = record; full parse + validation; coalesced stores
     if (!(kDiagBuild && (P.flags & (kDiagSkipParse | kDiagSkipPhaseB))))
-      phase_b<kAllFields, kCompact>(P, stage, meta, rec, G.n_items, G.g_item0, threadIdx.x, blockDim.x);
+      phase_b<kAllFields, kCompact, kDecWide>(P, stage, meta, rec, G.n_items, G.g_item0, threadIdx.x, blockDim.x);
     lds_barrier();
     DEC_PHASE(3);
     if (wave == 0) {
