@@ -149,7 +149,8 @@ def host_items(items, n):
     return pyoracle.Items(kb, ko, vb, vo, seq, vt, ho, hs)
 
 
-def check_encode_all(torch, items, starts, enc, nb, n_items, threads, restart_interval=16, block_type=0):
+def check_encode_all(torch, items, starts, enc, nb, n_items, threads, restart_interval=16, block_type=0,
+                     hash_ratio=0.0):
     """Every encoded block == the oracle's DataBlock::encode_into + Block::write_into
     of the same items (one memcmp over the whole batch).  Returns (ref_buf, ref_off)."""
     import numpy as np
@@ -158,7 +159,7 @@ def check_encode_all(torch, items, starts, enc, nb, n_items, threads, restart_in
     it = host_items(items, n_items)
     st = starts[:nb + 1].cpu().numpy().astype(np.uint32)
     ref_buf, ref_off = pyoracle.encode_blocks(it, st, restart_interval=restart_interval, block_type=block_type,
-                                              nthreads=threads)
+                                              hash_ratio=hash_ratio, nthreads=threads)
     got_off = enc["block_off"][:nb + 1].cpu().numpy().view(np.uint64)
     assert np.array_equal(got_off, ref_off), "block offsets differ from the oracle"
     got = enc["buf"][:int(ref_off[-1])].cpu().numpy()
@@ -473,6 +474,56 @@ def bench_large_blocks(torch, lsmgpu, threads, steps=5):
         torch.cuda.empty_cache()
     res["note"] = ("encode: plan workgroups of ~16 Ki items, then one 8-wave workgroup per block straight in HBM (encode_large_kernel: record per thread at its E1 offset, per-KiB XXH3 contributions on every wave, chain on one); decode: 4-wave workgroup per "
                    "block through a 72 KiB stage in 64 KiB chunks (XXH3 chain carried across chunks)")
+    return res
+
+
+def bench_hash_index(torch, lsmgpu, steps, threads, nb=1 << 20, ratio=1.33, n_queries=1 << 20, reps=5):
+    """The configs[1] batch with the data-block hash index (data_block_hash_ratio
+    1.33, src/config/mod.rs:286, hash_index/builder.rs:64-110): encode (the
+    bucket votes in encode_group_kernel<*, true>), decode, and point reads that
+    take the hash probe first.  Every block checked against the oracle."""
+    items, starts, n = make_workload(torch, lsmgpu, nb, seed=0x5EED0008)
+    enc_ctx = lsmgpu.Encoder()
+    enc = enc_ctx.encode(items, starts, nb, hash_ratio=ratio)
+    torch.cuda.synchronize()
+    total = int(enc["block_off"][nb].item())
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    e0.record()
+    for _ in range(steps):
+        enc_ctx.encode(items, starts, nb, hash_ratio=ratio, out=enc)
+    e1.record()
+    torch.cuda.synchronize()
+    enc_ms = e0.elapsed_time(e1) / steps
+    dec_ms, out = time_decode(torch, lsmgpu, enc["buf"], enc["block_off"], nb, n, steps)
+    ref_buf, ref_off = check_encode_all(torch, items, starts, enc, nb, n, threads, hash_ratio=ratio)
+    check_decode_all(out, ref_buf, ref_off, nb, threads)
+    del out, ref_buf
+    g = torch.Generator(device="cuda")
+    g.manual_seed(0x5EED0009)
+    qi = torch.randint(0, n, (n_queries,), dtype=torch.int64, device="cuda", generator=g)
+    qb = torch.div(qi, 52, rounding_mode="floor").to(torch.int32)
+    needles = torch.cat([items["keys"][:n * 16].view(n, 16)[qi].reshape(-1),
+                         torch.zeros(lsmgpu.LSM_INPUT_PADDING, dtype=torch.uint8, device="cuda")])
+    noff = torch.arange(n_queries + 1, dtype=torch.int64, device="cuda") * 16
+    snap = torch.full((n_queries,), (1 << 63) - 1, dtype=torch.int64, device="cuda")
+    pr = lsmgpu.point_read(enc["buf"], enc["block_off"], nb, qb, needles, noff, snap)
+    torch.cuda.synchronize()
+    assert int((pr["status"] != 0).sum().item()) == 0
+    assert bool((pr["item"].to(torch.int64) == qi - qb.to(torch.int64) * 52).all().item()), "point_read hits"
+    e0.record()
+    for _ in range(reps):
+        lsmgpu.point_read(enc["buf"], enc["block_off"], nb, qb, needles, noff, snap)
+    e1.record()
+    torch.cuda.synchronize()
+    pr_ms = e0.elapsed_time(e1) / reps
+    res = {"workload": f"configs[1] shape (1 M x 4 KiB, 16 B keys, 64 B values) with hash ratio {ratio}",
+           "blocks": nb, "bytes": total, "encode_ms": round(enc_ms, 4),
+           "encode_GiB_per_s": round(total / (enc_ms * 1e-3) / 2 ** 30, 3), "decode_ms": round(dec_ms, 4),
+           "decode_GiB_per_s": round(total / (dec_ms * 1e-3) / 2 ** 30, 3),
+           "point_read_ms": round(pr_ms, 4), "point_read_Mqueries_per_s": round(n_queries / pr_ms / 1e3, 1),
+           "oracle_checked_blocks": nb}
+    del items, enc
+    torch.cuda.empty_cache()
     return res
 
 
@@ -1148,6 +1199,7 @@ def main():
         extra["config5"] = bench_config5(torch, lsmgpu, max(3, args.steps // 4), rank, world, dist, red_dev, threads)
         if world == 1:
             extra["large_blocks"] = bench_large_blocks(torch, lsmgpu, threads)
+            extra["hash_index"] = bench_hash_index(torch, lsmgpu, max(3, args.steps // 4), threads)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu and ref_buf is not None:
