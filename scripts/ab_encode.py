@@ -27,6 +27,7 @@ def child(reps, which):
     shapes = {"c1": dict(n_blocks=1 << 20), "c3": dict(n_blocks=262144, items_per_block=56, key_len=40, val_len=256,
                                                       kind="prefix"),
               "r1": dict(n_blocks=1 << 20, kind="random"),
+              "h1": dict(n_blocks=1 << 20),  # configs[1] with the hash index (ratio 1.33, bench_hash_index)
               # the configs[4] data-block classes (bench.C5_SEGMENTS, ~1.4 GB each)
               "k16c": dict(n_blocks=97817, items_per_block=205), "k16r": dict(n_blocks=82754, items_per_block=205,
                                                                            kind="random"),
@@ -35,15 +36,16 @@ def child(reps, which):
     for name in which.split(","):
         items, starts, n = bench.make_workload(torch, lsmgpu, **shapes[name])
         nb = shapes[name]["n_blocks"]
+        hr = 1.33 if name == "h1" else 0.0
         enc_ctx = lsmgpu.Encoder()
-        enc = enc_ctx.encode(items, starts, nb)
+        enc = enc_ctx.encode(items, starts, nb, hash_ratio=hr)
         torch.cuda.synchronize()
         total = int(enc["block_off"][nb].item())
         bad = int((enc["status"][:nb] != 0).sum())
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for _ in range(reps):
-            enc_ctx.encode(items, starts, nb, out=enc)
+            enc_ctx.encode(items, starts, nb, hash_ratio=hr, out=enc)
         e1.record()
         torch.cuda.synchronize()
         ms = e0.elapsed_time(e1) / reps
