@@ -296,8 +296,9 @@ __device__ __forceinline__ void xxh3_128_short(uint32_t len, R8 rb, R64 r64, uin
   out_hi = 0 - xxh3_avalanche(hhi);
 }
 
+// XXH3-64 of 0..16 bytes (reads offsets < len only, r64 at offsets <= 8).
 template <class R8, class R64>
-__device__ __forceinline__ uint64_t xxh3_64_short(uint32_t len, R8 rb, R64 r64) {
+__device__ __forceinline__ uint64_t xxh3_64_le16(uint32_t len, R8 rb, R64 r64) {
   using S = Secret;
   if (len == 0) return xxh64_avalanche(S::u64(56) ^ S::u64(64));
   if (len <= 3) {
@@ -320,6 +321,26 @@ __device__ __forceinline__ uint64_t xxh3_64_short(uint32_t len, R8 rb, R64 r64) 
     uint64_t acc = len + bswap64(lo) + hi + mul_fold64(lo, hi);
     return xxh3_avalanche(acc);
   }
+  return 0;  // (len > 16: not this function's range)
+}
+// Readers over a 16-byte register window (the key's first 16 bytes).
+struct WinReader8 {
+  uint64_t lo, hi;
+  __device__ __forceinline__ uint32_t operator()(uint32_t o) const {
+    return (uint32_t)((o < 8 ? lo >> (8 * o) : hi >> (8 * (o - 8))) & 0xFF);
+  }
+};
+struct WinReader64 {  // o <= 8
+  uint64_t lo, hi;
+  __device__ __forceinline__ uint64_t operator()(uint32_t o) const {
+    return o == 0 ? lo : o >= 8 ? hi : (lo >> (8 * o)) | (hi << (64 - 8 * o));
+  }
+};
+
+template <class R8, class R64>
+__device__ __forceinline__ uint64_t xxh3_64_short(uint32_t len, R8 rb, R64 r64) {
+  using S = Secret;
+  if (len <= 16) return xxh3_64_le16(len, rb, r64);
   auto mix16 = [&](uint32_t io, int so) {
     return mul_fold64(r64(io) ^ S::u64(so), r64(io + 8) ^ S::u64(so + 8));
   };

@@ -123,6 +123,10 @@ struct EncodeParams {
   uint32_t* lists;      // [n_blocks]: the listed blocks in block order (from the size scan)
   uint32_t* list_count; // [1]
   uint32_t* erec;       // [n_items] E1 -> E2, see kErec*
+  uint16_t* hbucket;    // [n_items] E1 -> E2 (hash-index batches, when hb_valid): the key's bucket
+                        // in its block (kNoBucket for blocks of >= kNeedHash buckets, never group-class)
+  uint32_t hb_valid;
+  uint32_t* hb_fix;     // [1] set by E1 when it left keys of more than 16 bytes (kNeedHash)
   unsigned long long* phase;  // diagnostic builds: per-phase cycle totals [16]
 };
 
@@ -259,13 +263,17 @@ struct SpanCopy {
 struct ItemMeta {
   uint64_t ko, vo, seq;
   uint32_t klen, vl, vt, sh;
-  uint32_t e;  // E2 only: the plan's erec word
+  uint32_t e;   // E2 only: the plan's erec word
+  uint32_t hb;  // E2 only: the plan's hash bucket (kNoBucket: none)
 };
+constexpr uint32_t kNoBucket = 0xFFFF;
+
+constexpr uint32_t kNeedHash = 0xFFFE;  // E1 left this key (> 16 bytes) to encode_bucket_fixup_kernel
 
 // An item's fields exactly as loaded (E2's one-group-ahead prefetch).
 struct RawItem {
   uint64_t ko, ko1, vo, vo1, seq;
-  uint32_t vt, e;
+  uint32_t vt, e, hb;
 };
 
 // Plain loads of item i's fields (no arithmetic, so no wait is forced here).
@@ -276,6 +284,7 @@ __device__ __forceinline__ RawItem load_raw(const EncodeParams& P, uint64_t i) {
   r.ko1 = P.it.key_off[i + 1];
   r.seq = P.it.seqno[i];
   r.e = 0;
+  r.hb = kNoBucket;
   if (kIndex) {
     r.vo = P.it.handle_off[i];
     r.vo1 = P.it.handle_size[i];
@@ -300,6 +309,7 @@ __device__ __forceinline__ RawItem load_raw_rel(const EncodeParams& P, uint64_t 
   r.ko1 = at64(P.it.key_off, t + 1);
   r.seq = at64(P.it.seqno, t);
   r.e = 0;
+  r.hb = kNoBucket;
   if (kIndex) {
     r.vo = at64(P.it.handle_off, t);
     r.vo1 = (P.it.handle_size + base)[t];
@@ -326,6 +336,7 @@ __device__ __forceinline__ ItemMeta cook_item(const RawItem& r, bool& bad) {
   m.vt = r.vt;
   m.sh = 0;
   m.e = r.e;
+  m.hb = r.hb;
   if (kIndex) {
     m.vl = (uint32_t)r.vo1;
   } else {
@@ -1063,6 +1074,7 @@ constexpr uint32_t kPWStep = kPW * kWave;
 #ifndef LSM_PW_WPE
 #define LSM_PW_WPE 4
 #endif
+template <bool kBkt>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LSM_PW_WPE))) void encode_plan_wave_kernel(EncodeParams P) {
   __shared__ uint32_t bst[kPlanBlocks + 1];
   __shared__ unsigned long long bfirst[kPlanBlocks], bend[kPlanBlocks], lhead[kPlanBlocks];
@@ -1164,6 +1176,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LSM_PW_WPE)
       r.seq = raw.seq[q];
       r.vt = raw.vt[q];
       r.e = 0;
+      r.hb = kNoBucket;
       m[q] = cook_item<false>(r, bad);
       if (ok[q] && bad) atomicOr(&badf[j], 1u);
       wkos[t0 + q] = m[q].ko;
@@ -1176,6 +1189,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LSM_PW_WPE)
     for (uint32_t q = 0; q < kPW; ++q) wb[q] = gwin16a(P.it.keys + m[q].ko);
 #pragma unroll
     for (uint32_t q = 0; q < kPW; ++q) wkwin[t0 + q] = wb[q];
+    if (kBkt) {  // hash-index batches: each key's bucket in its block, for E2 (keys of <= 16
+                 // bytes from their window here, longer ones by encode_bucket_fixup_kernel)
+#pragma unroll
+      for (uint32_t q = 0; q < kPW; ++q) {
+        if (!ok[q]) continue;
+        const uint32_t n = bst[jq[q] + 1] - bst[jq[q]];
+        const uint32_t buckets = bucket_count(n, P.ratio);
+        const uint32_t hw = (buckets > 0 && (n + ri - 1) / ri <= kHashMaxPointers) ? buckets : 0;
+        uint32_t hb = kNoBucket;
+        if (hw && hw < kNeedHash) {  // (group-class blocks have at most kGHash buckets)
+          if (m[q].klen <= 16)
+            hb = (uint32_t)(xxh3_64_le16(m[q].klen, WinReader8{wb[q].lo, wb[q].hi},
+                                         WinReader64{wb[q].lo, wb[q].hi}) % hw);
+          else
+            hb = kNeedHash, P.hb_fix[0] = 1;
+        }
+        P.hbucket[(uint64_t)base + t0 + q] = (uint16_t)hb;
+      }
+    }
     wave_lds_sync();
     uint32_t nq[kPW];
     uint64_t hq[kPW];
@@ -1444,7 +1476,32 @@ __device__ __forceinline__ void group_barrier_lds() {
 // has hash indexes (hash ratio > 0).  Both are batch-wide, so the paths a
 // batch never takes are compiled out (their registers would spill the
 // common path: every scratch reload waits for all outstanding loads).
-template <bool kIndex, bool kHash>
+#ifndef LSM_NOVOTE
+#define LSM_NOVOTE 0
+#endif
+// The buckets of the keys E1 left (more than 16 bytes): a wave per block,
+// grid-stride; exits at once when E1 left none.
+__global__ __launch_bounds__(256) void encode_bucket_fixup_kernel(EncodeParams P) {
+  if (!P.hb_fix[0]) return;
+  const uint32_t lane = threadIdx.x & (kWave - 1);
+  const uint32_t w0 = (blockIdx.x * blockDim.x + threadIdx.x) / kWave, nw = gridDim.x * blockDim.x / kWave;
+  for (uint32_t b = w0; b < P.n_blocks; b += nw) {
+    const uint32_t s = P.starts[b], e = P.starts[b + 1];
+    if (e <= s) continue;
+    const uint32_t n = e - s, buckets = bucket_count(n, P.ratio);
+    const uint32_t hw = (buckets > 0 && (n + P.ri - 1) / P.ri <= kHashMaxPointers) ? buckets : 0;
+    if (!hw || hw >= kNeedHash) continue;
+    for (uint32_t i = s + lane; i < e; i += kWave) {
+      if (P.hbucket[i] != kNeedHash) continue;
+      const uint64_t ko = P.it.key_off[i];
+      const uint32_t klen = (uint32_t)(P.it.key_off[i + 1] - ko);
+      const uint64_t hv = xxh3_64_any(klen, BaseReader8{P.it.keys + ko, 0}, BaseReader64{P.it.keys + ko, 0});
+      P.hbucket[i] = (uint16_t)(hv % hw);
+    }
+  }
+}
+
+template <bool kIndex, bool kHash, bool kPlanBkt = false>
 __global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(LSM_G_WPE))) void encode_group_kernel(EncodeParams P) {
   __shared__ GroupLds L;
   typedef __attribute__((address_space(3))) void lds_void_t;
@@ -1542,6 +1599,7 @@ __global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(LSM_G
     const uint64_t i = (uint64_t)i0 + min(tid >> tpi_shift(n), n - 1);
     r = load_raw<kIndex>(P, i);
     r.e = P.erec[i];
+    if (kPlanBkt) r.hb = P.hbucket[i];
   };
   auto cook = [&](const RawItem& r) {
     bool bad = false;  // (vetted by the plan pass)
@@ -1664,10 +1722,12 @@ __global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(LSM_G
         const uint32_t bp = p0 + B.recs + 1 + (m.e >> 16) * B.step;
         for (uint32_t q = 0; q < B.step; ++q) L.img[bp + q] = (uint8_t)(roff >> (8 * q));
       }
-      if (kHash && B.hash_w) {
+      if (kHash && B.hash_w && !LSM_NOVOTE) {
         const uint32_t ridx = (tid - B.it0) / ri;
-        const uint64_t hv = xxh3_64_any(m.klen, BaseReader8{L.keys, kst}, BaseReader64{L.keys, kst});
-        const uint32_t bk = B.hash_base + (uint32_t)(hv % B.hash_w);
+        const uint32_t hb =
+            kPlanBkt ? m.hb
+                     : (uint32_t)(xxh3_64_any(m.klen, BaseReader8{L.keys, kst}, BaseReader64{L.keys, kst}) % B.hash_w);
+        const uint32_t bk = B.hash_base + hb;
         atomicMin(&hlo[bk], ridx);
         atomicMax(&hhi[bk], ridx);
       }
@@ -1712,10 +1772,12 @@ __global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(LSM_G
         const uint32_t bp = p0 + B.recs + 1 + (m.e >> 16) * B.step;
         for (uint32_t q = 0; q < B.step; ++q) L.img[bp + q] = (uint8_t)(roff >> (8 * q));
       }
-      if (kHash && B.hash_w && part == 0) {
+      if (kHash && B.hash_w && part == 0 && !LSM_NOVOTE) {
         const uint32_t ridx = (item - B.it0) / ri;
-        const uint64_t hv = xxh3_64_any(m.klen, BaseReader8{L.keys, kst}, BaseReader64{L.keys, kst});
-        const uint32_t bk = B.hash_base + (uint32_t)(hv % B.hash_w);
+        const uint32_t hb =
+            kPlanBkt ? m.hb
+                     : (uint32_t)(xxh3_64_any(m.klen, BaseReader8{L.keys, kst}, BaseReader64{L.keys, kst}) % B.hash_w);
+        const uint32_t bk = B.hash_base + hb;
         atomicMin(&hlo[bk], ridx);
         atomicMax(&hhi[bk], ridx);
       }
@@ -2067,7 +2129,7 @@ static uint32_t plan_blocks_per_wg(uint64_t n_items, uint32_t n_blocks) {
 size_t encode_workspace_size(uint64_t n_items, uint32_t n_blocks) {
   return 2 * al256(((size_t)n_blocks + 1) * 8) + al256((size_t)n_blocks * 8) +
          al256((size_t)n_blocks * sizeof(BlockPlan)) + al256((size_t)n_blocks * 4) + 256 +
-         al256(scan_tiles(n_blocks) * 8) + al256((size_t)n_items * 4);
+         al256(scan_tiles(n_blocks) * 8) + al256((size_t)n_items * 4) + al256((size_t)n_items * 2) + 256;
 }
 
 uint64_t encode_bound(uint64_t n_items, uint32_t n_blocks, uint64_t key_bytes, uint64_t val_bytes,
@@ -2107,17 +2169,25 @@ hipError_t launch_encode(const lsm_items& items, const uint32_t* starts, uint32_
   P.lists = (uint32_t*)w; w += al256((size_t)n_blocks * 4);
   P.list_count = (uint32_t*)w; w += 256;
   uint64_t* tiles = (uint64_t*)w; w += al256(scan_tiles(n_blocks) * 8);
-  P.erec = (uint32_t*)w;
+  P.erec = (uint32_t*)w; w += al256((size_t)items.n_items * 4);
+  P.hbucket = (uint16_t*)w; w += al256((size_t)items.n_items * 2);
+  P.hb_fix = (uint32_t*)w;
   hipError_t e;
   P.plan_bpw = plan_blocks_per_wg(items.n_items, n_blocks);
+  P.hb_valid = 0;
   const dim3 pgrid((n_blocks + P.plan_bpw - 1) / P.plan_bpw);
   if (P.type == 1)
     hipLaunchKernelGGL(encode_plan_kernel<true>, pgrid, dim3(256), 0, st, P);
 #ifndef LSM_PLAN_V1
   // (the wave kernel gives each wave whole blocks: with a few blocks of many items
   // per workgroup most waves would idle, so those batches keep the workgroup walk)
-  else if (P.plan_bpw >= 16)
-    hipLaunchKernelGGL(encode_plan_wave_kernel, pgrid, dim3(256), 0, st, P);
+  else if (P.plan_bpw >= 16 && P.ratio > 0.0f) {  // (only this plan kernel fills hbucket)
+    P.hb_valid = 1;
+    if ((e = hipMemsetAsync(P.hb_fix, 0, 4, st)) != hipSuccess) return e;
+    hipLaunchKernelGGL(encode_plan_wave_kernel<true>, pgrid, dim3(256), 0, st, P);
+    hipLaunchKernelGGL(encode_bucket_fixup_kernel, dim3(1024), dim3(256), 0, st, P);
+  } else if (P.plan_bpw >= 16)
+    hipLaunchKernelGGL(encode_plan_wave_kernel<false>, pgrid, dim3(256), 0, st, P);
 #endif
   else
     hipLaunchKernelGGL(encode_plan_kernel<false>, pgrid, dim3(256), 0, st, P);
@@ -2129,6 +2199,8 @@ hipError_t launch_encode(const lsm_items& items, const uint32_t* starts, uint32_
   const dim3 ggrid((n_blocks + kGRun - 1) / kGRun), gblock(kGThreads);
   if (P.type == 1)
     hipLaunchKernelGGL((encode_group_kernel<true, false>), ggrid, gblock, 0, st, P);
+  else if (P.ratio > 0.0f && P.hb_valid)  // buckets from the plan pass
+    hipLaunchKernelGGL((encode_group_kernel<false, true, true>), ggrid, gblock, 0, st, P);
   else if (P.ratio > 0.0f)
     hipLaunchKernelGGL((encode_group_kernel<false, true>), ggrid, gblock, 0, st, P);
   else

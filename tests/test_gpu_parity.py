@@ -148,6 +148,25 @@ def test_encode_decode_random_batches(gpu, ri, ratio):
     compare_decode(g, parsed, item_start, status)
 
 
+def test_hash_index_key_lengths(gpu):
+    """Hash-index buckets of keys of 0..300 bytes: the plan pass hashes keys of
+    <= 16 bytes from their first 16 bytes and leaves longer ones (every XXH3
+    length class, up to the > 240-byte long path) to encode_bucket_fixup_kernel;
+    bit-exact against the oracle."""
+    for kmin, kmax, seed in ((1, 16, 11), (17, 300, 12), (1, 300, 13)):
+        items = random_sorted_items(2000, seed=seed, kmin=kmin, kmax=kmax, vmax=40)
+        rng = random.Random(seed)
+        starts = [0]
+        while starts[-1] < items.n:
+            starts.append(min(items.n, starts[-1] + rng.randint(8, 40)))
+        starts = np.array(starts, np.uint32)
+        ref_buf, ref_off = pyoracle.encode_blocks(items, starts, restart_interval=4, hash_ratio=1.33)
+        buf, off, st = _gpu_encode(gpu, items, starts, 4, 1.33, 0)
+        assert (st == 0).all()
+        assert (off == ref_off).all()
+        assert buf.tobytes() == ref_buf.tobytes(), (kmin, kmax)
+
+
 @pytest.mark.parametrize("ratio", [0.0, 1.33])
 def test_encode_size_classes(gpu, ratio):
     """Blocks in every encode class (LDS image <= 5 KiB, <= 20 KiB, <= 96 KiB,
