@@ -1486,9 +1486,9 @@ __global__ __launch_bounds__(256) void encode_bucket_fixup_kernel(EncodeParams P
   const uint32_t lane = threadIdx.x & (kWave - 1);
   const uint32_t w0 = (blockIdx.x * blockDim.x + threadIdx.x) / kWave, nw = gridDim.x * blockDim.x / kWave;
   for (uint32_t b = w0; b < P.n_blocks; b += nw) {
-    const uint32_t s = P.starts[b], e = P.starts[b + 1];
-    if (e <= s) continue;
-    const uint32_t n = e - s, buckets = bucket_count(n, P.ratio);
+    const uint32_t s = P.starts[b], e = (uint32_t)min((uint64_t)P.starts[b + 1], P.it.n_items);
+    if (e <= s) continue;  // (an empty or malformed block: E1 marked it bad, E2 skips it)
+    const uint32_t n = P.starts[b + 1] - s, buckets = bucket_count(n, P.ratio);
     const uint32_t hw = (buckets > 0 && (n + P.ri - 1) / P.ri <= kHashMaxPointers) ? buckets : 0;
     if (!hw || hw >= kNeedHash) continue;
     for (uint32_t i = s + lane; i < e; i += kWave) {
