@@ -27,6 +27,8 @@
  *   lsm_xxh3_128_file  <- ChecksummedWriter         src/checksum.rs:59-96 (whole-file checksum)
  *   lsm_xxh3_128_stream_{init,update,digest}
  *                      <- ChecksummedWriter::{new,write,checksum} src/checksum.rs:59-96 (streaming)
+ *   lsm_xxh3_128_stream_{init,update,digest}_batch
+ *                      <- the same for every table of a MultiWriter  src/table/multi_writer.rs:181-257
  *   lsm_lz4_decompress_blocks <- Block::from_reader/from_file, CompressionType::Lz4  block/mod.rs:87-182
  *   lsm_lz4_plan_output <- the builder_unzeroed(uncompressed_length) sizing of the same  block/mod.rs:104-112
  *   lsm_lz4_plan_framed / lsm_lz4_decompress_framed + lsm_decode_blocks_tuned(LSM_DECODE_PAYLOAD_VERIFIED)
@@ -50,7 +52,7 @@
 extern "C" {
 #endif
 
-#define LSM_ABI_VERSION 4
+#define LSM_ABI_VERSION 5
 #define LSM_HEADER_LEN 33  /* Header::serialized_len(), header.rs:64-76 */
 #define LSM_TRAILER_LEN 31 /* TRAILER_SIZE, trailer.rs:14-23 */
 /* d_blocks must be 16-byte aligned and readable for LSM_INPUT_PADDING bytes
@@ -184,7 +186,12 @@ int lsm_set_device(int device);
  * device u64, the BlockHandle offsets/sizes).  expect_type: block type every
  * block must have (util.rs:81-86), or -1 for any.  Writes d_item_start
  * (n_blocks+1 u32: prefix sum of the trailers' item counts, clamped at
- * item_cap), the parsed items, and d_status[n_blocks].
+ * item_cap), the parsed items, and d_status[n_blocks].  The rows
+ * [d_item_start[b], d_item_start[b+1]) of a block whose d_status is not LSM_OK
+ * are unspecified (blocks larger than the LDS stage are parsed chunk by chunk
+ * while their checksum is still being computed, so a block that then fails it
+ * may have rows written): as in the reference, where Block::from_file returns
+ * Err and no item is yielded, a caller uses no row of a failed block.
  * d_workspace: lsm_decode_workspace_size(n_blocks) bytes of device memory. */
 size_t lsm_decode_workspace_size(uint32_t n_blocks);
 int lsm_decode_blocks(const uint8_t* d_blocks, const uint64_t* d_block_off, uint32_t n_blocks,
@@ -266,6 +273,30 @@ int lsm_xxh3_128_stream_init(void* d_state, void* stream);
 int lsm_xxh3_128_stream_update(void* d_state, const uint8_t* d_data, uint64_t len, void* d_workspace,
                                size_t workspace_bytes, void* stream);
 int lsm_xxh3_128_stream_digest(const void* d_state, uint64_t* d_out, void* stream);
+/* The same for n running states at once (a flush or compaction that rotates
+ * through several tables, src/table/multi_writer.rs:181-257, each with its own
+ * ChecksummedWriter): d_states holds n states back to back (n *
+ * lsm_xxh3_128_stream_state_size() bytes, 16-byte aligned, caller-owned).
+ *   init_batch    ChecksummedWriter::new for every state;
+ *   update_batch  state i is fed d_data[d_off[i] .. d_off[i+1]) (d_off: n+1
+ *                 device u64, non-decreasing; empty ranges allowed; every
+ *                 state at most once per call; the arena readable 16 bytes
+ *                 past each range) in one launch sequence: the per-KiB
+ *                 contributions of every state across the GPU, then 8 scramble
+ *                 chains per state side by side.  total_len >= d_off[n] - d_off[0]
+ *                 sizes the workspace (lsm_xxh3_128_stream_batch_workspace_size(n,
+ *                 total_len) bytes, 16-byte aligned).  d_status[i] (device i32):
+ *                 LSM_OK, or LSM_BAD_ARG for a state that was never initialised or
+ *                 a decreasing range (that state is left unchanged); if the ranges
+ *                 hold more bytes than total_len every state is LSM_BAD_ARG and
+ *                 none is changed;
+ *   digest_batch  d_out[2i], d_out[2i+1] = digest of state i (low, high). */
+int lsm_xxh3_128_stream_init_batch(void* d_states, uint32_t n, void* stream);
+size_t lsm_xxh3_128_stream_batch_workspace_size(uint32_t n, uint64_t total_len);
+int lsm_xxh3_128_stream_update_batch(void* d_states, uint32_t n, const uint8_t* d_data, const uint64_t* d_off,
+                                     uint64_t total_len, int32_t* d_status, void* d_workspace,
+                                     size_t workspace_bytes, void* stream);
+int lsm_xxh3_128_stream_digest_batch(const void* d_states, uint32_t n, uint64_t* d_out, void* stream);
 
 /* ---- point read -----------------------------------------------------------
  * Batched DataBlock::point_read(needle, snapshot_seqno) (data_block/mod.rs:412-472),

@@ -132,6 +132,18 @@ struct EncodeParams {
 
 __device__ __forceinline__ bool is_index(const EncodeParams& P) { return P.type == 1; }
 
+// d_block_item_start[i] as E1 walks it: clamped to n_items, so no item field
+// past the arenas is read (the reference takes &[InternalValue],
+// data_block/mod.rs:523-549, so its block ranges are in bounds by type; the
+// C ABI checks).  A block whose end is past n_items is rejected (ST_BAD_ARG).
+__device__ __forceinline__ uint32_t clamped_start(const EncodeParams& P, uint32_t i) {
+  const uint32_t v = P.starts[i];
+  return (uint64_t)v > P.it.n_items ? (uint32_t)P.it.n_items : v;
+}
+__device__ __forceinline__ bool start_past_items(const EncodeParams& P, uint32_t i) {
+  return (uint64_t)P.starts[i] > P.it.n_items;
+}
+
 // LDS a block's image needs in E2: worst-case 16-B pad + the block + 32 B of
 // read slack for the window reads, then the hash-index vote arrays.
 __device__ __forceinline__ uint64_t e2_need(uint64_t total, uint32_t hash_w) {
@@ -886,7 +898,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LSM_PLAN_WP
   const uint32_t tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid / kWave;
   const uint32_t b0 = blockIdx.x * P.plan_bpw;
   const uint32_t nb = min(P.plan_bpw, P.n_blocks - b0);
-  if (tid <= nb) bst[tid] = P.starts[b0 + tid];
+  if (tid <= nb) bst[tid] = clamped_start(P, b0 + tid);
   if (tid < nb) {
     bfirst[tid] = bend[tid] = lhead[tid] = 0;
     badf[tid] = 0;
@@ -1026,7 +1038,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LSM_PLAN_WP
   __syncthreads();
   if (tid >= nb) return;
   const uint32_t b = b0 + tid, s = bst[tid], e = bst[tid + 1];
-  bool bad = !mono || e <= s || badf[tid];
+  bool bad = !mono || e <= s || badf[tid] || start_past_items(P, b + 1);
   const uint32_t n = bad ? 0 : e - s;
   const uint64_t recs = bad ? 0 : bend[tid] - bfirst[tid], last_head = bad ? 0 : lhead[tid] - bfirst[tid];
   const uint32_t bin_len = n ? (n + ri - 1) / ri : 0;
@@ -1088,7 +1100,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LSM_PW_WPE)
   const uint32_t wave = __builtin_amdgcn_readfirstlane(tid / kWave);
   const uint32_t b0 = blockIdx.x * P.plan_bpw;
   const uint32_t nb = min(P.plan_bpw, P.n_blocks - b0);
-  if (tid <= nb) bst[tid] = P.starts[b0 + tid];
+  if (tid <= nb) bst[tid] = clamped_start(P, b0 + tid);
   if (tid < nb) {
     bfirst[tid] = bend[tid] = lhead[tid] = 0;
     badf[tid] = 0;
@@ -1295,7 +1307,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LSM_PW_WPE)
   __syncthreads();
   if (tid >= nb) return;
   const uint32_t b = b0 + tid, s = bst[tid], e = bst[tid + 1];
-  bool bad = !mono || e <= s || badf[tid];
+  bool bad = !mono || e <= s || badf[tid] || start_past_items(P, b + 1);
   const uint32_t n = bad ? 0 : e - s;
   const uint64_t recs = bad ? 0 : bend[tid] - bfirst[tid], last_head = bad ? 0 : lhead[tid] - bfirst[tid];
   const uint32_t bin_len = n ? (n + ri - 1) / ri : 0;
@@ -1486,15 +1498,18 @@ __global__ __launch_bounds__(256) void encode_bucket_fixup_kernel(EncodeParams P
   const uint32_t lane = threadIdx.x & (kWave - 1);
   const uint32_t w0 = (blockIdx.x * blockDim.x + threadIdx.x) / kWave, nw = gridDim.x * blockDim.x / kWave;
   for (uint32_t b = w0; b < P.n_blocks; b += nw) {
-    const uint32_t s = P.starts[b], e = (uint32_t)min((uint64_t)P.starts[b + 1], P.it.n_items);
-    if (e <= s) continue;  // (an empty or malformed block: E1 marked it bad, E2 skips it)
-    const uint32_t n = P.starts[b + 1] - s, buckets = bucket_count(n, P.ratio);
+    // blocks E1 rejected (non-monotone or out-of-range starts, over-long keys,
+    // bad value types) are skipped by E2: their hbucket entries may be stale
+    if ((P.plans[b].step_flags >> 8) & kPlanBad) continue;
+    const uint32_t s = P.starts[b], e = P.starts[b + 1];  // (E1 checked s < e <= n_items)
+    const uint32_t n = e - s, buckets = bucket_count(n, P.ratio);
     const uint32_t hw = (buckets > 0 && (n + P.ri - 1) / P.ri <= kHashMaxPointers) ? buckets : 0;
     if (!hw || hw >= kNeedHash) continue;
     for (uint32_t i = s + lane; i < e; i += kWave) {
       if (P.hbucket[i] != kNeedHash) continue;
       const uint64_t ko = P.it.key_off[i];
-      const uint32_t klen = (uint32_t)(P.it.key_off[i + 1] - ko);
+      // (E1 checked every key of a good block: <= 0xFFFF bytes; the cap is the same as E1's)
+      const uint32_t klen = (uint32_t)min(P.it.key_off[i + 1] - ko, (uint64_t)0xFFFF);
       const uint64_t hv = xxh3_64_any(klen, BaseReader8{P.it.keys + ko, 0}, BaseReader64{P.it.keys + ko, 0});
       P.hbucket[i] = (uint16_t)(hv % hw);
     }

@@ -61,7 +61,7 @@ class LsmTableScan(C.Structure):
                 ("global_seqno", C.c_uint64), ("block_count", C.c_uint64)]
 
 
-ABI_VERSION = 4
+ABI_VERSION = 5
 DECODE_ITEM_START_VALID = 1
 DECODE_PAYLOAD_VERIFIED = 2
 
@@ -131,6 +131,15 @@ def lib():
                                                  C.c_void_p]
         L.lsm_xxh3_128_stream_digest.restype = C.c_int
         L.lsm_xxh3_128_stream_digest.argtypes = [C.c_void_p, C.c_void_p, C.c_void_p]
+        L.lsm_xxh3_128_stream_init_batch.restype = C.c_int
+        L.lsm_xxh3_128_stream_init_batch.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p]
+        L.lsm_xxh3_128_stream_batch_workspace_size.restype = C.c_size_t
+        L.lsm_xxh3_128_stream_batch_workspace_size.argtypes = [C.c_uint32, C.c_uint64]
+        L.lsm_xxh3_128_stream_update_batch.restype = C.c_int
+        L.lsm_xxh3_128_stream_update_batch.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_uint64,
+                                                       C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]
+        L.lsm_xxh3_128_stream_digest_batch.restype = C.c_int
+        L.lsm_xxh3_128_stream_digest_batch.argtypes = [C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p]
         L.lsm_point_read_blocks.restype = C.c_int
         L.lsm_point_read_blocks.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p, C.c_void_p,
                                             C.c_void_p, C.c_uint32, C.POINTER(LsmPointResult), C.c_void_p,
@@ -197,7 +206,9 @@ EXPORTED_SYMBOLS = ["lsm_abi_version", "lsm_status_name", "lsm_last_error", "lsm
                     "lsm_lz4_decompress_framed", "lsm_scan_workspace_size", "lsm_scan_table",
                     "lsm_materialize_workspace_size", "lsm_materialize_plan", "lsm_materialize_keys",
                     "lsm_xxh3_128_stream_state_size", "lsm_xxh3_128_stream_workspace_size",
-                    "lsm_xxh3_128_stream_init", "lsm_xxh3_128_stream_update", "lsm_xxh3_128_stream_digest"]
+                    "lsm_xxh3_128_stream_init", "lsm_xxh3_128_stream_update", "lsm_xxh3_128_stream_digest",
+                    "lsm_xxh3_128_stream_init_batch", "lsm_xxh3_128_stream_batch_workspace_size",
+                    "lsm_xxh3_128_stream_update_batch", "lsm_xxh3_128_stream_digest_batch"]
 
 
 def _check(rc, what):
@@ -430,24 +441,37 @@ class ChecksummedWriter:
     the next bytes (ChecksummedWriter::write, checksum.rs:92-95),
     checksum() is Xxh3Default::digest128 of everything written so far, as
     (low, high) Python ints (synchronises; the state is kept, writes may go on).
-    Any split of the file into writes gives the one-shot xxh3_128."""
+    Any split of the file into writes gives the one-shot xxh3_128.
+
+    Every call runs on one stream, fixed at construction (`stream`, else the
+    stream current then).  write() first makes that stream wait for the
+    caller's current stream (where `data` was produced); checksum() waits for
+    the digest on that stream before reading it back."""
 
     def __init__(self, device=None, stream=None):
         torch = _torch()
         self.device = torch.device("cuda") if device is None else torch.device(device)
-        self.stream = stream
-        self.state = torch.empty(lib().lsm_xxh3_128_stream_state_size(), dtype=torch.uint8, device=self.device)
-        self._ws = torch.empty(0, dtype=torch.uint8, device=self.device)
+        self.stream = stream if stream is not None else torch.cuda.current_stream(self.device)
+        with torch.cuda.stream(self.stream):
+            self.state = torch.empty(lib().lsm_xxh3_128_stream_state_size(), dtype=torch.uint8, device=self.device)
+            self._ws = torch.empty(0, dtype=torch.uint8, device=self.device)
         self.bytes_written = 0
-        _check(lib().lsm_xxh3_128_stream_init(_ptr(self.state), _stream(stream)), "lsm_xxh3_128_stream_init")
+        _check(lib().lsm_xxh3_128_stream_init(_ptr(self.state), _stream(self.stream)), "lsm_xxh3_128_stream_init")
 
     def write(self, data, length=None, offset=0):
         """Feed data[offset .. offset + length) (uint8 cuda tensor, readable 16 B past the end)."""
         torch = _torch()
         length = data.numel() - offset if length is None else length
+        cur = torch.cuda.current_stream(self.device)
+        if cur != self.stream:
+            self.stream.wait_stream(cur)           # data may still be being written on the caller's stream
+            data.record_stream(self.stream)        # and must outlive the update queued below
         need = lib().lsm_xxh3_128_stream_workspace_size(length)
         if self._ws.numel() < need:
-            self._ws = torch.empty(need, dtype=torch.uint8, device=self.device)
+            # (allocated and freed on self.stream: the caching allocator reuses the old
+            # workspace only for work queued after the updates that read it)
+            with torch.cuda.stream(self.stream):
+                self._ws = torch.empty(need, dtype=torch.uint8, device=self.device)
         _check(lib().lsm_xxh3_128_stream_update(_ptr(self.state), C.c_void_p(data.data_ptr() + offset), length,
                                                 _ptr(self._ws), self._ws.numel(), _stream(self.stream)),
                "lsm_xxh3_128_stream_update")
@@ -456,11 +480,65 @@ class ChecksummedWriter:
 
     def checksum(self):
         torch = _torch()
-        out = torch.zeros(2, dtype=torch.int64, device=self.device)
+        with torch.cuda.stream(self.stream):
+            out = torch.zeros(2, dtype=torch.int64, device=self.device)
         _check(lib().lsm_xxh3_128_stream_digest(_ptr(self.state), _ptr(out), _stream(self.stream)),
                "lsm_xxh3_128_stream_digest")
+        self.stream.synchronize()
         lo, hi = (int(x) & (2 ** 64 - 1) for x in out.cpu().tolist())
         return lo, hi
+
+
+class ChecksummedWriterSet:
+    """n running whole-file checksums advanced together: one ChecksummedWriter
+    (src/checksum.rs:59-96) per table of a flush or compaction that rotates
+    through several tables (MultiWriter, src/table/multi_writer.rs:181-257).
+    write(data, off) feeds state i the bytes data[off[i] .. off[i+1]) for every
+    i in one launch sequence (lsm_xxh3_128_stream_update_batch); checksums()
+    returns every digest as (low, high) pairs.  Same stream rules as
+    ChecksummedWriter."""
+
+    def __init__(self, n, device=None, stream=None):
+        torch = _torch()
+        self.n = n
+        self.device = torch.device("cuda") if device is None else torch.device(device)
+        self.stream = stream if stream is not None else torch.cuda.current_stream(self.device)
+        size = lib().lsm_xxh3_128_stream_state_size()
+        with torch.cuda.stream(self.stream):
+            self.states = torch.empty(max(n, 1) * size, dtype=torch.uint8, device=self.device)
+            self.status = torch.zeros(max(n, 1), dtype=torch.int32, device=self.device)
+            self._ws = torch.empty(0, dtype=torch.uint8, device=self.device)
+        _check(lib().lsm_xxh3_128_stream_init_batch(_ptr(self.states), n, _stream(self.stream)),
+               "lsm_xxh3_128_stream_init_batch")
+
+    def write(self, data, off, total_len=None):
+        """data: uint8 cuda tensor (readable 16 B past each range); off: int64 cuda
+        tensor [n+1]; total_len >= off[n] - off[0] (default: data.numel())."""
+        torch = _torch()
+        total_len = data.numel() if total_len is None else total_len
+        cur = torch.cuda.current_stream(self.device)
+        if cur != self.stream:
+            self.stream.wait_stream(cur)
+            data.record_stream(self.stream)
+            off.record_stream(self.stream)
+        need = lib().lsm_xxh3_128_stream_batch_workspace_size(self.n, total_len)
+        if self._ws.numel() < need:
+            with torch.cuda.stream(self.stream):
+                self._ws = torch.empty(need, dtype=torch.uint8, device=self.device)
+        _check(lib().lsm_xxh3_128_stream_update_batch(_ptr(self.states), self.n, _ptr(data), _ptr(off), total_len,
+                                                      _ptr(self.status), _ptr(self._ws), self._ws.numel(),
+                                                      _stream(self.stream)), "lsm_xxh3_128_stream_update_batch")
+        return self.status
+
+    def checksums(self):
+        torch = _torch()
+        with torch.cuda.stream(self.stream):
+            out = torch.zeros(2 * max(self.n, 1), dtype=torch.int64, device=self.device)
+        _check(lib().lsm_xxh3_128_stream_digest_batch(_ptr(self.states), self.n, _ptr(out), _stream(self.stream)),
+               "lsm_xxh3_128_stream_digest_batch")
+        self.stream.synchronize()
+        v = [int(x) & (2 ** 64 - 1) for x in out.cpu().tolist()]
+        return [(v[2 * i], v[2 * i + 1]) for i in range(self.n)]
 
 
 BLOOM_BITS_PER_KEY, BLOOM_FP_RATE, BLOOM_BAD_FILTER = 0, 1, 0xFF

@@ -52,7 +52,7 @@ def test_library_exports_exactly_the_header(L):
 
 def test_abi_version_and_status_names(L):
     lib = L.lib()
-    assert lib.lsm_abi_version() == L.ABI_VERSION == 4
+    assert lib.lsm_abi_version() == L.ABI_VERSION == 5
     for code, name in L.STATUS.items():
         assert lib.lsm_status_name(code).decode() == name
 
@@ -118,8 +118,9 @@ def test_bad_args_rejected_without_device(L):
 
 
 def test_decode_tuning_flags_rejected(L):
-    """Only LSM_DECODE_ITEM_START_VALID is a public decode flag: diagnostic bits
-    that would skip the hash, the parse or the stores are LSM_BAD_ARG."""
+    """Only LSM_DECODE_ITEM_START_VALID and LSM_DECODE_PAYLOAD_VERIFIED are public
+    decode flags: diagnostic bits that would skip the hash, the parse or the
+    stores are LSM_BAD_ARG."""
     import ctypes as C
     lib = L.lib()
     ps = L.LsmParsed()

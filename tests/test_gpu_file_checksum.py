@@ -95,3 +95,75 @@ def test_stream_checksum_sst_writer_order(gpu, oracle):
     whole = np.concatenate(pieces)
     assert (got[1] << 64) | got[0] == pyoracle.xxh3_128(whole.tobytes())
     assert w.bytes_written == len(whole)
+
+
+def _batch_round(torch, files, pos, cuts, pad=64):
+    """One update_batch round: state i gets files[i][pos[i] .. pos[i] + cuts[i])."""
+    parts, off = [], [0]
+    for f, p, c in zip(files, pos, cuts):
+        parts.append(f[p:p + c])
+        off.append(off[-1] + c)
+    arena = np.concatenate(parts + [np.zeros(pad, np.uint8)])
+    return torch.from_numpy(arena).cuda(), torch.tensor(off, dtype=torch.int64, device="cuda"), off[-1]
+
+
+def test_stream_batch_random_chunkings(gpu):
+    """64 running checksums advanced together (lsm_xxh3_128_stream_update_batch:
+    the ChecksummedWriter of every table of a MultiWriter, multi_writer.rs:181-257):
+    random per-state chunk sizes (empty, < 240 B, KiB-straddling, large) over 6
+    rounds; mid-stream digests after round 3 and final digests equal the oracle's
+    one-shot xxh3_128 of each file."""
+    import torch
+    rng = np.random.default_rng(99)
+    r = random.Random(99)
+    n = 64
+    sizes = [r.choice([0, 1, 239, 240, 241, 1023, 1024, 1025, r.randrange(1, 5000), r.randrange(1, 400000)])
+             for _ in range(n)]
+    files = [rng.integers(0, 256, s, dtype=np.uint8) for s in sizes]
+    ws = gpu.ChecksummedWriterSet(n)
+    pos = [0] * n
+    for rnd in range(6):
+        cuts = []
+        for i in range(n):
+            left = sizes[i] - pos[i]
+            c = left if rnd == 5 else min(left, r.choice([0, 1, 63, 1024, r.randrange(0, 3000), r.randrange(0, 1 << 17)]))
+            cuts.append(c)
+        d, off, total = _batch_round(torch, files, pos, cuts)
+        st = ws.write(d, off, total).cpu().numpy()[:n]
+        assert (st == 0).all(), st
+        pos = [p + c for p, c in zip(pos, cuts)]
+        if rnd == 2:
+            got = ws.checksums()
+            for i in range(n):
+                assert (got[i][1] << 64) | got[i][0] == pyoracle.xxh3_128(files[i][:pos[i]].tobytes()), (i, pos[i])
+    assert pos == sizes
+    got = ws.checksums()
+    for i in range(n):
+        assert (got[i][1] << 64) | got[i][0] == pyoracle.xxh3_128(files[i].tobytes()), (i, sizes[i])
+
+
+def test_stream_batch_bad_states(gpu):
+    """A state never initialised and a decreasing range get LSM_BAD_ARG and stay
+    unchanged; the other states advance; a total_len below the ranges' bytes
+    rejects the whole call."""
+    import torch
+    rng = np.random.default_rng(5)
+    files = [rng.integers(0, 256, 5000, dtype=np.uint8) for _ in range(4)]
+    ws = gpu.ChecksummedWriterSet(4)
+    size = gpu.lib().lsm_xxh3_128_stream_state_size()
+    ws.states[size:2 * size].zero_()  # state 1: not initialised (no magic)
+    arena = np.concatenate(files + [np.zeros(64, np.uint8)])
+    d = torch.from_numpy(arena).cuda()
+    off = torch.tensor([0, 5000, 10000, 15000, 14000], dtype=torch.int64, device="cuda")  # state 3: decreasing
+    st = ws.write(d, off, 20000).cpu().numpy()
+    assert list(st) == [0, 10, 0, 10]
+    got = ws.checksums()
+    for i in (0, 2):
+        assert (got[i][1] << 64) | got[i][0] == pyoracle.xxh3_128(files[i].tobytes())
+    assert (got[3][1] << 64) | got[3][0] == pyoracle.xxh3_128(b"")
+    # ranges of 20000 bytes against total_len 1000: nothing changes
+    off2 = torch.tensor([0, 5000, 10000, 15000, 20000], dtype=torch.int64, device="cuda")
+    st = ws.write(d, off2, 1000).cpu().numpy()
+    assert list(st) == [10, 10, 10, 10]
+    got2 = ws.checksums()
+    assert got2[0] == got[0] and got2[2] == got[2] and got2[3] == got[3]
