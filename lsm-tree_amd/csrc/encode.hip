@@ -766,13 +766,19 @@ __device__ __forceinline__ void write_block_lds_mw(const EncodeParams& P, uint32
 constexpr uint32_t kErecHead = 0x8000u;
 
 // Group write kernel (E2) budget, see encode_group_kernel.
-constexpr uint32_t kGWaves = 4, kGThreads = kGWaves * kWave;
+#ifndef LSM_G_WAVES
+#define LSM_G_WAVES 4
+#endif
+constexpr uint32_t kGWaves = LSM_G_WAVES, kGThreads = kGWaves * kWave;
 #ifndef LSM_G_RUN
 #define LSM_G_RUN 32
 #endif
 constexpr uint32_t kGRun = LSM_G_RUN;          // blocks per workgroup (<= 63: one lane each)
-constexpr uint32_t kGBlocks = 16;              // blocks per group
-constexpr uint32_t kGItems = 256;              // items per group (one thread each)
+#ifndef LSM_G_BLOCKS
+#define LSM_G_BLOCKS 16
+#endif
+constexpr uint32_t kGBlocks = LSM_G_BLOCKS;    // blocks per group
+constexpr uint32_t kGItems = kGThreads;        // items per group (one thread each)
 constexpr uint32_t kGSlack = 48;               // readable bytes past each staged span
 #ifndef LSM_G_KEYS  // group LDS budget (four configs[1] blocks by default)
 #define LSM_G_KEYS 4096
@@ -1827,11 +1833,11 @@ __global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(LSM_G
     ENC_PHASE(4);
     // ---- payload xxh3_128: 1 KiB units over the 16 DPP rows
     {
-      const uint32_t row = wave * 4 + (lane >> 4), r = lane & 15, q = r & 3, s = r >> 2;
+      const uint32_t row = wave * 4 + (lane >> 4), r = lane & 15, q = r & 3, s = r >> 2;  // (4 kGWaves rows)
       const uint32_t ubase = rl32(r_upre, r0);
       const uint32_t units = (kDiagBuild && (P.diag & 10)) ? 0 : rl32(r_upre, r0 + k) - ubase;
       const uint64_t* acc = L.secret.acc + s + 2 * q;
-      for (uint32_t u = row; u < units; u += 16) {
+      for (uint32_t u = row; u < units; u += 4 * kGWaves) {
         uint32_t jb = 0;  // (unit starts from the run registers: no dependent LDS reads)
         for (uint32_t x = 1; x < k; ++x) jb += (rl32(r_upre, r0 + x) - ubase <= u) ? 1u : 0u;
         const GBlk& B = L.blk[jb];

@@ -262,6 +262,59 @@ __global__ __launch_bounds__(kWG) void bench(const uint8_t* vals, const uint32_t
     for (int i = t; i < kImg; i += kWG) out[i] = img[i];
 }
 
+// 8: the body dwords by rows: 16-lane DPP row r copies record 16 r + k at step k (lane l =
+// destination dword l of the body: consecutive banks), the record's params broadcast by
+// row_newbcast; head / tail bytes by the record's own lane as in 0.
+__device__ __forceinline__ uint32_t row_bcast(uint32_t v, int k) {
+  switch (k) {
+#define RB(K) case K: return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)v, 0x150 + K, 0xF, 0xF, false);
+    RB(0) RB(1) RB(2) RB(3) RB(4) RB(5) RB(6) RB(7) RB(8) RB(9) RB(10) RB(11) RB(12) RB(13) RB(14) RB(15)
+#undef RB
+  }
+  return 0;
+}
+template <int V>
+__global__ __launch_bounds__(kWG) void bench_row(const uint8_t* vals, const uint32_t* dpos, uint8_t* out, int iters) {
+  __shared__ __attribute__((aligned(16))) uint8_t stage[kStage];
+  __shared__ __attribute__((aligned(16))) uint8_t img[kImg];
+  const int t = threadIdx.x, l = t & 15;
+  for (int i = t; i < kStage / 4; i += kWG) reinterpret_cast<uint32_t*>(stage)[i] = reinterpret_cast<const uint32_t*>(vals)[i];
+  for (int i = t; i < kImg / 4; i += kWG) reinterpret_cast<uint32_t*>(img)[i] = 0;
+  __syncthreads();
+  const uint32_t d = dpos[t];
+  const uint32_t n = kVal, s = kVal * t;
+  const uint32_t h = min(n, (4u - (d & 3u)) & 3u);
+  const uint32_t d1 = d + h, e = d + n, body = ((e & ~3u) - d1) >> 2;
+  const uint32_t sp = s + h, sh = sp & 3u;
+  const uint32_t p_dst = d1 >> 2, p_src = sp >> 2, p_meta = body | (sh << 8);
+  const uint32_t* s32 = reinterpret_cast<const uint32_t*>(stage);
+  uint32_t* d32 = reinterpret_cast<uint32_t*>(img);
+  for (int it = 0; it < iters; ++it) {
+    uint32_t hb[3], tb[3];
+    const uint32_t t0 = d1 + 4 * body;
+#pragma unroll
+    for (uint32_t k = 0; k < 3; ++k) if (k < h) hb[k] = stage[s + k];
+#pragma unroll
+    for (uint32_t k = 0; k < 3; ++k) if (t0 + k < e) tb[k] = stage[s + (t0 + k - d)];
+#pragma unroll
+    for (uint32_t k = 0; k < 3; ++k) if (k < h) img[d + k] = (uint8_t)hb[k];
+#pragma unroll
+    for (uint32_t k = 0; k < 3; ++k) if (t0 + k < e) img[t0 + k] = (uint8_t)tb[k];
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      const uint32_t rd = row_bcast(p_dst, k), rs = row_bcast(p_src, k), rm = row_bcast(p_meta, k);
+      const uint32_t cnt = rm & 0xFF, rsh = rm >> 8;
+      const uint32_t w0 = s32[rs + l], w1 = s32[rs + l + 1];
+      if ((uint32_t)l < cnt) d32[rd + l] = __builtin_amdgcn_alignbyte(w1, w0, rsh);
+    }
+    __builtin_amdgcn_s_waitcnt(0xc07f);
+    __builtin_amdgcn_s_barrier();
+  }
+  __syncthreads();
+  if (blockIdx.x == 0)
+    for (int i = t; i < kImg; i += kWG) out[i] = img[i];
+}
+
 int main() {
   std::vector<uint8_t> v(kStage);
   for (int i = 0; i < kStage; ++i) v[i] = (uint8_t)(i * 37 + 11);
@@ -304,5 +357,8 @@ int main() {
   run("7 rec-dma", bench_rec_dma<7>);
   run("0 rot-wrap", bench<0>);
   run("7 rec-dma", bench_rec_dma<7>);
+  run("8 rows", bench_row<8>);
+  run("0 rot-wrap", bench<0>);
+  run("8 rows", bench_row<8>);
   return 0;
 }
