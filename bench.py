@@ -589,6 +589,39 @@ def bench_file_checksum(torch, lsmgpu, enc, total_bytes, reps=5):
                     "host-timed incl. the 16-B digest copy"}
 
 
+def bench_file_checksum_batch(torch, lsmgpu, enc, total_bytes, n_files=64, reps=5):
+    """Running whole-file checksums of n_files tables advanced together
+    (lsm_xxh3_128_stream_update_batch: one ChecksummedWriter per table of a
+    MultiWriter, src/table/multi_writer.rs:181-257): the encoded configs[1] batch
+    cut into n_files equal files (~62 MB each), every digest checked against the
+    oracle's one-shot xxh3_128 outside the timed region."""
+    import numpy as np
+    import pyoracle
+    per = total_bytes // n_files
+    off = torch.arange(n_files + 1, dtype=torch.int64, device=enc["buf"].device) * per
+    w = lsmgpu.ChecksummedWriterSet(n_files)
+    st = w.write(enc["buf"], off, per * n_files)
+    got = w.checksums()
+    assert int((st[:n_files] != 0).sum()) == 0
+    host = enc["buf"][:per * n_files].cpu().numpy()
+    for i in range(n_files):
+        exp = pyoracle.xxh3_128(host[i * per:(i + 1) * per].tobytes())
+        assert (got[i][1] << 64) | got[i][0] == exp, f"batched checksum of file {i} differs from the oracle"
+    del host
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        ws = lsmgpu.ChecksummedWriterSet(n_files)
+        ws.write(enc["buf"], off, per * n_files)
+        ws.checksums()  # (synchronises)
+    ms = (time.perf_counter() - t0) * 1e3 / reps
+    nbytes = per * n_files
+    return {"files": n_files, "bytes_per_file": per, "ms": round(ms, 4),
+            "GiB_per_s": round(nbytes / (ms * 1e-3) / 2 ** 30, 1),
+            "note": "init + one update_batch + digest_batch per rep, host-timed incl. the digest copy; "
+                    "every digest equals the oracle's one-shot xxh3_128"}
+
+
 def bench_bloom(torch, lsmgpu, items, n_items, reps=5):
     """Standard Bloom filter over the configs[1] batch's keys (FullFilterWriter,
     src/table/writer/filter/full.rs:47-92, BitsPerKey(10) default)."""
@@ -1178,6 +1211,8 @@ def main():
     if not args.no_extra:
         extra["point_read"] = bench_point_read(torch, lsmgpu, items, enc, nb, n_items)
         extra["file_checksum"] = bench_file_checksum(torch, lsmgpu, enc, total_bytes)
+        if rank == 0:
+            extra["file_checksum_batch"] = bench_file_checksum_batch(torch, lsmgpu, enc, total_bytes)
         extra["bloom"] = bench_bloom(torch, lsmgpu, items, n_items)
         if rank == 0:
             extra["lz4"] = bench_lz4(torch, lsmgpu, enc, nb)
