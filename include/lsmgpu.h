@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define LSM_ABI_VERSION 5
+#define LSM_ABI_VERSION 6
 #define LSM_HEADER_LEN 33  /* Header::serialized_len(), header.rs:64-76 */
 #define LSM_TRAILER_LEN 31 /* TRAILER_SIZE, trailer.rs:14-23 */
 /* d_blocks must be 16-byte aligned and readable for LSM_INPUT_PADDING bytes
@@ -192,8 +192,14 @@ int lsm_set_device(int device);
  * while their checksum is still being computed, so a block that then fails it
  * may have rows written): as in the reference, where Block::from_file returns
  * Err and no item is yielded, a caller uses no row of a failed block.
- * d_workspace: lsm_decode_workspace_size(n_blocks) bytes of device memory. */
+ * d_workspace: lsm_decode_workspace_size(n_blocks) bytes of device memory, or
+ * lsm_decode_workspace_size_ex(n_blocks, blocks_bytes) bytes: with that much
+ * (blocks_bytes >= the bytes the batch spans), blocks larger than 72 KiB (the
+ * writer's up-to-4-MiB data blocks, writer/mod.rs:193-198; full block indexes)
+ * are cut into work units across the whole GPU instead of one workgroup each.
+ * Same outputs and statuses either way. */
 size_t lsm_decode_workspace_size(uint32_t n_blocks);
+size_t lsm_decode_workspace_size_ex(uint32_t n_blocks, uint64_t blocks_bytes);
 int lsm_decode_blocks(const uint8_t* d_blocks, const uint64_t* d_block_off, uint32_t n_blocks,
                       int32_t expect_type, const lsm_parsed_items* d_out, uint64_t item_cap,
                       uint32_t* d_item_start, int32_t* d_status, void* d_workspace,

@@ -62,6 +62,9 @@ int lsm_set_device(int device) {
 }
 
 size_t lsm_decode_workspace_size(uint32_t n_blocks) { return lsmgpu::decode_workspace_size(n_blocks); }
+size_t lsm_decode_workspace_size_ex(uint32_t n_blocks, uint64_t blocks_bytes) {
+  return lsmgpu::decode_workspace_size_ex(n_blocks, blocks_bytes);
+}
 
 static int decode_blocks_common(const uint8_t* d_blocks, const uint64_t* d_block_off, uint32_t n_blocks,
                                 int32_t expect_type, const lsm_parsed_items* d_out, bool compact, uint64_t item_cap,
@@ -97,7 +100,7 @@ static int decode_blocks_common(const uint8_t* d_blocks, const uint64_t* d_block
     return LSM_BAD_ARG;
   P.stage_bytes = (P.stage_bytes + 15) & ~15u;
   if (lsmgpu::decode_lds_bytes(P.stage_bytes, P.tile_items, P.blocks_per_wave) > 160 * 1024) return LSM_BAD_ARG;
-  hipError_t e = lsmgpu::launch_decode(P, d_workspace, (hipStream_t)stream);
+  hipError_t e = lsmgpu::launch_decode(P, d_workspace, workspace_bytes, (hipStream_t)stream);
   return e == hipSuccess ? LSM_OK : set_hip_error(e, "lsm_decode_blocks");
 }
 

@@ -618,6 +618,11 @@ __device__ __forceinline__ void defer_blocks_wave(const DecodeParams& P, bool pr
   if (pred) gstore(P.defer_list, base + rank, b);
 }
 
+__device__ __forceinline__ void defer2_block(const DecodeParams& P, uint32_t b) {
+  const uint32_t slot = atomicAdd(P.defer2_count, 1u);
+  gstore(P.defer2_list, slot, b);
+}
+
 // Deferred blocks up to kBigStage bytes (the 16..64 KiB data blocks larger
 // than a group stage, and blocks with rare record shapes): one 4-wave
 // workgroup per block, the block staged in LDS by LDS-DMA, then wave 0
@@ -802,6 +807,154 @@ __global__ __launch_bounds__(kBigWaves * kWave) void decode_deferred_staged_kern
   }
 }
 
+// ---- Blocks larger than the general path's stage across the whole GPU (the
+// writer's up-to-4-MiB data blocks, writer/mod.rs:193-198; full block
+// indexes): decode_chunked walks such a block on ONE workgroup, chunk by
+// chunk.  Here its work is cut into units that any workgroup takes:
+//   plan   (the last decode_big_kernel workgroup, once every block is listed):
+//          per huge block the header (incl. its checksum) and trailer views
+//          from HBM, its KiB-block and parse-unit counts, prefix sums of both
+//          over the list (contributions in the workspace pool: 64 B per KiB)
+//   work   (decode_huge_kernel, every CU): parse units = kHugeIv restart
+//          intervals, thread per interval, records walked straight from HBM
+//          (walk_interval_at: every oracle check, the LEB cursor for rare
+//          shapes); hash units = kHugeKib KiB blocks' XXH3 contributions
+//   chain  (decode_huge_chain_kernel): eight single-wave chains per block
+//          (accumulator k on wave k, xxh3_chain_wave), the last one to finish
+//          merges the tail, compares the checksum and writes the status
+// A block whose header fails, or that no longer fits the pool, goes to the
+// general path (defer2) as before: statuses and outputs are the same on both.
+constexpr uint32_t kHugeIv = 256;   // restart intervals per parse unit (thread per interval)
+constexpr uint32_t kHugeKib = 32;   // KiB blocks per hash unit (8 per wave, loads issued together)
+constexpr uint32_t kHugeGrid = 2048;
+
+struct HugeRec {
+  BlockMeta m;         // header view, trailer fields merged in: m.st = trailer status (header checks passed)
+  uint64_t span0, item_base;
+  uint64_t acc[8];     // chain results (accumulator k from chain wave k)
+  uint32_t b, nbk, accepted, parse_bad;
+  uint32_t done, pad[3];
+};
+static_assert(sizeof(HugeRec) % 16 == 0, "HugeRec layout");
+
+struct HugeHdr {
+  uint64_t total_kib;  // contributions over every accepted block
+  uint32_t n3;         // listed huge blocks (HugeRec entries)
+  uint32_t total_pu;   // parse units
+};
+
+// Pool: [HugeHdr | 256][kpre u64 x (n + 1)][ppre u64 x (n + 1)][HugeRec x n][contributions, 64 B per KiB].
+struct HugeLayout {
+  HugeHdr* hdr;
+  uint64_t* kpre;
+  uint64_t* ppre;
+  HugeRec* rec;
+  uint64_t* contrib;
+  uint64_t cap_kib;
+  bool ok;
+};
+__host__ __device__ __forceinline__ uint64_t huge_fixed_bytes(uint64_t n) {
+  return (256 + 16 * (n + 1) + sizeof(HugeRec) * n + 255) & ~255ULL;
+}
+__device__ __forceinline__ HugeLayout huge_layout(const DecodeParams& P, uint32_t n) {
+  HugeLayout L;
+  uint8_t* b = P.huge_pool;
+  L.hdr = reinterpret_cast<HugeHdr*>(b);
+  L.kpre = reinterpret_cast<uint64_t*>(b + 256);
+  L.ppre = L.kpre + (n + 1);
+  L.rec = reinterpret_cast<HugeRec*>(L.ppre + (n + 1));
+  const uint64_t fixed = huge_fixed_bytes(n);
+  L.contrib = reinterpret_cast<uint64_t*>(b + fixed);
+  L.ok = b != nullptr && fixed <= P.huge_pool_bytes;
+  L.cap_kib = L.ok ? (P.huge_pool_bytes - fixed) / 64 : 0;
+  return L;
+}
+
+__device__ __forceinline__ void defer3_block(const DecodeParams& P, uint32_t b) {
+  const uint32_t slot = atomicAdd(P.defer3_count, 1u);
+  gstore(P.defer3_list, slot, b);
+}
+
+// Plan over the huge list, by one workgroup of nthr threads (nthr / 64 <= 16
+// waves); sh: 40 u64 of LDS.  Blocks it does not accept go to defer2.
+__device__ void huge_plan(const DecodeParams& P, uint64_t* sh, uint32_t nthr) {
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = nthr >> 6;
+  const uint32_t n = gload(P.defer3_count, 0);
+  const HugeLayout L = huge_layout(P, n);
+  if (!L.ok) {  // (uniform) no pool, or too small for the records: the general path takes them all
+    for (uint32_t i = tid; i < n; i += nthr) defer2_block(P, gload(P.defer3_list, i));
+    if (P.huge_pool && P.huge_pool_bytes >= 256 && tid == 0) {
+      L.hdr->n3 = 0;
+      L.hdr->total_pu = 0;
+      L.hdr->total_kib = 0;
+    }
+    return;
+  }
+  const bool hash = !(P.flags & LSM_DECODE_PAYLOAD_VERIFIED);
+  if (tid == 0) sh[32] = 0, sh[33] = 0;
+  __syncthreads();
+  for (uint32_t c = 0; c < n; c += nthr) {
+    const uint32_t i = c + tid;
+    uint64_t nbk = 0, npu = 0;
+    bool acc = false;
+    uint32_t b = 0;
+    BlockMeta m{};
+    uint64_t span0 = 0, item_base = 0;
+    if (i < n) {
+      b = gload(P.defer3_list, i);
+      const uint64_t off = gload(P.block_off, b), end = gload(P.block_off, b + 1);
+      span0 = off & ~15ULL;
+      item_base = gload(P.item_start, b);
+      const uint32_t cap = gload(P.item_start, b + 1) - (uint32_t)item_base;
+      const uint8_t* gbase = P.blocks + span0;
+      meta_header(gbase, (uint32_t)(off - span0), end >= off ? end - off : 0, m);
+      acc = m.st == ST_OK;  // every header check, its checksum included
+      if (acc) {
+        const uint32_t plen = m.len - kHdrLen;
+        nbk = hash ? (plen - 1) / 1024 : 0;  // (plen > 72 KiB here: the long path)
+        meta_trailer(gbase, P.expect_type, cap, m, P.compact);  // (after the payload checksum in oracle order)
+        npu = m.st == ST_OK ? (m.bin_len + kHugeIv - 1) / kHugeIv : 0;
+      }
+    }
+    const uint64_t ik = wave_incl_scan_u64(nbk), ip = wave_incl_scan_u64(npu);
+    if (lane == 63) sh[wave] = ik, sh[16 + wave] = ip;
+    __syncthreads();
+    uint64_t bk = sh[32], bp = sh[33], tk = 0, tp = 0;
+    for (uint32_t w = 0; w < nw; ++w) {
+      bk += w < wave ? sh[w] : 0;
+      bp += w < wave ? sh[16 + w] : 0;
+      tk += sh[w];
+      tp += sh[16 + w];
+    }
+    const uint64_t kp = bk + ik - nbk, pp = bp + ip - npu;
+    if (i < n) {
+      acc = acc && kp + nbk <= L.cap_kib;  // (the pool holds the contributions of a prefix of the list)
+      HugeRec* r = L.rec + i;
+      r->m = m;
+      r->span0 = span0;
+      r->item_base = item_base;
+      r->b = b;
+      r->nbk = (uint32_t)nbk;
+      r->accepted = acc;
+      r->parse_bad = 0;
+      r->done = 0;
+      gstore(L.kpre, i, kp);
+      gstore(L.ppre, i, pp);
+      if (!acc) defer2_block(P, b);
+    }
+    __syncthreads();
+    if (tid == 0) sh[32] += tk, sh[33] += tp;
+    __syncthreads();
+  }
+  if (tid == 0) {
+    gstore(L.kpre, n, sh[32]);
+    gstore(L.ppre, n, sh[33]);
+    L.hdr->total_kib = sh[32];
+    L.hdr->total_pu = (uint32_t)sh[33];
+    L.hdr->n3 = n;
+  }
+}
+
 // Large blocks (SURVEY configs[4]: 16 / 64 KiB data blocks) listed by the
 // group kernel: persistent 8-wave workgroups, two per CU (one stage each:
 // the other workgroup's decode overlaps this one's DMA).  Per block, after
@@ -837,11 +990,6 @@ constexpr uint32_t kBigGSync = (sizeof(BigSync) + 15) & ~15u;
 constexpr uint32_t kBigGLds = 80 + kBigGSync + kBigGRec + kBigGOwner + kBigGContrib + kBigGSlot;
 constexpr uint32_t kBigGPerCU = 2;
 static_assert(kBigGLds * kBigGPerCU <= 160 * 1024, "big-block workgroups per CU");
-
-__device__ __forceinline__ void defer2_block(const DecodeParams& P, uint32_t b) {
-  const uint32_t slot = atomicAdd(P.defer2_count, 1u);
-  gstore(P.defer2_list, slot, b);
-}
 
 // A listed block's handle and item range; fits = it takes the stage path.
 struct BigBlk {
@@ -913,7 +1061,10 @@ __global__ __launch_bounds__(kBigGWaves * kWave) void decode_big_kernel(DecodePa
       }
       const BigBlk x = big_blk(P, li);
       if (x.fits) return x;
-      if (tid == 0) defer2_block(P, x.b);  // (workgroup-uniform)
+      if (tid == 0) {  // (workgroup-uniform)
+        if (P.huge_pool && x.end >= x.off && x.span1 - x.span0 > kBigStage) defer3_block(P, x.b);
+        else defer2_block(P, x.b);
+      }
     }
   };
   auto issue_dma = [&](const BigBlk& x, uint8_t* dst) {  // wave w moves 1-KiB pieces w, w + 8, ...
@@ -1015,12 +1166,146 @@ __global__ __launch_bounds__(kBigGWaves * kWave) void decode_big_kernel(DecodePa
 #endif
     X = Xn;
   }
+  if (P.huge_pool) {  // the last workgroup to finish plans the huge blocks (every listing is done)
+    __syncthreads();
+    if (tid == 0) {
+      __threadfence();
+      sync->a_done = atomicAdd(P.big_done, 1u) == gridDim.x - 1;
+    }
+    __syncthreads();
+    if (sync->a_done) {
+      __threadfence();
+      huge_plan(P, rec, kThreads);
+    }
+  }
 #if defined(LSM_DIAG) && !defined(LSM_DIAG_NOTIME)
   if (tid == 0) {
     for (int i = 0; i < 8; ++i) atomicAdd(&g_dec_phase[i], (unsigned long long)ph[i]);
     atomicAdd(&g_dec_phase[15], (unsigned long long)nblk);
   }
 #endif
+}
+
+// The last i in [0, n) with a[i] <= v (a[0] = 0, nondecreasing): the huge
+// block that owns unit / KiB block v (blocks without any are passed over).
+__device__ __forceinline__ uint32_t last_le(const uint64_t* a, uint32_t n, uint64_t v) {
+  uint32_t lo = 0, hi = n;
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (gload(a, mid) <= v) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
+
+// Huge-block work units (see huge_plan): parse units first, then hash units.
+__global__ __launch_bounds__(256) void decode_huge_kernel(DecodeParams P) {
+  const HugeHdr* hp = reinterpret_cast<const HugeHdr*>(P.huge_pool);
+  const uint32_t n = hp->n3;
+  if (!n) return;
+  const HugeLayout L = huge_layout(P, n);
+  const uint32_t tpu = hp->total_pu;
+  const uint64_t tk = hp->total_kib;
+  const uint64_t units = tpu + (tk + kHugeKib - 1) / kHugeKib;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int q = lane & 3, s = lane >> 2;
+  const uint64_t k0 = kLongSecret.acc[s + 2 * q], k1 = kLongSecret.acc[s + 2 * q + 1];
+  for (uint64_t u = blockIdx.x; u < units; u += gridDim.x) {
+    if (u < tpu) {  // kHugeIv restart intervals of one block, thread per interval
+      const uint32_t i = last_le(L.ppre, n, u);
+      const HugeRec* r = L.rec + i;
+      if (!r->accepted) continue;  // (uniform)
+      const BlockMeta m = r->m;
+      const uint32_t iv = (uint32_t)(u - gload(L.ppre, i)) * kHugeIv + tid;
+      bool ok = true;
+      if (iv < m.bin_len) {
+        const uint64_t item_base = r->item_base;
+        ok = walk_interval(P.blocks + r->span0, m.p0, m, iv, [&](uint32_t j, const ItemFields& f) {
+          emit_global(P.out, item_base + j, f, P.seqno_add, P.compact);
+        });
+      }
+      const uint64_t bad = __ballot(!ok);
+      if (bad && lane == (uint32_t)__builtin_ctzll(bad)) atomicOr(const_cast<uint32_t*>(&r->parse_bad), 1u);
+    } else {  // kHugeKib KiB blocks' contributions: wave w takes g0 + w, g0 + w + 4, ...
+      const uint64_t g0 = (u - tpu) * kHugeKib, g1 = min(tk, g0 + kHugeKib);
+      uint32_t i = last_le(L.kpre, n, g0);
+      constexpr uint32_t kPer = kHugeKib / 4;
+      const uint8_t* base[kPer];
+      uint32_t pos[kPer];
+      uint64_t gg[kPer];
+      bool live[kPer];
+#pragma unroll
+      for (uint32_t j = 0; j < kPer; ++j) {
+        const uint64_t g = g0 + wave + 4 * j;
+        live[j] = g < g1;
+        gg[j] = g;
+        base[j] = P.blocks;
+        pos[j] = 0;
+        if (live[j]) {
+          while (gload(L.kpre, i + 1) <= g) ++i;
+          const HugeRec* r = L.rec + i;
+          live[j] = r->accepted != 0;
+          base[j] = P.blocks + r->span0;
+          pos[j] = r->m.p0 + (uint32_t)(g - gload(L.kpre, i)) * 1024 + 16 * lane;
+        }
+      }
+      Win16 w[kPer];
+#pragma unroll
+      for (uint32_t j = 0; j < kPer; ++j) w[j] = live[j] ? read_win16(base[j], pos[j]) : Win16{0, 0};
+#pragma unroll
+      for (uint32_t j = 0; j < kPer; ++j) {
+        uint64_t c0 = 0, c1 = 0;
+        stripe_part(w[j], k0, k1, c0, c1);
+        c0 = quad_group_sum64(c0);
+        c1 = quad_group_sum64(c1);
+        if (live[j] && lane < 4) {
+          gstore(L.contrib, 8 * gg[j] + 2 * q, c0);
+          gstore(L.contrib, 8 * gg[j] + 2 * q + 1, c1);
+        }
+      }
+    }
+  }
+}
+
+// Chains of the huge blocks: single-wave workgroup pairs (block i, accumulator
+// k); the last of a block's eight chains merges, checks and writes its status
+// (oracle order: payload checksum, then trailer, then parse).
+__global__ __launch_bounds__(64) void decode_huge_chain_kernel(DecodeParams P) {
+  const HugeHdr* hp = reinterpret_cast<const HugeHdr*>(P.huge_pool);
+  const uint32_t n = hp->n3;
+  if (!n) return;
+  const HugeLayout L = huge_layout(P, n);
+  const bool hash = !(P.flags & LSM_DECODE_PAYLOAD_VERIFIED);
+  const int lane = threadIdx.x & 63;
+  for (uint64_t p = blockIdx.x; p < 8ULL * n; p += gridDim.x) {
+    const uint32_t i = (uint32_t)(p >> 3), k = (uint32_t)(p & 7);
+    HugeRec* r = L.rec + i;
+    if (!r->accepted) continue;
+    const BlockMeta m = r->m;
+    const int32_t tail_st = m.st != ST_OK ? m.st : r->parse_bad ? (int32_t)ST_PARSE : (int32_t)ST_OK;
+    if (!hash) {
+      if (k == 0 && lane == 0) gstore(P.status, r->b, tail_st);
+      continue;
+    }
+    uint64_t a0, a1;
+    xxh3_acc_init((int)(k >> 1), a0, a1);
+    const uint64_t x = xxh3_chain_wave(L.contrib + 8 * gload(L.kpre, i), r->nbk, k, (k & 1) ? a1 : a0,
+                                       kLongSecret.acc[16 + k]);
+    uint32_t last = 0;
+    if (lane == 0) {
+      r->acc[k] = x;
+      __threadfence();
+      last = atomicAdd(&r->done, 1u) == 7;
+    }
+    if (!__shfl((int)last, 0)) continue;
+    __threadfence();
+    const int q = lane & 3;
+    const uint64_t c0 = __hip_atomic_load(&r->acc[2 * q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const uint64_t c1 = __hip_atomic_load(&r->acc[2 * q + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    uint64_t lo, hi;
+    xxh3_wave_tail_merge(P.blocks + r->span0, m.p0, m.len - kHdrLen, &kLongSecret, c0, c1, lo, hi);
+    if (lane == 0) gstore(P.status, r->b, (lo != m.ck_lo || hi != m.ck_hi) ? (int32_t)ST_CKSUM : tail_st);
+  }
 }
 
 // Workgroup = kGroupWaves waves sharing one LDS stage (default 32 KiB: eight
@@ -1263,10 +1548,19 @@ struct ItemStartOut {
 
 static size_t counts_bytes(uint32_t n_blocks) { return ((size_t)n_blocks * 8 + 255) / 256 * 256; }
 static size_t tiles_bytes(uint32_t n_blocks) { return (scan_tiles(n_blocks) * 8 + 255) / 256 * 256; }
-static size_t defer_bytes(uint32_t n_blocks) { return ((size_t)n_blocks * 4 + 256 + 255) / 256 * 256; }
+static size_t defer_bytes(uint32_t n_blocks) { return ((size_t)n_blocks * 4 + 255) / 256 * 256; }
 
+// counts | scan tiles | 256 B of counters (defer, defer2, defer3, big_done) | three block lists
 size_t decode_workspace_size(uint32_t n_blocks) {
-  return counts_bytes(n_blocks) + tiles_bytes(n_blocks) + 2 * defer_bytes(n_blocks);
+  return counts_bytes(n_blocks) + tiles_bytes(n_blocks) + 256 + 3 * defer_bytes(n_blocks);
+}
+
+// + the huge-block pool for a batch of blocks_bytes bytes: every huge block
+// spans more than kBigStage bytes, contributions 64 B per KiB.
+size_t decode_workspace_size_ex(uint32_t n_blocks, uint64_t blocks_bytes) {
+  const uint64_t most = blocks_bytes / kBigStage + 1;
+  const uint64_t n3 = most < n_blocks ? most : n_blocks;
+  return decode_workspace_size(n_blocks) + huge_fixed_bytes(n3) + 64 * (blocks_bytes / 1024 + 1) + 256;
 }
 
 uint32_t decode_lds_bytes(uint32_t stage_bytes, uint32_t tile_items, uint32_t blocks_per_wave) {
@@ -1275,19 +1569,24 @@ uint32_t decode_lds_bytes(uint32_t stage_bytes, uint32_t tile_items, uint32_t bl
          ((stage_bytes + 15) & ~15u) + kStagePad + (uint32_t)sizeof(LongSecret);
 }
 
-hipError_t launch_decode(const DecodeParams& P0, void* ws, hipStream_t st) {
+hipError_t launch_decode(const DecodeParams& P0, void* ws, size_t ws_bytes, hipStream_t st) {
   DecodeParams P = P0;
   uint64_t* counts = (uint64_t*)ws;
   uint64_t* tiles = (uint64_t*)((uint8_t*)ws + counts_bytes(P.n_blocks));
   uint8_t* dws = (uint8_t*)ws + counts_bytes(P.n_blocks) + tiles_bytes(P.n_blocks);
   P.defer_count = (uint32_t*)dws;
+  P.defer2_count = (uint32_t*)dws + 1;
+  P.defer3_count = (uint32_t*)dws + 2;
+  P.big_done = (uint32_t*)dws + 3;
   P.defer_list = (uint32_t*)(dws + 256);
-  uint8_t* dws2 = dws + defer_bytes(P.n_blocks);
-  P.defer2_count = (uint32_t*)dws2;
-  P.defer2_list = (uint32_t*)(dws2 + 256);
-  hipError_t e = hipMemsetAsync(P.defer_count, 0, 4, st);
+  P.defer2_list = (uint32_t*)(dws + 256 + defer_bytes(P.n_blocks));
+  P.defer3_list = (uint32_t*)(dws + 256 + 2 * defer_bytes(P.n_blocks));
+  const size_t base = decode_workspace_size(P.n_blocks);
+  const size_t pool0 = (base + 255) & ~(size_t)255;
+  P.huge_pool = ws_bytes >= pool0 + huge_fixed_bytes(1) + 64 * 128 ? (uint8_t*)ws + pool0 : nullptr;
+  P.huge_pool_bytes = P.huge_pool ? ws_bytes - pool0 : 0;
+  hipError_t e = hipMemsetAsync(dws, 0, 16, st);
   if (e != hipSuccess) return e;
-  if ((e = hipMemsetAsync(P.defer2_count, 0, 4, st)) != hipSuccess) return e;
   if (!(P.flags & LSM_DECODE_ITEM_START_VALID)) {
     hipLaunchKernelGGL(trailer_counts_kernel, dim3((P.n_blocks + 255) / 256), dim3(256), 0, st, P.blocks,
                        P.block_off, P.n_blocks, counts);
@@ -1338,6 +1637,10 @@ hipError_t launch_decode(const DecodeParams& P0, void* ws, hipStream_t st) {
     const uint32_t big = kBigStageOff + kBigStage + kStagePad;
     if ((e = set_lds_attr((const void*)decode_deferred_staged_kernel, big, &done_big)) != hipSuccess) return e;
     hipLaunchKernelGGL(decode_deferred_staged_kernel, dim3(dgrid), dim3(kBigWaves * kWave), big, st, P2);
+  }
+  if (P.huge_pool && bgrid) {  // (the plan ran at the end of the big-block kernel)
+    hipLaunchKernelGGL(decode_huge_kernel, dim3(kHugeGrid), dim3(256), 0, st, P);
+    hipLaunchKernelGGL(decode_huge_chain_kernel, dim3(kHugeGrid), dim3(64), 0, st, P);
   }
   return hipGetLastError();
 }

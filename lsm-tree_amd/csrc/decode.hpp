@@ -43,6 +43,11 @@ struct DecodeParams {
   uint32_t* defer_list;
   uint32_t* defer2_count;  // workspace: blocks decode_big_kernel hands on to the general path
   uint32_t* defer2_list;
+  uint32_t* defer3_count;  // workspace: blocks larger than the general path's stage (decode_big_kernel lists them)
+  uint32_t* defer3_list;
+  uint32_t* big_done;      // workspace: decode_big_kernel workgroups finished (the last one plans the huge blocks)
+  uint8_t* huge_pool;      // workspace past decode_workspace_size (null: huge blocks take the general path)
+  uint64_t huge_pool_bytes;
   uint64_t seqno_add;     // added to every decoded seqno (Scanner's global_seqno, scanner.rs:84)
   uint32_t compact;       // lsm_decode_blocks16: out.key_off / val_off / val_len are uint16_t arrays
 };
@@ -78,8 +83,9 @@ inline hipError_t set_lds_attr(const void* fn, uint32_t bytes, uint64_t* done_ma
 int hip_status(hipError_t e, const char* where);
 
 size_t decode_workspace_size(uint32_t n_blocks);
+size_t decode_workspace_size_ex(uint32_t n_blocks, uint64_t blocks_bytes);
 uint32_t decode_lds_bytes(uint32_t stage_bytes, uint32_t tile_items, uint32_t blocks_per_wave);
-hipError_t launch_decode(const DecodeParams& P, void* workspace, hipStream_t st);
+hipError_t launch_decode(const DecodeParams& P, void* workspace, size_t workspace_bytes, hipStream_t st);
 
 hipError_t launch_xxh3_128_batch(const uint8_t* data, const uint64_t* off, uint32_t n, uint64_t* out,
                                  hipStream_t st);

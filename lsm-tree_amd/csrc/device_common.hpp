@@ -595,6 +595,57 @@ __device__ __forceinline__ void xxh3_wave_tail_merge(const uint8_t* base, uint32
   out_hi = xxh3_avalanche(~((uint64_t)len * P64_2) + thi);
 }
 
+// The serial scramble chain of accumulator k (this wave) over n >= 1 KiB
+// blocks' contributions c[8 i + k], from the accumulator value acc.  One
+// dependent VALU chain per wave: the 8 accumulators are independent, so 8
+// single-wave workgroups (on different SIMDs) run them side by side; a wave
+// holding two chains issues twice the quarter-rate multiplies per step and is
+// slower per step than two waves (scripts/exp/chain_exp.cpp: 1 chain / wave
+// 53 cycles per KiB, 2 chains / wave 79, the one-wave lane-quad chain 133).
+// Step i: acc = scramble(acc + c_i); the addition of c_{i+1} is folded into
+// the addend of the next multiply: y = lo' * P32_1 + (c_{i+1} + (hs * P32_1 << 32)).
+// Contributions arrive 64 steps per coalesced load, kDepth loads in flight,
+// and reach the chain by v_readlane.
+template <int kDepth = 8>
+__device__ __forceinline__ uint64_t xxh3_chain_wave(const uint64_t* __restrict__ c, uint64_t n, uint32_t k,
+                                                     uint64_t acc, uint64_t s) {
+  const int lane = threadIdx.x & 63;
+  const uint32_t s_lo = (uint32_t)s, s_hi = (uint32_t)(s >> 32);
+  // y = acc + c_0, lane-varying by construction (+0): keeps the chain in VGPRs (VALU)
+  uint64_t y = acc + c[k] + __builtin_amdgcn_mbcnt_lo(0, 0);
+  auto step = [&](uint64_t cn) {  // y = scramble(y) + cn
+    const uint32_t hi = (uint32_t)(y >> 32);
+    const uint32_t lo = (uint32_t)y ^ (hi >> 15) ^ s_lo;
+    const uint32_t hs = hi ^ s_hi;
+    y = (uint64_t)lo * P32_1 + (cn + ((uint64_t)(hs * P32_1) << 32));
+  };
+  const uint64_t* cn = c + 8;  // the contributions that follow c_0
+  const uint64_t m = n - 1, full = m / 64;
+  uint64_t buf[kDepth];
+#pragma unroll
+  for (int d = 0; d < kDepth; ++d) buf[d] = (uint64_t)d < full ? cn[8 * (64 * d + lane) + k] : 0;
+  for (uint64_t b = 0; b < full; ++b) {
+    const uint32_t lo = (uint32_t)buf[0], hi = (uint32_t)(buf[0] >> 32);
+#pragma unroll
+    for (int d = 0; d + 1 < kDepth; ++d) buf[d] = buf[d + 1];
+    buf[kDepth - 1] = b + kDepth < full ? cn[8 * (64 * (b + kDepth) + lane) + k] : 0;
+#pragma unroll
+    for (int t = 0; t < 64; ++t)
+      step((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)lo, t) |
+           ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)hi, t) << 32));
+  }
+  {
+    const uint64_t n0 = full * 64;
+    const uint64_t cl = n0 + lane < m ? cn[8 * (n0 + lane) + k] : 0;
+    const uint32_t lo = (uint32_t)cl, hi = (uint32_t)(cl >> 32);
+    for (uint32_t t = 0; n0 + t < m; ++t)
+      step((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)lo, (int)t) |
+           ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)hi, (int)t) << 32));
+  }
+  step(0);  // the last block's scramble, nothing added after it
+  return y;
+}
+
 template <uint32_t kBatch = 8>
 __device__ __forceinline__ void xxh3_128_wave_finish(const uint8_t* base, uint32_t pos, uint32_t len,
                                                      const LongSecret* __restrict__ ls, const uint64_t* contrib,

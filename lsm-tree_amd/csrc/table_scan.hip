@@ -161,7 +161,7 @@ extern "C" int lsm_scan_table(const uint8_t* d_file, uint64_t file_len, const ls
   const uint32_t levels = 1 + table->two_level;
   for (uint32_t lvl = 0; lvl < levels; ++lvl) {
     DecodeParams P = index_params(d_file, w.lvl_off, n_lvl, w, cap_blocks + 1);
-    hipError_t e = launch_decode(P, w.dec_ws, st);
+    hipError_t e = launch_decode(P, w.dec_ws, w.dec_bytes, st);
     if (e == hipSuccess) e = hipMemsetAsync(w.flag, 0xFF, 16, st);
     if (e != hipSuccess) return fail(e);
     hipLaunchKernelGGL(first_failed_kernel, dim3((n_lvl + 255) / 256), dim3(256), 0, st, w.lvl_status, n_lvl,
@@ -213,6 +213,6 @@ extern "C" int lsm_scan_table(const uint8_t* d_file, uint64_t file_len, const ls
   P.tile_items = kDefaultTileItems;
   P.flags = 0;
   P.seqno_add = table->global_seqno;
-  hipError_t e = launch_decode(P, w.dec_ws, st);
+  hipError_t e = launch_decode(P, w.dec_ws, w.dec_bytes, st);
   return e == hipSuccess ? LSM_OK : fail(e);
 }

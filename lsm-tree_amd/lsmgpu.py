@@ -61,7 +61,7 @@ class LsmTableScan(C.Structure):
                 ("global_seqno", C.c_uint64), ("block_count", C.c_uint64)]
 
 
-ABI_VERSION = 5
+ABI_VERSION = 6
 DECODE_ITEM_START_VALID = 1
 DECODE_PAYLOAD_VERIFIED = 2
 
@@ -93,6 +93,8 @@ def lib():
         L.lsm_set_device.argtypes = [C.c_int]
         L.lsm_decode_workspace_size.restype = C.c_size_t
         L.lsm_decode_workspace_size.argtypes = [C.c_uint32]
+        L.lsm_decode_workspace_size_ex.restype = C.c_size_t
+        L.lsm_decode_workspace_size_ex.argtypes = [C.c_uint32, C.c_uint64]
         L.lsm_decode_blocks.restype = C.c_int
         L.lsm_decode_blocks.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_int32, C.POINTER(LsmParsed),
                                         C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]
@@ -196,7 +198,7 @@ def lib():
 
 
 EXPORTED_SYMBOLS = ["lsm_abi_version", "lsm_status_name", "lsm_last_error", "lsm_device_count", "lsm_set_device",
-                    "lsm_decode_workspace_size", "lsm_decode_blocks", "lsm_decode_blocks_tuned", "lsm_decode_blocks16",
+                    "lsm_decode_workspace_size", "lsm_decode_workspace_size_ex", "lsm_decode_blocks", "lsm_decode_blocks_tuned", "lsm_decode_blocks16",
                     "lsm_encode_bound",
                     "lsm_encode_workspace_size", "lsm_encode_blocks", "lsm_cut_blocks", "lsm_xxh3_128_batch",
                     "lsm_point_read_blocks", "lsm_xxh3_128_file_workspace_size", "lsm_xxh3_128_file",
@@ -265,9 +267,12 @@ class Decoder:
         self.device = device
         self.ws = None
 
-    def workspace(self, n_blocks):
+    def workspace(self, n_blocks, blocks_bytes=0):
+        """Workspace for n_blocks; with blocks_bytes (the batch buffer's size) it
+        includes the pool that spreads blocks > 72 KiB over the whole GPU."""
         torch = _torch()
-        need = lib().lsm_decode_workspace_size(n_blocks)
+        need = (lib().lsm_decode_workspace_size_ex(n_blocks, blocks_bytes) if blocks_bytes
+                else lib().lsm_decode_workspace_size(n_blocks))
         if self.ws is None or self.ws.numel() < need:
             self.ws = torch.empty(max(need, 256), dtype=torch.uint8, device=self.device)
         return self.ws
@@ -285,13 +290,17 @@ class Decoder:
         return out
 
     def decode(self, blocks, block_off, n_blocks, out, item_cap, expect_type=-1, tuning=None, stream=None,
-               compact=False):
+               compact=False, pool=True, workspace_bytes=None):
         """Enqueue lsm_decode_blocks (compact: lsm_decode_blocks16 into 16-bit
         offset arrays from alloc_outputs(..., compact=True)).  blocks: uint8 cuda
-        (padded); block_off: int64 cuda [n+1]."""
+        (padded); block_off: int64 cuda [n+1].  pool=False: the base workspace
+        only (blocks > 72 KiB on one workgroup each); workspace_bytes: pass
+        exactly that much workspace (tests of a pool too small for the batch)."""
         if tuning is None and os.environ.get("LSMGPU_DECODE_TUNING"):  # diagnostic override
             tuning = tuple(int(x, 0) for x in os.environ["LSMGPU_DECODE_TUNING"].split(","))
-        ws = self.workspace(n_blocks)
+        ws = self.workspace(n_blocks, blocks.numel() if pool else 0)
+        if workspace_bytes is not None:
+            ws = _torch().empty(max(workspace_bytes, 1), dtype=_torch().uint8, device=self.device)[:workspace_bytes]
         if compact:
             ps = LsmParsed16()
             for f, dt in PARSED16_FIELDS:
@@ -322,7 +331,7 @@ class Decoder:
 
 
 def decode_blocks(blocks, block_off, n_blocks=None, expect_type=-1, item_cap=None, fields=None, tuning=None,
-                  compact=False):
+                  compact=False, pool=True, workspace_bytes=None):
     """Convenience: decode device blocks, returns dict of device tensors
     (compact: the 19 B/item lsm_parsed_items16 layout)."""
     n_blocks = (block_off.numel() - 1) if n_blocks is None else n_blocks
@@ -330,7 +339,8 @@ def decode_blocks(blocks, block_off, n_blocks=None, expect_type=-1, item_cap=Non
         item_cap = blocks.numel() // 3 + 1
     d = Decoder(blocks.device)
     out = d.alloc_outputs(item_cap, n_blocks, fields, compact)
-    return d.decode(blocks, block_off, n_blocks, out, item_cap, expect_type, tuning, compact=compact)
+    return d.decode(blocks, block_off, n_blocks, out, item_cap, expect_type, tuning, compact=compact, pool=pool,
+                    workspace_bytes=workspace_bytes)
 
 
 class Encoder:

@@ -87,13 +87,15 @@ def pack(blocks: list[bytes]):
     return np.frombuffer(b"".join(blocks), np.uint8).copy(), off
 
 
-def gpu_decode(L, blocks_np, off_np, expect_type=-1, tuning=None, item_cap=None):
+def gpu_decode(L, blocks_np, off_np, expect_type=-1, tuning=None, item_cap=None, pool=True, workspace_bytes=None,
+               compact=False):
     import torch
     d_blocks = L.to_device_bytes(blocks_np)
     d_off = torch.from_numpy(off_np.astype(np.int64)).cuda()
     n = len(off_np) - 1
     item_cap = item_cap if item_cap is not None else len(blocks_np) // 3 + 1
-    out = L.decode_blocks(d_blocks, d_off, n, expect_type=expect_type, item_cap=item_cap, tuning=tuning)
+    out = L.decode_blocks(d_blocks, d_off, n, expect_type=expect_type, item_cap=item_cap, tuning=tuning, pool=pool,
+                          workspace_bytes=workspace_bytes, compact=compact)
     torch.cuda.synchronize()
     res = {k: v.cpu().numpy() for k, v in out.items()}
     res["status"] = res["status"][:n]

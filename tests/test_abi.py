@@ -52,7 +52,7 @@ def test_library_exports_exactly_the_header(L):
 
 def test_abi_version_and_status_names(L):
     lib = L.lib()
-    assert lib.lsm_abi_version() == L.ABI_VERSION == 5
+    assert lib.lsm_abi_version() == L.ABI_VERSION == 6
     for code, name in L.STATUS.items():
         assert lib.lsm_status_name(code).decode() == name
 

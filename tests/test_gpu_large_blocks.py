@@ -1,9 +1,11 @@
 """Data blocks above the general path's 72 KiB stage, up to the writer's 4 MiB
 data-block target (use_data_block_size, src/table/writer/mod.rs:193-198):
 encoded on the device (E3, straight in HBM) bit-exact against the oracle and
-decoded through the stage in 64 KiB chunks (decode_chunked: per-KiB XXH3
-contributions on all waves, the chain carried across chunks, intervals parsed
-from LDS or walked from HBM when they straddle the staged window).
+decoded two ways: with the workspace pool (pool=True, the default:
+lsm_decode_workspace_size_ex) the blocks are cut into parse units (restart
+intervals) and hash units (KiB blocks) over the whole GPU plus eight
+single-wave XXH3 chains per block; without it (pool=False) each goes through
+the stage in 64 KiB chunks on one workgroup (decode_chunked).
 Cases: 256 KiB, 1 MiB and 4 MiB blocks, hash ratio 0 and 1.33 (the hash index
 is dropped above 254 restart heads, trailer.rs:100-111), restart intervals 16
 and 1, tombstones, a flipped payload bit (CKSUM) and a broken record re-sealed
@@ -27,9 +29,10 @@ def _gpu_encode(gpu, items, starts, ri, ratio):
     return out["buf"].cpu().numpy()[:int(off[-1])], off, out["status"].cpu().numpy()[:len(starts) - 1]
 
 
+@pytest.mark.parametrize("pool", [True, False])
 @pytest.mark.parametrize("ratio", [0.0, 1.33])
 @pytest.mark.parametrize("ri", [16, 1])
-def test_large_data_blocks_round_trip(gpu, ri, ratio):
+def test_large_data_blocks_round_trip(gpu, ri, ratio, pool):
     items = counter_items(80000, seed=41 + ri, tomb_frac=0.05)
     starts = np.array([0, 3300, 16400, 78200, 80000], np.uint32)  # ~256 KiB, 1 MiB, 4 MiB, ~130 KiB blocks
     ref_buf, ref_off = pyoracle.encode_blocks(items, starts, restart_interval=ri, hash_ratio=ratio)
@@ -37,13 +40,14 @@ def test_large_data_blocks_round_trip(gpu, ri, ratio):
     assert sizes.max() > 4_100_000 and (sizes > 72 * 1024).all(), sizes
     buf, off, st = _gpu_encode(gpu, items, starts, ri, ratio)
     assert (st == 0).all() and (off == ref_off).all() and buf.tobytes() == ref_buf.tobytes()
-    g = gpu_decode(gpu, buf, off)
+    g = gpu_decode(gpu, buf, off, pool=pool)
     parsed, item_start, status = pyoracle.decode_blocks(buf, off)
     assert (status == 0).all()
     compare_decode(g, parsed, item_start, status)
 
 
-def test_large_data_blocks_corrupted(gpu):
+@pytest.mark.parametrize("pool", [True, False])
+def test_large_data_blocks_corrupted(gpu, pool):
     items = counter_items(20000, seed=7)
     starts = np.array([0, 16400, 20000], np.uint32)  # a 1 MiB and a ~300 KiB block
     buf, off = pyoracle.encode_blocks(items, starts)
@@ -58,7 +62,7 @@ def test_large_data_blocks_corrupted(gpu):
     late[-4] += 1  # item_count + 1: the last interval walks one record too many
     tests = blocks + [bytes(bad_ck), pyoracle.block_write(bytes(rec), 0), pyoracle.block_write(bytes(late), 0)]
     buf2, off2 = pack(tests)
-    g = gpu_decode(gpu, buf2, off2)
+    g = gpu_decode(gpu, buf2, off2, pool=pool)
     parsed, item_start, status = pyoracle.decode_blocks(buf2, off2)
     assert (status[:2] == 0).all() and status[2] == 4 and (status[3:] != 0).all(), status
     compare_decode(g, parsed, item_start, status)
@@ -81,3 +85,75 @@ def test_large_blocks_few_items(gpu, ratio):
     parsed, item_start, status = pyoracle.decode_blocks(buf, off)
     assert (status == 0).all()
     compare_decode(g, parsed, item_start, status)
+
+
+def _mixed_batch(seed=5):
+    """48 blocks of 80-400 KiB between 4 KiB blocks, and corrupted copies of
+    some: header checksum (HDR_CKSUM), payload bit (CKSUM), broken record
+    re-sealed (PARSE), item count + 1 re-sealed (trailer / PARSE), data_length
+    (TRUNCATED), expected type (index block)."""
+    r = np.random.default_rng(seed)
+    cuts = [0]
+    for i in range(48):
+        cuts.append(cuts[-1] + 40)                          # ~4 KiB
+        cuts.append(cuts[-1] + int(r.integers(900, 4600)))  # ~80-400 KiB
+    items = counter_items(cuts[-1], seed=seed, tomb_frac=0.03)
+    starts = np.array(cuts, np.uint32)
+    buf, off = pyoracle.encode_blocks(items, starts)
+    blocks = [bytes(buf[int(off[i]):int(off[i + 1])]) for i in range(len(starts) - 1)]
+    big = [i for i, b in enumerate(blocks) if len(b) > 72 * 1024]
+    assert len(big) >= 40
+    out = list(blocks)
+    b0 = bytearray(blocks[big[0]]); b0[10] ^= 0x01                 # header checksum
+    b1 = bytearray(blocks[big[1]]); b1[33 + len(b1) // 2] ^= 0x20   # payload: CKSUM
+    rec = bytearray(blocks[big[2]][33:])
+    step, bin_off = rec[-30], int.from_bytes(rec[-25:-21], "little")
+    st = int.from_bytes(rec[bin_off + step * 20:bin_off + step * 21], "little")
+    rec[st] = 9                                                      # a restart head's value type
+    late = bytearray(blocks[big[3]][33:]); late[-4] += 1             # item count + 1
+    out += [bytes(b0), bytes(b1), pyoracle.block_write(bytes(rec), 0), pyoracle.block_write(bytes(late), 0),
+            pyoracle.block_write(bytes(blocks[big[4]][33:]), 1)]       # type 1 with data records
+    trunc = bytearray(blocks[big[5]]); trunc[21] ^= 0x01             # data_length field (header checksum too)
+    out.append(bytes(trunc))
+    return pack(out)
+
+
+@pytest.mark.parametrize("pool", [True, False])
+def test_huge_blocks_mixed_batch(gpu, pool):
+    buf, off = _mixed_batch()
+    g = gpu_decode(gpu, buf, off, pool=pool)
+    parsed, item_start, status = pyoracle.decode_blocks(buf, off)
+    assert (status[:-6] == 0).all() and (status[-6:] != 0).all(), status[-6:]
+    compare_decode(g, parsed, item_start, status)
+    for et in (0, 1):  # expected type: TYPE_MISMATCH wherever the type differs
+        g = gpu_decode(gpu, buf, off, expect_type=et, pool=pool)
+        parsed, item_start, status = pyoracle.decode_blocks(buf, off, expect_type=et)
+        compare_decode(g, parsed, item_start, status)
+
+
+def test_huge_blocks_pool_sizes(gpu):
+    """A pool too small for every huge block of the batch: the blocks whose
+    contributions do not fit take the one-workgroup path; results unchanged."""
+    buf, off = _mixed_batch(seed=9)
+    parsed, item_start, status = pyoracle.decode_blocks(buf, off)
+    n = len(off) - 1
+    base = gpu.lib().lsm_decode_workspace_size(n)
+    full = gpu.lib().lsm_decode_workspace_size_ex(n, len(buf) + 64)
+    assert full > base
+    for extra in (0, 100, 4096, 40000, 300_000, 1_500_000, full - base):
+        g = gpu_decode(gpu, buf, off, workspace_bytes=base + extra)
+        compare_decode(g, parsed, item_start, status)
+
+
+def test_huge_blocks_payload_verified(gpu):
+    """LSM_DECODE_PAYLOAD_VERIFIED (frames whose checksum the LZ4 path already
+    checked): no payload hash; trailer / parse statuses as the oracle's."""
+    buf, off = _mixed_batch(seed=13)
+    parsed, item_start, status = pyoracle.decode_blocks(buf, off)
+    keep = [i for i in range(len(off) - 1) if status[i] != 4]  # drop the CKSUM block
+    blocks = [bytes(buf[int(off[i]):int(off[i + 1])]) for i in keep]
+    buf2, off2 = pack(blocks)
+    parsed, item_start, status = pyoracle.decode_blocks(buf2, off2)
+    for pool in (True, False):
+        g = gpu_decode(gpu, buf2, off2, tuning=(0, 0, 0, gpu.DECODE_PAYLOAD_VERIFIED), pool=pool)
+        compare_decode(g, parsed, item_start, status)
