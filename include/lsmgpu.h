@@ -223,10 +223,15 @@ int lsm_decode_blocks16(const uint8_t* d_blocks, const uint64_t* d_block_off, ui
  * mod.rs:530).  Output blocks (header || payload) are packed back to back
  * into d_out; d_block_off (n_blocks+1 device u64) receives their offsets.
  * d_out needs lsm_encode_bound(...) bytes (status LSM_OVERFLOW otherwise).
- * d_workspace: lsm_encode_workspace_size(n_items, n_blocks) bytes. */
+ * d_workspace: lsm_encode_workspace_size(n_items, n_blocks) bytes, or
+ * lsm_encode_workspace_size_ex(n_items, n_blocks, out_cap) bytes: with that
+ * much, blocks whose image exceeds 96 KiB (the writer's up-to-4-MiB data
+ * blocks, writer/mod.rs:193-198) are written and hashed by work units across
+ * the whole GPU instead of one workgroup each.  Same bytes either way. */
 uint64_t lsm_encode_bound(uint64_t n_items, uint32_t n_blocks, uint64_t key_bytes, uint64_t val_bytes,
                           const lsm_block_params* params);
 size_t lsm_encode_workspace_size(uint64_t n_items, uint32_t n_blocks);
+size_t lsm_encode_workspace_size_ex(uint64_t n_items, uint32_t n_blocks, uint64_t out_cap);
 int lsm_encode_blocks(const lsm_items* d_items, const uint32_t* d_block_item_start, uint32_t n_blocks,
                       const lsm_block_params* params, uint8_t* d_out, uint64_t out_cap,
                       uint64_t* d_block_off, int32_t* d_status, void* d_workspace,

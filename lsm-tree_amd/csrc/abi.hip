@@ -147,6 +147,9 @@ uint64_t lsm_encode_bound(uint64_t n_items, uint32_t n_blocks, uint64_t key_byte
 size_t lsm_encode_workspace_size(uint64_t n_items, uint32_t n_blocks) {
   return lsmgpu::encode_workspace_size(n_items, n_blocks);
 }
+size_t lsm_encode_workspace_size_ex(uint64_t n_items, uint32_t n_blocks, uint64_t out_cap) {
+  return lsmgpu::encode_workspace_size_ex(n_items, n_blocks, out_cap);
+}
 
 int lsm_encode_blocks(const lsm_items* d_items, const uint32_t* d_block_item_start, uint32_t n_blocks,
                       const lsm_block_params* params, uint8_t* d_out, uint64_t out_cap, uint64_t* d_block_off,
@@ -166,7 +169,7 @@ int lsm_encode_blocks(const lsm_items* d_items, const uint32_t* d_block_item_sta
   if (!d_workspace || workspace_bytes < lsmgpu::encode_workspace_size(d_items->n_items, n_blocks))
     return LSM_BAD_ARG;
   hipError_t e = lsmgpu::launch_encode(*d_items, d_block_item_start, n_blocks, *params, d_out, out_cap,
-                                       d_block_off, d_status, d_workspace, (hipStream_t)stream);
+                                       d_block_off, d_status, d_workspace, workspace_bytes, (hipStream_t)stream);
   return e == hipSuccess ? LSM_OK : set_hip_error(e, "lsm_encode_blocks");
 }
 

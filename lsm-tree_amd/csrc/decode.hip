@@ -811,39 +811,46 @@ __global__ __launch_bounds__(kBigWaves * kWave) void decode_deferred_staged_kern
 // writer's up-to-4-MiB data blocks, writer/mod.rs:193-198; full block
 // indexes): decode_chunked walks such a block on ONE workgroup, chunk by
 // chunk.  Here its work is cut into units that any workgroup takes:
-//   plan   (the last decode_big_kernel workgroup, once every block is listed):
+//   plan   (decode_huge_plan_kernel, one workgroup, after decode_big_kernel lists them):
 //          per huge block the header (incl. its checksum) and trailer views
 //          from HBM, its KiB-block and parse-unit counts, prefix sums of both
 //          over the list (contributions in the workspace pool: 64 B per KiB)
-//   work   (decode_huge_kernel, every CU): parse units = kHugeIv restart
-//          intervals, thread per interval, records walked straight from HBM
-//          (walk_interval_at: every oracle check, the LEB cursor for rare
-//          shapes); hash units = kHugeKib KiB blocks' XXH3 contributions
+//   work   (decode_huge_kernel, every CU): units = kHugeWin-byte windows of a
+//          block's span.  A unit stages its window (+ kHugeOverlap) in LDS by
+//          LDS-DMA, finds the restart intervals that start in it (a 256-way
+//          search of the binary index in HBM, two or three round trips),
+//          walks them from LDS (thread per interval, walk_interval_at: every
+//          oracle check, the LEB cursor for rare shapes; from HBM when one
+//          runs past the staged bytes) and computes the XXH3 contributions
+//          of the KiB blocks that start in the window, from LDS too
 //   chain  (decode_huge_chain_kernel): eight single-wave chains per block
 //          (accumulator k on wave k, xxh3_chain_wave), the last one to finish
 //          merges the tail, compares the checksum and writes the status
 // A block whose header fails, or that no longer fits the pool, goes to the
 // general path (defer2) as before: statuses and outputs are the same on both.
-constexpr uint32_t kHugeIv = 256;   // restart intervals per parse unit (thread per interval)
-constexpr uint32_t kHugeKib = 32;   // KiB blocks per hash unit (8 per wave, loads issued together)
+constexpr uint32_t kHugeWin = 32 * 1024;               // span bytes per unit
+constexpr uint32_t kHugeOverlap = 8 * 1024 - 256;      // staged past the window (intervals that straddle it)
+constexpr uint32_t kHugeStage = kHugeWin + kHugeOverlap;
+constexpr uint32_t kHugeLds = kHugeStage + kStagePad + 64;
 constexpr uint32_t kHugeGrid = 2048;
+constexpr uint32_t kHugeChainGrid = 1024, kHugeChainLds = 40 * 1024;
 
 struct HugeRec {
   BlockMeta m;         // header view, trailer fields merged in: m.st = trailer status (header checks passed)
   uint64_t span0, item_base;
   uint64_t acc[8];     // chain results (accumulator k from chain wave k)
   uint32_t b, nbk, accepted, parse_bad;
-  uint32_t done, pad[3];
+  uint32_t done, span, pad[2];  // span: the block's 16-B-aligned byte span
 };
 static_assert(sizeof(HugeRec) % 16 == 0, "HugeRec layout");
 
 struct HugeHdr {
   uint64_t total_kib;  // contributions over every accepted block
   uint32_t n3;         // listed huge blocks (HugeRec entries)
-  uint32_t total_pu;   // parse units
+  uint32_t total_pu;   // work units (kHugeWin windows)
 };
 
-// Pool: [HugeHdr | 256][kpre u64 x (n + 1)][ppre u64 x (n + 1)][HugeRec x n][contributions, 64 B per KiB].
+// Pool: [HugeHdr | 256][kpre u64 x (n + 1)][upre u64 x (n + 1)][HugeRec x n][contributions, 64 B per KiB].
 struct HugeLayout {
   HugeHdr* hdr;
   uint64_t* kpre;
@@ -899,7 +906,7 @@ __device__ void huge_plan(const DecodeParams& P, uint64_t* sh, uint32_t nthr) {
     bool acc = false;
     uint32_t b = 0;
     BlockMeta m{};
-    uint64_t span0 = 0, item_base = 0;
+    uint64_t span0 = 0, item_base = 0, span = 0;
     if (i < n) {
       b = gload(P.defer3_list, i);
       const uint64_t off = gload(P.block_off, b), end = gload(P.block_off, b + 1);
@@ -913,7 +920,8 @@ __device__ void huge_plan(const DecodeParams& P, uint64_t* sh, uint32_t nthr) {
         const uint32_t plen = m.len - kHdrLen;
         nbk = hash ? (plen - 1) / 1024 : 0;  // (plen > 72 KiB here: the long path)
         meta_trailer(gbase, P.expect_type, cap, m, P.compact);  // (after the payload checksum in oracle order)
-        npu = m.st == ST_OK ? (m.bin_len + kHugeIv - 1) / kHugeIv : 0;
+        span = ((max(end, off) + 15) & ~15ULL) - span0;
+        npu = (nbk || m.st == ST_OK) ? (span + kHugeWin - 1) / kHugeWin : 0;
       }
     }
     const uint64_t ik = wave_incl_scan_u64(nbk), ip = wave_incl_scan_u64(npu);
@@ -938,6 +946,7 @@ __device__ void huge_plan(const DecodeParams& P, uint64_t* sh, uint32_t nthr) {
       r->accepted = acc;
       r->parse_bad = 0;
       r->done = 0;
+      r->span = (uint32_t)span;
       gstore(L.kpre, i, kp);
       gstore(L.ppre, i, pp);
       if (!acc) defer2_block(P, b);
@@ -953,6 +962,11 @@ __device__ void huge_plan(const DecodeParams& P, uint64_t* sh, uint32_t nthr) {
     L.hdr->total_pu = (uint32_t)sh[33];
     L.hdr->n3 = n;
   }
+}
+
+__global__ __launch_bounds__(1024) void decode_huge_plan_kernel(DecodeParams P) {
+  __shared__ uint64_t sh[40];
+  huge_plan(P, sh, 1024);
 }
 
 // Large blocks (SURVEY configs[4]: 16 / 64 KiB data blocks) listed by the
@@ -1166,18 +1180,6 @@ __global__ __launch_bounds__(kBigGWaves * kWave) void decode_big_kernel(DecodePa
 #endif
     X = Xn;
   }
-  if (P.huge_pool) {  // the last workgroup to finish plans the huge blocks (every listing is done)
-    __syncthreads();
-    if (tid == 0) {
-      __threadfence();
-      sync->a_done = atomicAdd(P.big_done, 1u) == gridDim.x - 1;
-    }
-    __syncthreads();
-    if (sync->a_done) {
-      __threadfence();
-      huge_plan(P, rec, kThreads);
-    }
-  }
 #if defined(LSM_DIAG) && !defined(LSM_DIAG_NOTIME)
   if (tid == 0) {
     for (int i = 0; i < 8; ++i) atomicAdd(&g_dec_phase[i], (unsigned long long)ph[i]);
@@ -1198,113 +1200,146 @@ __device__ __forceinline__ uint32_t last_le(const uint64_t* a, uint32_t n, uint6
   return lo;
 }
 
-// Huge-block work units (see huge_plan): parse units first, then hash units.
+// Huge-block work units (see huge_plan): unit u = window c of block i.
 __global__ __launch_bounds__(256) void decode_huge_kernel(DecodeParams P) {
+  extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
+  uint8_t* stage = smem + 64;
+  uint32_t* cnt = reinterpret_cast<uint32_t*>(smem);  // [0, 1]: search counts; [2..]: per-wave partials
   const HugeHdr* hp = reinterpret_cast<const HugeHdr*>(P.huge_pool);
   const uint32_t n = hp->n3;
   if (!n) return;
   const HugeLayout L = huge_layout(P, n);
-  const uint32_t tpu = hp->total_pu;
-  const uint64_t tk = hp->total_kib;
-  const uint64_t units = tpu + (tk + kHugeKib - 1) / kHugeKib;
-  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int q = lane & 3, s = lane >> 2;
-  const uint64_t k0 = kLongSecret.acc[s + 2 * q], k1 = kLongSecret.acc[s + 2 * q + 1];
-  for (uint64_t u = blockIdx.x; u < units; u += gridDim.x) {
-    if (u < tpu) {  // kHugeIv restart intervals of one block, thread per interval
-      const uint32_t i = last_le(L.ppre, n, u);
-      const HugeRec* r = L.rec + i;
-      if (!r->accepted) continue;  // (uniform)
-      const BlockMeta m = r->m;
-      const uint32_t iv = (uint32_t)(u - gload(L.ppre, i)) * kHugeIv + tid;
+  const uint32_t units = hp->total_pu;
+  const uint32_t tid = threadIdx.x, lane = tid & 63;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid / kWave);
+  const bool hash = !(P.flags & LSM_DECODE_PAYLOAD_VERIFIED);
+  for (uint32_t u = blockIdx.x; u < units; u += gridDim.x) {
+    const uint32_t i = last_le(L.ppre, n, u);
+    const HugeRec* r = L.rec + i;
+    if (!r->accepted) continue;  // (uniform)
+    const BlockMeta m = r->m;
+    const TrailerInfo t = trailer_of(m);
+    const uint32_t span = r->span;
+    const uint8_t* gbase = P.blocks + r->span0;
+    const uint32_t cs = (uint32_t)(u - gload(L.ppre, i)) * kHugeWin;
+    const uint32_t ce = min(cs + kHugeWin, span), ss = min(ce + kHugeOverlap, span);
+    {  // stage [cs, ss): wave w moves 1-KiB pieces w, w + 4, ...
+      const uint32_t chunks = (ss - cs + 15) >> 4;
+      const uint8_t* src = gbase + cs + 16 * lane;
+      for (uint32_t c = wave; c * kWave < chunks; c += 4)
+        if (c * kWave + lane < chunks)
+          __builtin_amdgcn_global_load_lds((gbl_void_t*)(src + 1024 * c), (lds_void_t*)(stage + 1024 * c), 16, 0, 0);
+    }
+    // the intervals that start in [cs, ce): [r0, r1), by a 256-way search of the binary index (HBM)
+    const bool parse = m.st == ST_OK;
+    uint32_t r0 = 0, r1 = 0;
+    if (parse) {
+      const uint32_t nint = t.bin_len, p0 = m.p0;
+      uint32_t lo0 = 0, hi0 = nint, lo1 = 0, hi1 = nint;  // r0 in [lo0, hi0], r1 in [lo1, hi1]
+      while (hi0 > lo0 || hi1 > lo1) {  // (uniform) each round narrows both ranges 256-fold
+        const uint32_t len0 = hi0 - lo0, len1 = hi1 - lo1;
+        const uint32_t st0 = (len0 + 255) / 256, st1 = (len1 + 255) / 256;
+        const uint32_t x0 = lo0 + tid * st0, x1 = lo1 + tid * st1;
+        const bool b0 = x0 < hi0 && p0 + bin_get(gbase, p0, t, x0) < cs;
+        const bool b1 = x1 < hi1 && p0 + bin_get(gbase, p0, t, x1) < ce;
+        const uint32_t c0 = (uint32_t)__builtin_popcountll(__ballot(b0)), c1 = (uint32_t)__builtin_popcountll(__ballot(b1));
+        if (lane == 0) cnt[2 + wave] = c0, cnt[6 + wave] = c1;
+        lds_barrier();
+        const uint32_t k0 = cnt[2] + cnt[3] + cnt[4] + cnt[5], k1 = cnt[6] + cnt[7] + cnt[8] + cnt[9];
+        lds_barrier();
+        // k samples lie below the bound (a prefix of them, for monotone starts): the
+        // answer is in (lo + (k - 1) st, lo + k st]; with st = 1 the range closes
+        if (len0) {
+          const uint32_t nlo = k0 ? lo0 + (k0 - 1) * st0 + 1 : lo0;
+          hi0 = min(hi0, lo0 + k0 * st0);
+          lo0 = min(nlo, hi0);
+        }
+        if (len1) {
+          const uint32_t nlo = k1 ? lo1 + (k1 - 1) * st1 + 1 : lo1;
+          hi1 = min(hi1, lo1 + k1 * st1);
+          lo1 = min(nlo, hi1);
+        }
+      }
+      // the same bound gives the same answer in the neighbouring unit, and the first
+      // / last windows take every interval before / after: each interval is walked
+      // at least once even when the binary index is not monotone (its walk then fails)
+      r0 = cs == 0 ? 0 : lo0;
+      r1 = ce == span ? nint : lo1;
+    }
+    vm_wait<0>();
+    lds_barrier();
+    const uint8_t* sbase = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(stage) - cs);  // span-relative
+    if (hash && r->nbk) {  // the KiB blocks that start in [cs, ce)
+      const uint32_t p0 = m.p0, nbk = r->nbk;
+      const uint32_t n0 = min(nbk, cs > p0 ? (cs - p0 + 1023) / 1024 : 0u);
+      const uint32_t n1 = min(nbk, ce > p0 ? (ce - p0 + 1023) / 1024 : 0u);
+      if (n1 > n0)
+        xxh3_kib_contribs(sbase, p0 + 1024 * n0, (n1 - n0) * 1024 + 1, &kLongSecret,
+                          L.contrib + 8 * (gload(L.kpre, i) + n0), wave, 4);
+    }
+    if (parse) {
+      const uint64_t item_base = r->item_base;
+      const uint32_t p0 = m.p0;
       bool ok = true;
-      if (iv < m.bin_len) {
-        const uint64_t item_base = r->item_base;
-        ok = walk_interval(P.blocks + r->span0, m.p0, m, iv, [&](uint32_t j, const ItemFields& f) {
+      for (uint32_t x = r0 + tid; x < r1; x += 256) {
+        const uint32_t s_cur = bin_get(gbase, p0, t, x);
+        const bool last = x + 1 == t.bin_len;
+        const uint32_t stop = last ? t.rec_end : bin_get(gbase, p0, t, x + 1);
+        const bool staged = p0 + s_cur >= cs && stop <= t.rec_end && (p0 + stop + kChunkReadAhead <= ss || ss == span);
+        ok &= walk_interval_at(staged ? sbase : gbase, p0, m, t, x, s_cur, stop, [&](uint32_t j, const ItemFields& f) {
           emit_global(P.out, item_base + j, f, P.seqno_add, P.compact);
         });
       }
       const uint64_t bad = __ballot(!ok);
       if (bad && lane == (uint32_t)__builtin_ctzll(bad)) atomicOr(const_cast<uint32_t*>(&r->parse_bad), 1u);
-    } else {  // kHugeKib KiB blocks' contributions: wave w takes g0 + w, g0 + w + 4, ...
-      const uint64_t g0 = (u - tpu) * kHugeKib, g1 = min(tk, g0 + kHugeKib);
-      uint32_t i = last_le(L.kpre, n, g0);
-      constexpr uint32_t kPer = kHugeKib / 4;
-      const uint8_t* base[kPer];
-      uint32_t pos[kPer];
-      uint64_t gg[kPer];
-      bool live[kPer];
-#pragma unroll
-      for (uint32_t j = 0; j < kPer; ++j) {
-        const uint64_t g = g0 + wave + 4 * j;
-        live[j] = g < g1;
-        gg[j] = g;
-        base[j] = P.blocks;
-        pos[j] = 0;
-        if (live[j]) {
-          while (gload(L.kpre, i + 1) <= g) ++i;
-          const HugeRec* r = L.rec + i;
-          live[j] = r->accepted != 0;
-          base[j] = P.blocks + r->span0;
-          pos[j] = r->m.p0 + (uint32_t)(g - gload(L.kpre, i)) * 1024 + 16 * lane;
-        }
-      }
-      Win16 w[kPer];
-#pragma unroll
-      for (uint32_t j = 0; j < kPer; ++j) w[j] = live[j] ? read_win16(base[j], pos[j]) : Win16{0, 0};
-#pragma unroll
-      for (uint32_t j = 0; j < kPer; ++j) {
-        uint64_t c0 = 0, c1 = 0;
-        stripe_part(w[j], k0, k1, c0, c1);
-        c0 = quad_group_sum64(c0);
-        c1 = quad_group_sum64(c1);
-        if (live[j] && lane < 4) {
-          gstore(L.contrib, 8 * gg[j] + 2 * q, c0);
-          gstore(L.contrib, 8 * gg[j] + 2 * q + 1, c1);
-        }
-      }
     }
+    lds_barrier();  // (the next unit rewrites the stage)
   }
 }
 
 // Chains of the huge blocks: single-wave workgroup pairs (block i, accumulator
-// k); the last of a block's eight chains merges, checks and writes its status
-// (oracle order: payload checksum, then trailer, then parse).
+// k).  The merge runs in decode_huge_finish_kernel: the kernel boundary makes
+// the eight results visible (an agent-scope fence per chain would write back
+// the XCD's whole L2).
 __global__ __launch_bounds__(64) void decode_huge_chain_kernel(DecodeParams P) {
+  const HugeHdr* hp = reinterpret_cast<const HugeHdr*>(P.huge_pool);
+  const uint32_t n = hp->n3;
+  if (!n || (P.flags & LSM_DECODE_PAYLOAD_VERIFIED)) return;
+  const HugeLayout L = huge_layout(P, n);
+  for (uint64_t p = blockIdx.x; p < 8ULL * n; p += gridDim.x) {
+    const uint32_t i = (uint32_t)(p >> 3), k = (uint32_t)(p & 7);
+    HugeRec* r = L.rec + i;
+    if (!r->accepted) continue;
+    uint64_t a0, a1;
+    xxh3_acc_init((int)(k >> 1), a0, a1);
+    const uint64_t x = xxh3_chain_wave(L.contrib + 8 * gload(L.kpre, i), r->nbk, k, (k & 1) ? a1 : a0,
+                                       kLongSecret.acc[16 + k]);
+    if ((threadIdx.x & 63) == 0) r->acc[k] = x;
+  }
+}
+
+// Wave per huge block: tail merge, checksum compare, status (oracle order:
+// payload checksum, then trailer, then parse).
+__global__ __launch_bounds__(256) void decode_huge_finish_kernel(DecodeParams P) {
   const HugeHdr* hp = reinterpret_cast<const HugeHdr*>(P.huge_pool);
   const uint32_t n = hp->n3;
   if (!n) return;
   const HugeLayout L = huge_layout(P, n);
   const bool hash = !(P.flags & LSM_DECODE_PAYLOAD_VERIFIED);
-  const int lane = threadIdx.x & 63;
-  for (uint64_t p = blockIdx.x; p < 8ULL * n; p += gridDim.x) {
-    const uint32_t i = (uint32_t)(p >> 3), k = (uint32_t)(p & 7);
-    HugeRec* r = L.rec + i;
+  const int lane = threadIdx.x & 63, q = lane & 3;
+  for (uint32_t i = (blockIdx.x * blockDim.x + threadIdx.x) / 64; i < n; i += gridDim.x * blockDim.x / 64) {
+    const HugeRec* r = L.rec + i;
     if (!r->accepted) continue;
     const BlockMeta m = r->m;
     const int32_t tail_st = m.st != ST_OK ? m.st : r->parse_bad ? (int32_t)ST_PARSE : (int32_t)ST_OK;
-    if (!hash) {
-      if (k == 0 && lane == 0) gstore(P.status, r->b, tail_st);
-      continue;
+    int32_t st = tail_st;
+    if (hash) {
+      uint64_t lo, hi;
+      xxh3_wave_tail_merge(P.blocks + r->span0, m.p0, m.len - kHdrLen, &kLongSecret, r->acc[2 * q], r->acc[2 * q + 1],
+                           lo, hi);
+      if (lo != m.ck_lo || hi != m.ck_hi) st = ST_CKSUM;
     }
-    uint64_t a0, a1;
-    xxh3_acc_init((int)(k >> 1), a0, a1);
-    const uint64_t x = xxh3_chain_wave(L.contrib + 8 * gload(L.kpre, i), r->nbk, k, (k & 1) ? a1 : a0,
-                                       kLongSecret.acc[16 + k]);
-    uint32_t last = 0;
-    if (lane == 0) {
-      r->acc[k] = x;
-      __threadfence();
-      last = atomicAdd(&r->done, 1u) == 7;
-    }
-    if (!__shfl((int)last, 0)) continue;
-    __threadfence();
-    const int q = lane & 3;
-    const uint64_t c0 = __hip_atomic_load(&r->acc[2 * q], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    const uint64_t c1 = __hip_atomic_load(&r->acc[2 * q + 1], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-    uint64_t lo, hi;
-    xxh3_wave_tail_merge(P.blocks + r->span0, m.p0, m.len - kHdrLen, &kLongSecret, c0, c1, lo, hi);
-    if (lane == 0) gstore(P.status, r->b, (lo != m.ck_lo || hi != m.ck_hi) ? (int32_t)ST_CKSUM : tail_st);
+    if (lane == 0) gstore(P.status, r->b, st);
   }
 }
 
@@ -1550,7 +1585,7 @@ static size_t counts_bytes(uint32_t n_blocks) { return ((size_t)n_blocks * 8 + 2
 static size_t tiles_bytes(uint32_t n_blocks) { return (scan_tiles(n_blocks) * 8 + 255) / 256 * 256; }
 static size_t defer_bytes(uint32_t n_blocks) { return ((size_t)n_blocks * 4 + 255) / 256 * 256; }
 
-// counts | scan tiles | 256 B of counters (defer, defer2, defer3, big_done) | three block lists
+// counts | scan tiles | 256 B of counters (defer, defer2, defer3) | three block lists
 size_t decode_workspace_size(uint32_t n_blocks) {
   return counts_bytes(n_blocks) + tiles_bytes(n_blocks) + 256 + 3 * defer_bytes(n_blocks);
 }
@@ -1577,7 +1612,6 @@ hipError_t launch_decode(const DecodeParams& P0, void* ws, size_t ws_bytes, hipS
   P.defer_count = (uint32_t*)dws;
   P.defer2_count = (uint32_t*)dws + 1;
   P.defer3_count = (uint32_t*)dws + 2;
-  P.big_done = (uint32_t*)dws + 3;
   P.defer_list = (uint32_t*)(dws + 256);
   P.defer2_list = (uint32_t*)(dws + 256 + defer_bytes(P.n_blocks));
   P.defer3_list = (uint32_t*)(dws + 256 + 2 * defer_bytes(P.n_blocks));
@@ -1628,6 +1662,8 @@ hipError_t launch_decode(const DecodeParams& P0, void* ws, size_t ws_bytes, hipS
     if ((e = hipLaunchKernel(big_k[variant], dim3(bgrid), dim3(kBigGWaves * kWave), args, kBigGLds, st)) != hipSuccess)
       return e;
   }
+  if (P.huge_pool && bgrid)  // the huge blocks the big-block kernel listed: plan (rejects go to defer2)
+    hipLaunchKernelGGL(decode_huge_plan_kernel, dim3(1), dim3(1024), 0, st, P);
   const uint32_t dgrid = P.n_blocks < 1024 ? P.n_blocks : 1024;
   if (dgrid) {
     DecodeParams P2 = P;
@@ -1638,9 +1674,12 @@ hipError_t launch_decode(const DecodeParams& P0, void* ws, size_t ws_bytes, hipS
     if ((e = set_lds_attr((const void*)decode_deferred_staged_kernel, big, &done_big)) != hipSuccess) return e;
     hipLaunchKernelGGL(decode_deferred_staged_kernel, dim3(dgrid), dim3(kBigWaves * kWave), big, st, P2);
   }
-  if (P.huge_pool && bgrid) {  // (the plan ran at the end of the big-block kernel)
-    hipLaunchKernelGGL(decode_huge_kernel, dim3(kHugeGrid), dim3(256), 0, st, P);
-    hipLaunchKernelGGL(decode_huge_chain_kernel, dim3(kHugeGrid), dim3(64), 0, st, P);
+  if (P.huge_pool && bgrid) {
+    hipLaunchKernelGGL(decode_huge_kernel, dim3(kHugeGrid), dim3(256), kHugeLds, st, P);
+    // (an unused 40 KiB LDS request: at most four chain workgroups per CU, one per
+    // SIMD, so no two serial chains share a SIMD's quarter-rate multiplies)
+    hipLaunchKernelGGL(decode_huge_chain_kernel, dim3(kHugeChainGrid), dim3(64), kHugeChainLds, st, P);
+    hipLaunchKernelGGL(decode_huge_finish_kernel, dim3(256), dim3(256), 0, st, P);
   }
   return hipGetLastError();
 }

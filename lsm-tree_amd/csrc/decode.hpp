@@ -45,7 +45,6 @@ struct DecodeParams {
   uint32_t* defer2_list;
   uint32_t* defer3_count;  // workspace: blocks larger than the general path's stage (decode_big_kernel lists them)
   uint32_t* defer3_list;
-  uint32_t* big_done;      // workspace: decode_big_kernel workgroups finished (the last one plans the huge blocks)
   uint8_t* huge_pool;      // workspace past decode_workspace_size (null: huge blocks take the general path)
   uint64_t huge_pool_bytes;
   uint64_t seqno_add;     // added to every decoded seqno (Scanner's global_seqno, scanner.rs:84)

@@ -39,6 +39,7 @@ namespace lsmgpu {
 // written, by the LDS image they need (e2_need), by 1-wave workgroups with a
 // 20 KiB (medium) or 96 KiB (big) image, or straight in HBM (E3, huge).
 constexpr uint32_t kPlanHuge = 1, kPlanBad = 2, kPlanMedium = 4, kPlanBig = 8;
+constexpr uint32_t kPlanHugeGpu = 16;  // a huge block the whole-GPU E3 path took over (not the one-workgroup E3)
 constexpr uint32_t kImgMedium = 20 * 1024;
 constexpr uint32_t kImgBig = 96 * 1024;
 #ifndef LSM_LIST_BW
@@ -128,6 +129,9 @@ struct EncodeParams {
   uint32_t hb_valid;
   uint32_t* hb_fix;     // [1] set by E1 when it left keys of more than 16 bytes (kNeedHash)
   unsigned long long* phase;  // diagnostic builds: per-phase cycle totals [16]
+  uint8_t* huge_pool;   // workspace past encode_workspace_size (null: E3 one workgroup per block)
+  uint64_t huge_pool_bytes;
+  uint32_t huge_cap;    // huge-list entries the pool's layout provides
 };
 
 __device__ __forceinline__ bool is_index(const EncodeParams& P) { return P.type == 1; }
@@ -801,6 +805,7 @@ __device__ __host__ __forceinline__ bool group_fits(uint64_t n, uint64_t kspan, 
                                                     uint32_t hash_w) {
   return n <= kGItems && kspan + 15 <= kGKeys && vspan + 15 <= kGVals && total + 15 <= kGImg && hash_w <= kGHash;
 }
+
 
 // ---------------------------------------------------------------- E1: plan
 // A 256-thread workgroup owns kPlanBlocks consecutive blocks and walks their
@@ -2080,7 +2085,7 @@ __global__ __launch_bounds__(kE3Threads) void encode_large_kernel(EncodeParams P
       if (lane == 0) img[p0 + pl.recs] = kTrailerMarker;
       write_trailer_bytes(img, p0 + plen - kTrailerLen, ri, step, pl.bin_len, bin_off, pl.hash_w, hash_off, n);
     }
-    __threadfence();  // the block's bytes, for the re-reads below
+    __builtin_amdgcn_fence(__ATOMIC_SEQ_CST, "workgroup");  // the block's bytes, for this workgroup's re-reads below
     __syncthreads();
     uint64_t lo = 0, hi = 0;
     if (plen > 240) {
@@ -2112,17 +2117,333 @@ __global__ __launch_bounds__(kE3Threads) void encode_large_kernel(EncodeParams P
   }
 }
 
+// ---------------------------------------- E3 across the GPU (workspace pool)
+// The one-workgroup E3 above writes a 1-4 MiB block's records with 512
+// threads and carries its XXH3 chain on one wave, 64 KiB at a time.  With the
+// pool (lsm_encode_workspace_size_ex) the huge blocks are collected by the
+// size scan and cut into units any workgroup takes:
+//   plan     (one workgroup) per collected block its record units, KiB-block
+//            count and the prefix sums of both; accepted blocks are re-flagged
+//            kPlanHugeGpu (the one-workgroup E3 passes them over)
+//   records  record units of kEHugeItems items (thread per item at its E1
+//            offset; blocks of <= kGItems items: one unit with a workgroup
+//            scan), then one tail unit per block (hash-index votes, marker,
+//            trailer)
+//   hash     units of kEHugeKib KiB blocks: XXH3 contributions into the pool
+//   chain    eight single-wave chains per block; the last one merges the tail
+//            and writes the header and the status
+constexpr uint32_t kEHugeItems = 1024;  // items per record unit (four per thread)
+constexpr uint32_t kEHugeKib = 32;      // KiB blocks per hash unit (eight per wave)
+constexpr uint32_t kEHugeGrid = 2048;
+
+struct EncHuge {
+  uint64_t dst_off;
+  uint64_t acc[8];
+  uint32_t b, s, n, total;
+  uint32_t nbk, nru, accepted, done;
+  uint32_t pad[2];
+};
+static_assert(sizeof(EncHuge) % 16 == 0, "EncHuge layout");
+struct EncHugeHdr {
+  uint64_t total_kib;
+  uint32_t count;      // collected (atomic; may exceed the capacity: the rest stay with the one-workgroup E3)
+  uint32_t n3;         // planned entries
+  uint64_t total_units;
+};
+// Pool: [hdr | 256][list u32 x cap][kpre u64 x (cap + 1)][upre u64 x (cap + 1)][EncHuge x cap][contributions]
+struct EncHugeLayout {
+  EncHugeHdr* hdr;
+  uint32_t* list;
+  uint64_t* kpre;
+  uint64_t* upre;
+  EncHuge* rec;
+  uint64_t* contrib;
+  uint64_t cap_kib;
+};
+__host__ __device__ __forceinline__ uint64_t enc_huge_fixed_bytes(uint64_t cap) {
+  return (256 + ((4 * cap + 15) & ~15ULL) + 16 * (cap + 1) + sizeof(EncHuge) * cap + 255) & ~255ULL;
+}
+__device__ __forceinline__ EncHugeLayout enc_huge_layout(const EncodeParams& P) {
+  EncHugeLayout L;
+  uint8_t* b = P.huge_pool;
+  const uint64_t cap = P.huge_cap;
+  L.hdr = reinterpret_cast<EncHugeHdr*>(b);
+  L.list = reinterpret_cast<uint32_t*>(b + 256);
+  L.kpre = reinterpret_cast<uint64_t*>(b + 256 + ((4 * cap + 15) & ~15ULL));
+  L.upre = L.kpre + (cap + 1);
+  L.rec = reinterpret_cast<EncHuge*>(L.upre + (cap + 1));
+  const uint64_t fixed = enc_huge_fixed_bytes(cap);
+  L.contrib = reinterpret_cast<uint64_t*>(b + fixed);
+  L.cap_kib = (P.huge_pool_bytes - fixed) / 64;
+  return L;
+}
+
+__device__ __forceinline__ uint32_t last_le_u64(const uint64_t* a, uint32_t n, uint64_t v) {
+  uint32_t lo = 0, hi = n;
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (a[mid] <= v) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
+
+// One workgroup of 1024 threads.
+__global__ __launch_bounds__(1024) void encode_huge_plan_kernel(EncodeParams P) {
+  __shared__ uint64_t sh[40];
+  const EncHugeLayout L = enc_huge_layout(P);
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const uint32_t n = min(L.hdr->count, P.huge_cap);
+  if (tid == 0) sh[32] = 0, sh[33] = 0;
+  __syncthreads();
+  for (uint32_t c = 0; c < n; c += 1024) {
+    const uint32_t i = c + tid;
+    uint64_t nbk = 0, nu = 0;
+    bool acc = false;
+    EncHuge h{};
+    if (i < n) {
+      h.b = L.list[i];
+      h.dst_off = P.block_off[h.b];
+      const uint64_t dst_end = P.block_off[h.b + 1];
+      h.s = P.starts[h.b];
+      h.n = P.starts[h.b + 1] - h.s;
+      h.total = (uint32_t)(dst_end - h.dst_off);
+      acc = dst_end <= P.out_cap;  // (else the one-workgroup E3 reports the overflow)
+      nbk = (h.total - kHdrLen - 1) / 1024;  // (payload > 96 KiB: the long path)
+      h.nru = h.n <= kGItems ? 1 : (h.n + kEHugeItems - 1) / kEHugeItems;
+      nu = acc ? h.nru + 1 : 0;
+      nbk = acc ? nbk : 0;
+    }
+    const uint64_t ik = wave_incl_scan_u64(nbk), iu = wave_incl_scan_u64(nu);
+    if (lane == 63) sh[wave] = ik, sh[16 + wave] = iu;
+    __syncthreads();
+    uint64_t bk = sh[32], bu = sh[33], tk = 0, tu = 0;
+    for (uint32_t w = 0; w < 16; ++w) {
+      bk += w < wave ? sh[w] : 0;
+      bu += w < wave ? sh[16 + w] : 0;
+      tk += sh[w];
+      tu += sh[16 + w];
+    }
+    const uint64_t kp = bk + ik - nbk;
+    if (i < n) {
+      acc = acc && kp + nbk <= L.cap_kib;  // (the pool holds the contributions of a prefix of the list)
+      h.nbk = (uint32_t)nbk;
+      h.accepted = acc;
+      h.done = 0;
+      L.rec[i] = h;
+      L.kpre[i] = kp;
+      L.upre[i] = bu + iu - nu;
+      if (acc) P.plans[h.b].step_flags = (P.plans[h.b].step_flags & 0xFF) | (kPlanHugeGpu << 8);
+    }
+    __syncthreads();
+    if (tid == 0) sh[32] += tk, sh[33] += tu;
+    __syncthreads();
+  }
+  if (tid == 0) {
+    L.kpre[n] = sh[32];
+    L.upre[n] = sh[33];
+    L.hdr->total_kib = sh[32];
+    L.hdr->total_units = sh[33];
+    L.hdr->n3 = n;
+  }
+}
+
+// Record units (u < nru of a block) and the tail unit (u == nru).
+__global__ __launch_bounds__(256) void encode_huge_records_kernel(EncodeParams P) {
+  __shared__ uint32_t hlo[kE3HashChunk], hhi[kE3HashChunk];
+  __shared__ uint32_t psum[4];
+  const EncHugeLayout L = enc_huge_layout(P);
+  const uint32_t n3 = L.hdr->n3;
+  if (!n3) return;
+  const uint64_t units = L.hdr->total_units;
+  const uint32_t tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid >> 6;
+  for (uint64_t u = blockIdx.x; u < units; u += gridDim.x) {
+    const uint32_t i = last_le_u64(L.upre, n3, u);
+    const EncHuge h = L.rec[i];
+    if (!h.accepted) continue;  // (uniform; rejected blocks own no units)
+    const uint32_t k = (uint32_t)(u - L.upre[i]);
+    const BlockPlan pl = P.plans[h.b];
+    const uint32_t step = pl.step_flags & 0xFF;
+    const uint32_t ri = is_index(P) ? 1 : P.ri;
+    const uint32_t plen = h.total - kHdrLen;
+    const uint64_t dabs = (uint64_t)(uintptr_t)P.out + h.dst_off;
+    uint8_t* img = reinterpret_cast<uint8_t*>(dabs & ~15ULL);
+    const uint32_t p0 = (uint32_t)(dabs & 15) + kHdrLen;
+    const uint32_t bin_off = pl.recs + 1;
+    if (k < h.nru) {
+      if (h.n <= kGItems) {  // one pass: record offsets from a workgroup scan
+        const uint32_t j = tid;
+        const bool head = j % ri == 0;
+        ItemMeta m;
+        bool bad = false;
+        if (j < h.n) m = load_item_lcp(P, h.s, j, ri, bad);
+        const uint32_t rec = j < h.n ? (uint32_t)item_record_len(P, m, head) : 0u;
+        const uint32_t incl = wave_incl_scan_u32(rec);
+        if (lane == kWave - 1) psum[wave] = incl;
+        __syncthreads();
+        uint32_t base = 0;
+        for (uint32_t w = 0; w < wave; ++w) base += psum[w];
+        const uint32_t roff = base + incl - rec;
+        if (j < h.n) {
+          RecordCopy rc;
+          rc.issue(P, m, head, p0 + roff);
+          rc.store(P, m, head, img);
+          if (head) store_le(img, p0 + bin_off + (j / ri) * step, roff, step);
+        }
+        __syncthreads();  // (psum is rewritten by the next unit)
+      } else {
+        const uint32_t j0 = k * kEHugeItems, j1 = min(h.n, j0 + kEHugeItems);
+        for (uint32_t j = j0 + tid; j < j1; j += 256) {
+          const bool head = j % ri == 0;
+          bool bad = false;
+          const ItemMeta m = load_item_lcp(P, h.s, j, ri, bad);
+          const uint32_t roff = P.erec[h.s + j];
+          RecordCopy rc;
+          rc.issue(P, m, head, p0 + roff);
+          rc.store(P, m, head, img);
+          if (head) store_le(img, p0 + bin_off + (j / ri) * step, roff, step);
+        }
+      }
+      continue;
+    }
+    // tail unit: hash-index votes (LDS passes), marker, trailer
+    const uint32_t hash_off = pl.hash_w ? bin_off + pl.bin_len * step : 0;
+    for (uint32_t base = 0; base < pl.hash_w; base += kE3HashChunk) {
+      const uint32_t lim = min(kE3HashChunk, pl.hash_w - base);
+      for (uint32_t q = tid; q < lim; q += 256) {
+        hlo[q] = 0xFFFFFFFFu;
+        hhi[q] = 0;
+      }
+      __syncthreads();
+      for (uint32_t j = tid; j < h.n; j += 256) {
+        const uint64_t it = (uint64_t)h.s + j;
+        const uint64_t ko = P.it.key_off[it];
+        const uint32_t bk = key_bucket(P, ko, (uint32_t)(P.it.key_off[it + 1] - ko), pl.hash_w);
+        if (bk >= base && bk < base + lim) {
+          atomicMin(&hlo[bk - base], j / ri);
+          atomicMax(&hhi[bk - base], j / ri);
+        }
+      }
+      __syncthreads();
+      for (uint32_t q = tid; q < lim; q += 256) img[p0 + hash_off + base + q] = (uint8_t)bucket_byte(hlo[q], hhi[q]);
+      __syncthreads();
+    }
+    if (wave == 0) {
+      if (lane == 0) img[p0 + pl.recs] = kTrailerMarker;
+      write_trailer_bytes(img, p0 + plen - kTrailerLen, ri, step, pl.bin_len, bin_off, pl.hash_w, hash_off, h.n);
+    }
+  }
+}
+
+// Hash units: contributions of kEHugeKib KiB blocks of the written payloads.
+__global__ __launch_bounds__(256) void encode_huge_contrib_kernel(EncodeParams P) {
+  const EncHugeLayout L = enc_huge_layout(P);
+  const uint32_t n3 = L.hdr->n3;
+  if (!n3) return;
+  const uint64_t tk = L.hdr->total_kib;
+  const uint64_t units = (tk + kEHugeKib - 1) / kEHugeKib;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+  const int q = lane & 3, sq = lane >> 2;
+  const uint64_t k0 = kLongSecret.acc[sq + 2 * q], k1 = kLongSecret.acc[sq + 2 * q + 1];
+  constexpr uint32_t kPer = kEHugeKib / 4;
+  for (uint64_t u = blockIdx.x; u < units; u += gridDim.x) {
+    const uint64_t g0 = u * kEHugeKib, g1 = min(tk, g0 + kEHugeKib);
+    uint32_t i = last_le_u64(L.kpre, n3, g0);
+    const uint8_t* base[kPer];
+    uint32_t pos[kPer];
+    uint64_t gg[kPer];
+    bool live[kPer];
+#pragma unroll
+    for (uint32_t j = 0; j < kPer; ++j) {
+      const uint64_t g = g0 + wave + 4 * j;
+      live[j] = g < g1;
+      gg[j] = g;
+      base[j] = P.out;
+      pos[j] = 0;
+      if (live[j]) {
+        while (L.kpre[i + 1] <= g) ++i;
+        const uint64_t dabs = (uint64_t)(uintptr_t)P.out + L.rec[i].dst_off;
+        base[j] = reinterpret_cast<const uint8_t*>(dabs & ~15ULL);
+        pos[j] = (uint32_t)(dabs & 15) + kHdrLen + (uint32_t)(g - L.kpre[i]) * 1024 + 16 * lane;
+      }
+    }
+    Win16 w[kPer];
+#pragma unroll
+    for (uint32_t j = 0; j < kPer; ++j) w[j] = live[j] ? read_win16(base[j], pos[j]) : Win16{0, 0};
+#pragma unroll
+    for (uint32_t j = 0; j < kPer; ++j) {
+      uint64_t c0 = 0, c1 = 0;
+      stripe_part(w[j], k0, k1, c0, c1);
+      c0 = quad_group_sum64(c0);
+      c1 = quad_group_sum64(c1);
+      if (live[j] && lane < 4) {
+        L.contrib[8 * gg[j] + 2 * q] = c0;
+        L.contrib[8 * gg[j] + 2 * q + 1] = c1;
+      }
+    }
+  }
+}
+
+// (block i, accumulator k) per single-wave workgroup.  The merge and the
+// header run in encode_huge_finish_kernel: the kernel boundary makes the eight
+// results visible (an agent-scope fence per chain would write back the XCD's
+// whole L2).
+__global__ __launch_bounds__(64) void encode_huge_chain_kernel(EncodeParams P) {
+  const EncHugeLayout L = enc_huge_layout(P);
+  const uint32_t n3 = L.hdr->n3;
+  if (!n3) return;
+  for (uint64_t p = blockIdx.x; p < 8ULL * n3; p += gridDim.x) {
+    const uint32_t i = (uint32_t)(p >> 3), k = (uint32_t)(p & 7);
+    EncHuge* r = L.rec + i;
+    if (!r->accepted) continue;
+    uint64_t a0, a1;
+    xxh3_acc_init((int)(k >> 1), a0, a1);
+    const uint64_t x = xxh3_chain_wave(L.contrib + 8 * L.kpre[i], r->nbk, k, (k & 1) ? a1 : a0, kLongSecret.acc[16 + k]);
+    if ((threadIdx.x & 63) == 0) r->acc[k] = x;
+  }
+}
+
+// Wave per huge block: tail merge, header (Header::encode_into), status.
+__global__ __launch_bounds__(256) void encode_huge_finish_kernel(EncodeParams P) {
+  const EncHugeLayout L = enc_huge_layout(P);
+  const uint32_t n3 = L.hdr->n3;
+  if (!n3) return;
+  const int lane = threadIdx.x & 63, q = lane & 3;
+  for (uint32_t i = (blockIdx.x * blockDim.x + threadIdx.x) / 64; i < n3; i += gridDim.x * blockDim.x / 64) {
+    const EncHuge* r = L.rec + i;
+    if (!r->accepted) continue;
+    const uint64_t dabs = (uint64_t)(uintptr_t)P.out + r->dst_off;
+    uint8_t* img = reinterpret_cast<uint8_t*>(dabs & ~15ULL);
+    const uint32_t pad = (uint32_t)(dabs & 15), plen = r->total - kHdrLen;
+    uint64_t lo, hi;
+    xxh3_wave_tail_merge(img, pad + kHdrLen, plen, &kLongSecret, r->acc[2 * q], r->acc[2 * q + 1], lo, hi);
+    write_header_bytes(img, pad, P.type, lo, hi, plen);
+    if (lane == 0) P.status[r->b] = ST_OK;
+  }
+}
+
 // Scan output: block offsets (low 40 bits of the prefix) and the list of the
 // listed blocks (high bits = their running count).
+// With the pool, huge blocks are also collected (hdr->count) for the whole-GPU E3.
 struct EncodeOffOut {
   uint64_t* off;
   const uint64_t* sizes;
   uint32_t* list;
   uint32_t* count;
   uint64_t n;
+  const BlockPlan* plans;
+  uint32_t* huge_count;  // null: no pool
+  uint32_t* huge_list;
+  uint32_t huge_cap;
   __device__ void operator()(uint64_t i, uint64_t prefix) const {
     off[i] = prefix & kOffMask;
-    if (i < n && (sizes[i] & ~kOffMask)) list[prefix >> 40] = (uint32_t)i;
+    if (i < n && (sizes[i] & ~kOffMask)) {
+      list[prefix >> 40] = (uint32_t)i;
+      if (huge_count && (plans[i].step_flags >> 8) == kPlanHuge) {
+        const uint32_t slot = atomicAdd(huge_count, 1u);
+        if (slot < huge_cap) huge_list[slot] = (uint32_t)i;
+      }
+    }
     if (i == n) *count = (uint32_t)(prefix >> 40);
   }
 };
@@ -2153,6 +2474,18 @@ size_t encode_workspace_size(uint64_t n_items, uint32_t n_blocks) {
          al256(scan_tiles(n_blocks) * 8) + al256((size_t)n_items * 4) + al256((size_t)n_items * 2) + 256;
 }
 
+// Huge-list entries for an output of out_cap bytes: a huge block's image
+// exceeds kImgBig, so its encoded bytes exceed 32 KiB (entries past the
+// capacity stay with the one-workgroup E3).
+static uint64_t enc_huge_cap(uint32_t n_blocks, uint64_t out_cap) {
+  return std::min<uint64_t>(n_blocks, out_cap / 32768 + 1);
+}
+
+size_t encode_workspace_size_ex(uint64_t n_items, uint32_t n_blocks, uint64_t out_cap) {
+  return encode_workspace_size(n_items, n_blocks) + enc_huge_fixed_bytes(enc_huge_cap(n_blocks, out_cap)) +
+         64 * (out_cap / 1024 + 1) + 256;
+}
+
 uint64_t encode_bound(uint64_t n_items, uint32_t n_blocks, uint64_t key_bytes, uint64_t val_bytes,
                       const lsm_block_params* params) {
   const float ratio = params ? params->hash_ratio : 0.0f;
@@ -2164,7 +2497,7 @@ uint64_t encode_bound(uint64_t n_items, uint32_t n_blocks, uint64_t key_bytes, u
 
 hipError_t launch_encode(const lsm_items& items, const uint32_t* starts, uint32_t n_blocks,
                          const lsm_block_params& params, uint8_t* out, uint64_t out_cap, uint64_t* block_off,
-                         int32_t* status, void* ws, hipStream_t st) {
+                         int32_t* status, void* ws, size_t ws_bytes, hipStream_t st) {
   EncodeParams P;
   P.it = items;
   P.starts = starts;
@@ -2194,6 +2527,16 @@ hipError_t launch_encode(const lsm_items& items, const uint32_t* starts, uint32_
   P.hbucket = (uint16_t*)w; w += al256((size_t)items.n_items * 2);
   P.hb_fix = (uint32_t*)w;
   hipError_t e;
+  {  // the whole-GPU E3 pool, when the workspace carries one
+    const size_t base = al256(encode_workspace_size(items.n_items, n_blocks));
+    const uint64_t cap = enc_huge_cap(n_blocks, out_cap);
+    const uint64_t fixed = enc_huge_fixed_bytes(cap);
+    const bool pool = cap && ws_bytes >= base + fixed + 64 * 128;
+    P.huge_pool = pool ? (uint8_t*)ws + base : nullptr;
+    P.huge_pool_bytes = pool ? ws_bytes - base : 0;
+    P.huge_cap = pool ? (uint32_t)cap : 0;
+    if (pool && (e = hipMemsetAsync(P.huge_pool, 0, 256, st)) != hipSuccess) return e;
+  }
   P.plan_bpw = plan_blocks_per_wg(items.n_items, n_blocks);
   P.hb_valid = 0;
   const dim3 pgrid((n_blocks + P.plan_bpw - 1) / P.plan_bpw);
@@ -2212,9 +2555,13 @@ hipError_t launch_encode(const lsm_items& items, const uint32_t* starts, uint32_
 #endif
   else
     hipLaunchKernelGGL(encode_plan_kernel<false>, pgrid, dim3(256), 0, st, P);
-  if ((e = launch_excl_scan(P.sizes, n_blocks, tiles,
-                            EncodeOffOut{block_off, P.sizes, P.lists, P.list_count, n_blocks}, st)) != hipSuccess)
-    return e;
+  EncodeOffOut oo{block_off, P.sizes, P.lists, P.list_count, n_blocks, P.plans, nullptr, nullptr, 0};
+  if (P.huge_pool) {
+    oo.huge_count = &reinterpret_cast<EncHugeHdr*>(P.huge_pool)->count;
+    oo.huge_list = reinterpret_cast<uint32_t*>(P.huge_pool + 256);
+    oo.huge_cap = P.huge_cap;
+  }
+  if ((e = launch_excl_scan(P.sizes, n_blocks, tiles, oo, st)) != hipSuccess) return e;
   static uint64_t attr_done = 0;
   if ((e = set_lds_attr((const void*)encode_write_list_kernel, kImgBig, &attr_done)) != hipSuccess) return e;
   const dim3 ggrid((n_blocks + kGRun - 1) / kGRun), gblock(kGThreads);
@@ -2239,6 +2586,14 @@ hipError_t launch_encode(const lsm_items& items, const uint32_t* starts, uint32_
   hipLaunchKernelGGL(encode_write_list_mw_kernel<kListBigWaves>, dim3(512), dim3(kListBigWaves * kWave), kImgBig, st,
                      P, kPlanBig);
 #endif
+  if (P.huge_pool) {  // huge blocks across the GPU (the ones it does not take stay flagged for E3 below)
+    hipLaunchKernelGGL(encode_huge_plan_kernel, dim3(1), dim3(1024), 0, st, P);
+    hipLaunchKernelGGL(encode_huge_records_kernel, dim3(kEHugeGrid), dim3(256), 0, st, P);
+    hipLaunchKernelGGL(encode_huge_contrib_kernel, dim3(kEHugeGrid), dim3(256), 0, st, P);
+    // (an unused 40 KiB LDS request: one chain workgroup per SIMD)
+    hipLaunchKernelGGL(encode_huge_chain_kernel, dim3(1024), dim3(64), 40 * 1024, st, P);
+    hipLaunchKernelGGL(encode_huge_finish_kernel, dim3(256), dim3(256), 0, st, P);
+  }
   hipLaunchKernelGGL(encode_large_kernel, dim3(512), dim3(kE3Threads), 0, st, P);
   return hipGetLastError();
 }

@@ -110,6 +110,8 @@ def lib():
         L.lsm_encode_bound.argtypes = [C.c_uint64, C.c_uint32, C.c_uint64, C.c_uint64, C.POINTER(LsmBlockParams)]
         L.lsm_encode_workspace_size.restype = C.c_size_t
         L.lsm_encode_workspace_size.argtypes = [C.c_uint64, C.c_uint32]
+        L.lsm_encode_workspace_size_ex.restype = C.c_size_t
+        L.lsm_encode_workspace_size_ex.argtypes = [C.c_uint64, C.c_uint32, C.c_uint64]
         L.lsm_encode_blocks.restype = C.c_int
         L.lsm_encode_blocks.argtypes = [C.POINTER(LsmItems), C.c_void_p, C.c_uint32, C.POINTER(LsmBlockParams),
                                         C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t,
@@ -200,7 +202,7 @@ def lib():
 EXPORTED_SYMBOLS = ["lsm_abi_version", "lsm_status_name", "lsm_last_error", "lsm_device_count", "lsm_set_device",
                     "lsm_decode_workspace_size", "lsm_decode_workspace_size_ex", "lsm_decode_blocks", "lsm_decode_blocks_tuned", "lsm_decode_blocks16",
                     "lsm_encode_bound",
-                    "lsm_encode_workspace_size", "lsm_encode_blocks", "lsm_cut_blocks", "lsm_xxh3_128_batch",
+                    "lsm_encode_workspace_size", "lsm_encode_workspace_size_ex", "lsm_encode_blocks", "lsm_cut_blocks", "lsm_xxh3_128_batch",
                     "lsm_point_read_blocks", "lsm_xxh3_128_file_workspace_size", "lsm_xxh3_128_file",
                     "lsm_bloom_calculate_m", "lsm_bloom_shape", "lsm_bloom_filter_size", "lsm_hash64_keys",
                     "lsm_bloom_build", "lsm_bloom_contains", "lsm_lz4_workspace_size", "lsm_lz4_decompress_blocks",
@@ -349,9 +351,10 @@ class Encoder:
         self.ws = None
 
     def encode(self, items, starts, n_blocks, restart_interval=16, hash_ratio=0.0, block_type=BLOCK_DATA,
-               out=None, stream=None):
+               out=None, stream=None, pool=True):
         """items: dict of cuda tensors keys(u8, padded) key_off(i64 n+1) vals(u8, padded) val_off(i64 n+1)
-        seqno(i64) vtype(u8) [handle_off(i64) handle_size(i32)]; starts: int32 cuda [n_blocks+1]."""
+        seqno(i64) vtype(u8) [handle_off(i64) handle_size(i32)]; starts: int32 cuda [n_blocks+1].
+        pool=False: the base workspace only (blocks > 96 KiB on one workgroup each)."""
         torch = _torch()
         n_items = items["seqno"].numel()
         it = LsmItems()
@@ -368,7 +371,8 @@ class Encoder:
         key_bytes = int(items["keys"].numel())
         val_bytes = int(items["vals"].numel()) if "vals" in items else 0
         bound = lib().lsm_encode_bound(n_items, n_blocks, key_bytes, val_bytes, C.byref(params))
-        need = lib().lsm_encode_workspace_size(n_items, n_blocks)
+        need = (lib().lsm_encode_workspace_size_ex(n_items, n_blocks, bound) if pool
+                else lib().lsm_encode_workspace_size(n_items, n_blocks))
         if self.ws is None or self.ws.numel() < need:
             self.ws = torch.empty(max(need, 256), dtype=torch.uint8, device=self.device)
         if out is None or out["buf"].numel() < bound:
@@ -377,7 +381,7 @@ class Encoder:
                    "status": torch.empty(max(n_blocks, 1), dtype=torch.int32, device=self.device)}
         rc = lib().lsm_encode_blocks(C.byref(it), _ptr(starts), n_blocks, C.byref(params), _ptr(out["buf"]),
                                      bound, _ptr(out["block_off"]), _ptr(out["status"]), _ptr(self.ws),
-                                     self.ws.numel(), _stream(stream))
+                                     need, _stream(stream))
         _check(rc, "lsm_encode_blocks")
         return out
 

@@ -1,7 +1,8 @@
 """Data blocks above the general path's 72 KiB stage, up to the writer's 4 MiB
 data-block target (use_data_block_size, src/table/writer/mod.rs:193-198):
-encoded on the device (E3, straight in HBM) bit-exact against the oracle and
-decoded two ways: with the workspace pool (pool=True, the default:
+encoded on the device bit-exact against the oracle two ways (pool=True: the
+whole-GPU E3, record / tail / hash units and eight chains per block;
+pool=False: one workgroup per block) and decoded two ways: with the workspace pool (pool=True, the default:
 lsm_decode_workspace_size_ex) the blocks are cut into parse units (restart
 intervals) and hash units (KiB blocks) over the whole GPU plus eight
 single-wave XXH3 chains per block; without it (pool=False) each goes through
@@ -19,11 +20,11 @@ from helpers import compare_decode, counter_items, gpu_decode, pack
 pytestmark = pytest.mark.gpu
 
 
-def _gpu_encode(gpu, items, starts, ri, ratio):
+def _gpu_encode(gpu, items, starts, ri, ratio, pool=True):
     import torch
     d_items = gpu.items_to_device(items)
     d_starts = torch.from_numpy(np.asarray(starts, np.int64).astype(np.int32)).cuda()
-    out = gpu.Encoder().encode(d_items, d_starts, len(starts) - 1, restart_interval=ri, hash_ratio=ratio)
+    out = gpu.Encoder().encode(d_items, d_starts, len(starts) - 1, restart_interval=ri, hash_ratio=ratio, pool=pool)
     torch.cuda.synchronize()
     off = out["block_off"].cpu().numpy().view(np.uint64)
     return out["buf"].cpu().numpy()[:int(off[-1])], off, out["status"].cpu().numpy()[:len(starts) - 1]
@@ -38,7 +39,7 @@ def test_large_data_blocks_round_trip(gpu, ri, ratio, pool):
     ref_buf, ref_off = pyoracle.encode_blocks(items, starts, restart_interval=ri, hash_ratio=ratio)
     sizes = np.diff(ref_off.astype(np.int64))
     assert sizes.max() > 4_100_000 and (sizes > 72 * 1024).all(), sizes
-    buf, off, st = _gpu_encode(gpu, items, starts, ri, ratio)
+    buf, off, st = _gpu_encode(gpu, items, starts, ri, ratio, pool)
     assert (st == 0).all() and (off == ref_off).all() and buf.tobytes() == ref_buf.tobytes()
     g = gpu_decode(gpu, buf, off, pool=pool)
     parsed, item_start, status = pyoracle.decode_blocks(buf, off)
@@ -68,8 +69,9 @@ def test_large_data_blocks_corrupted(gpu, pool):
     compare_decode(g, parsed, item_start, status)
 
 
+@pytest.mark.parametrize("pool", [True, False])
 @pytest.mark.parametrize("ratio", [0.0, 1.33])
-def test_large_blocks_few_items(gpu, ratio):
+def test_large_blocks_few_items(gpu, ratio, pool):
     """Blocks beyond the 96 KiB list image with at most 256 items (long values):
     E3 takes their record offsets from its own workgroup scan (E1 keeps full
     32-bit offsets only for blocks of more than 256 items); long seqnos and
@@ -79,9 +81,9 @@ def test_large_blocks_few_items(gpu, ratio):
     ref_buf, ref_off = pyoracle.encode_blocks(items, starts, restart_interval=16, hash_ratio=ratio)
     sizes = np.diff(ref_off.astype(np.int64))
     assert (sizes > 96 * 1024).all(), sizes
-    buf, off, st = _gpu_encode(gpu, items, starts, 16, ratio)
+    buf, off, st = _gpu_encode(gpu, items, starts, 16, ratio, pool)
     assert (st == 0).all() and (off == ref_off).all() and buf.tobytes() == ref_buf.tobytes()
-    g = gpu_decode(gpu, buf, off)
+    g = gpu_decode(gpu, buf, off, pool=pool)
     parsed, item_start, status = pyoracle.decode_blocks(buf, off)
     assert (status == 0).all()
     compare_decode(g, parsed, item_start, status)
@@ -157,3 +159,36 @@ def test_huge_blocks_payload_verified(gpu):
     for pool in (True, False):
         g = gpu_decode(gpu, buf2, off2, tuning=(0, 0, 0, gpu.DECODE_PAYLOAD_VERIFIED), pool=pool)
         compare_decode(g, parsed, item_start, status)
+
+
+@pytest.mark.parametrize("pool", [True, False])
+def test_huge_blocks_encode_mixed(gpu, pool):
+    """~48 blocks of 80-400 KiB between 4 KiB blocks (hash ratio 1.33: the small
+    blocks carry a hash index, the huge ones drop it): bytes == oracle."""
+    r = np.random.default_rng(3)
+    cuts = [0]
+    for i in range(48):
+        cuts.append(cuts[-1] + 40)
+        cuts.append(cuts[-1] + int(r.integers(900, 4600)))
+    items = counter_items(cuts[-1], seed=3, tomb_frac=0.03)
+    starts = np.array(cuts, np.uint32)
+    ref_buf, ref_off = pyoracle.encode_blocks(items, starts, restart_interval=16, hash_ratio=1.33)
+    buf, off, st = _gpu_encode(gpu, items, starts, 16, 1.33, pool)
+    assert (st == 0).all() and (off == ref_off).all() and buf.tobytes() == ref_buf.tobytes()
+
+
+@pytest.mark.parametrize("pool", [True, False])
+def test_huge_index_blocks_encode(gpu, pool):
+    """Full block indexes over 96 KiB (restart interval 1, u64 handles)."""
+    import torch
+    from helpers import index_items
+    items = index_items(14000, seed=11)
+    starts = np.array([0, 6000, 6001, 14000], np.uint32)
+    ref_buf, ref_off = pyoracle.encode_blocks(items, starts, block_type=1)
+    d_items = gpu.items_to_device(items)
+    d_starts = torch.from_numpy(starts.astype(np.int32)).cuda()
+    out = gpu.Encoder().encode(d_items, d_starts, 3, restart_interval=1, block_type=1, pool=pool)
+    torch.cuda.synchronize()
+    off = out["block_off"].cpu().numpy().view(np.uint64)
+    assert (out["status"].cpu().numpy()[:3] == 0).all() and (off == ref_off).all()
+    assert out["buf"].cpu().numpy()[:int(off[-1])].tobytes() == ref_buf.tobytes()
