@@ -424,6 +424,14 @@ int lsm_lz4_plan_framed(const uint8_t* d_blocks, const uint64_t* d_block_off, ui
 int lsm_lz4_decompress_framed(const uint8_t* d_blocks, const uint64_t* d_block_off, uint32_t n_blocks,
                               uint8_t* d_out, const uint64_t* d_out_off, int32_t* d_status,
                               void* d_workspace, size_t workspace_bytes, void* stream);
+/* lsm_lz4_plan_output (framed = 0) / lsm_lz4_plan_framed (framed = 1) for an output
+ * arena the caller sized without reading the plan back (no host synchronisation):
+ * when the planned bytes exceed out_cap every range is left empty, so the
+ * decompress writes nothing and reports LSM_OVERFLOW for each block whose header
+ * verifies (grow the arena and repeat). */
+int lsm_lz4_plan_capped(const uint8_t* d_blocks, const uint64_t* d_block_off, uint32_t n_blocks,
+                        uint64_t max_block_bytes, int framed, uint64_t out_cap, uint64_t* d_out_off,
+                        void* d_workspace, size_t workspace_bytes, void* stream);
 
 /* ---- materialize (DataBlockParsedItem::materialize, data_block/mod.rs:296-315) --
  * Owned keys of decoded items: key = Slice::fused(prefix, suffix) =
@@ -445,6 +453,15 @@ int lsm_materialize_plan(const uint8_t* d_blocks, const uint64_t* d_block_off, u
 int lsm_materialize_keys(const uint8_t* d_blocks, const uint64_t* d_block_off, uint32_t n_blocks,
                          const uint32_t* d_item_start, const int32_t* d_status, const lsm_parsed_items* d_parsed,
                          uint64_t n_items, const uint64_t* d_key_out_off, uint8_t* d_key_out, void* stream);
+/* lsm_materialize_keys into an arena of key_cap bytes sized without reading
+ * d_key_out_off[n_items] back (no host synchronisation): every key is written
+ * when they fit, none otherwise; *d_result (device i32) = LSM_OK or
+ * LSM_OVERFLOW.  n_items may be the parsed arrays' capacity (items past
+ * d_item_start[n_blocks] have empty keys). */
+int lsm_materialize_keys_capped(const uint8_t* d_blocks, const uint64_t* d_block_off, uint32_t n_blocks,
+                                const uint32_t* d_item_start, const int32_t* d_status,
+                                const lsm_parsed_items* d_parsed, uint64_t n_items, const uint64_t* d_key_out_off,
+                                uint8_t* d_key_out, uint64_t key_cap, int32_t* d_result, void* stream);
 
 /* ---- whole-table scan (Scanner, src/table/scanner.rs:24-92) -----------------
  * Decodes every data block of one table file image d_file[0 .. file_len) (16-byte

@@ -831,7 +831,13 @@ __global__ __launch_bounds__(kBigWaves * kWave) void decode_deferred_staged_kern
 constexpr uint32_t kHugeWin = 32 * 1024;               // span bytes per unit
 constexpr uint32_t kHugeOverlap = 8 * 1024 - 256;      // staged past the window (intervals that straddle it)
 constexpr uint32_t kHugeStage = kHugeWin + kHugeOverlap;
-constexpr uint32_t kHugeLds = kHugeStage + kStagePad + 64;
+constexpr uint32_t kHugeMaxIv = 512;                   // intervals per window for phase A / B (else thread walks)
+constexpr uint32_t kHugeTile = 1024;                   // items per window for phase A / B
+constexpr uint32_t kHugeBix = kHugeStage + kStagePad;  // LDS: the window's binary-index entries
+constexpr uint32_t kHugeMeta = kHugeBix + 4 * (kHugeMaxIv + 4);
+constexpr uint32_t kHugeOwner = kHugeMeta + 80;
+constexpr uint32_t kHugeRec = kHugeOwner + kHugeMaxIv;
+constexpr uint32_t kHugeLds = 64 + kHugeRec + 8 * (kHugeTile + 1);
 constexpr uint32_t kHugeGrid = 2048;
 constexpr uint32_t kHugeChainGrid = 1024, kHugeChainLds = 40 * 1024;
 
@@ -1200,7 +1206,13 @@ __device__ __forceinline__ uint32_t last_le(const uint64_t* a, uint32_t n, uint6
   return lo;
 }
 
-// Huge-block work units (see huge_plan): unit u = window c of block i.
+// Huge-block work units (see huge_plan): unit u = window c of block i.  Data
+// windows whose intervals are all staged take phase A / B (decode_big_kernel's
+// record walk: lane = interval for the boundaries, thread = record for the
+// fields) on a window view of the block (meta offsets relative to the stage,
+// interval numbers absolute, the binary-index entries copied next to the
+// stage); others walk their intervals thread by thread.
+template <bool kAllFields>
 __global__ __launch_bounds__(256) void decode_huge_kernel(DecodeParams P) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint8_t* stage = smem + 64;
@@ -1213,8 +1225,14 @@ __global__ __launch_bounds__(256) void decode_huge_kernel(DecodeParams P) {
   const uint32_t tid = threadIdx.x, lane = tid & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(tid / kWave);
   const bool hash = !(P.flags & LSM_DECODE_PAYLOAD_VERIFIED);
-  for (uint32_t u = blockIdx.x; u < units; u += gridDim.x) {
-    const uint32_t i = last_le(L.ppre, n, u);
+  // a run of consecutive units per workgroup: one block search per run, and a
+  // window's first interval is the previous window's end (the same bound)
+  const uint32_t per = (units + gridDim.x - 1) / gridDim.x;
+  const uint32_t u_begin = blockIdx.x * per, u_end = min(units, u_begin + per);
+  uint32_t i = u_begin < u_end ? last_le(L.ppre, n, u_begin) : 0;
+  uint32_t carry_u = 0xFFFFFFFFu, carry_r = 0;  // unit whose r1 search answer is carry_r (block i)
+  for (uint32_t u = u_begin; u < u_end; ++u) {
+    while (i + 1 < n && gload(L.ppre, i + 1) <= u) ++i, carry_u = 0xFFFFFFFFu;
     const HugeRec* r = L.rec + i;
     if (!r->accepted) continue;  // (uniform)
     const BlockMeta m = r->m;
@@ -1236,6 +1254,7 @@ __global__ __launch_bounds__(256) void decode_huge_kernel(DecodeParams P) {
     if (parse) {
       const uint32_t nint = t.bin_len, p0 = m.p0;
       uint32_t lo0 = 0, hi0 = nint, lo1 = 0, hi1 = nint;  // r0 in [lo0, hi0], r1 in [lo1, hi1]
+      if (carry_u + 1 == u) lo0 = hi0 = carry_r;
       while (hi0 > lo0 || hi1 > lo1) {  // (uniform) each round narrows both ranges 256-fold
         const uint32_t len0 = hi0 - lo0, len1 = hi1 - lo1;
         const uint32_t st0 = (len0 + 255) / 256, st1 = (len1 + 255) / 256;
@@ -1265,33 +1284,93 @@ __global__ __launch_bounds__(256) void decode_huge_kernel(DecodeParams P) {
       // at least once even when the binary index is not monotone (its walk then fails)
       r0 = cs == 0 ? 0 : lo0;
       r1 = ce == span ? nint : lo1;
+      carry_u = u;
+      carry_r = lo1;
     }
-    vm_wait<0>();
-    lds_barrier();
     const uint8_t* sbase = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(stage) - cs);  // span-relative
-    if (hash && r->nbk) {  // the KiB blocks that start in [cs, ce)
+    if (parse) {
+      const uint64_t item_base = r->item_base;
+      const uint32_t p0 = m.p0, ri = t.ri, niv = r1 - r0;
+      const uint32_t items_w = niv ? min(r1 * ri, t.item_count) - r0 * ri : 0;
+      // phase A / B when every interval of the window is staged (a wave-uniform vote)
+      bool fast = m.type != 1 && niv <= kHugeMaxIv && items_w <= kHugeTile;
+      if (fast) {
+        bool mine = true;
+        for (uint32_t x = r0 + tid; x < r1; x += 256) {
+          const uint32_t s_cur = bin_get(gbase, p0, t, x);
+          const uint32_t stop = x + 1 == t.bin_len ? t.rec_end : bin_get(gbase, p0, t, x + 1);
+          mine = mine && p0 + s_cur >= cs && stop <= t.rec_end && (p0 + stop + kChunkReadAhead <= ss || ss == span);
+        }
+        if (lane == 0) cnt[10 + wave] = __ballot(!mine) != 0;
+        lds_barrier();
+        fast = !(cnt[10] | cnt[11] | cnt[12] | cnt[13]);
+      }
+      uint8_t* bix = smem + 64 + kHugeBix;
+      BlockMeta* wmeta = reinterpret_cast<BlockMeta*>(smem + 64 + kHugeMeta);
+      uint8_t* owner = smem + 64 + kHugeOwner;
+      uint64_t* rec = reinterpret_cast<uint64_t*>(smem + 64 + kHugeRec);
+      if (fast) {
+        // the entries r0 .. min(r1, nint - 1) as dwords next to the stage
+        const uint32_t e1 = min(r1, t.bin_len - 1);
+        const uint32_t eb = p0 + t.bin_off + r0 * t.step, elen = (e1 - r0 + 1) * t.step;
+        for (uint32_t d = tid; 4 * d < elen; d += 256)
+          reinterpret_cast<uint32_t*>(bix)[d] = read_u32_unaligned(gbase, eb + 4 * d);
+        for (uint32_t x = tid; x < niv; x += 256) owner[x] = 0;
+        for (uint32_t x = tid; x <= items_w; x += 256) rec[x] = 0;
+        if (tid == 0) {
+          BlockMeta w = m;
+          w.p0 = m.p0 - cs;  // stage offsets (the window starts at span offset cs)
+          w.rec_end = m.rec_end - cs;
+          w.bin_off = kHugeBix - w.p0 - r0 * t.step;  // bin_get(stage, w.p0, r) reads bix[r - r0]
+          w.item0 = 0u - r0 * ri;                     // descriptors numbered from the window's first item
+          w.chain0 = 0u - r0;                         // phase A's interval c is interval r0 + c
+          w.st = ST_OK;
+          *wmeta = w;
+        }
+      }
+      vm_wait<0>();
+      lds_barrier();
+      if (fast) phase_a<true>(stage, wmeta, owner, rec, wave * kWave, 4 * kWave, niv, kHugeTile);
+      if (hash && r->nbk) {  // the KiB blocks that start in [cs, ce)
+        const uint32_t nbk = r->nbk;
+        const uint32_t n0 = min(nbk, cs > p0 ? (cs - p0 + 1023) / 1024 : 0u);
+        const uint32_t n1 = min(nbk, ce > p0 ? (ce - p0 + 1023) / 1024 : 0u);
+        if (n1 > n0)
+          xxh3_kib_contribs(sbase, p0 + 1024 * n0, (n1 - n0) * 1024 + 1, &kLongSecret,
+                            L.contrib + 8 * (gload(L.kpre, i) + n0), wave, 4);
+      }
+      bool walk = !fast;
+      if (fast) {
+        lds_barrier();
+        phase_b<kAllFields, false, true>(P, stage, wmeta, rec, items_w, (uint32_t)(item_base + r0 * ri), tid, 256);
+        lds_barrier();
+        const int32_t wst = wmeta->st;
+        if (wst == ST_PARSE && tid == 0) atomicOr(const_cast<uint32_t*>(&r->parse_bad), 1u);
+        walk = wst == ST_DEFER;  // a record shape the straight-line parsers do not take: the LEB cursor
+      }
+      if (walk) {
+        bool ok = true;
+        for (uint32_t x = r0 + tid; x < r1; x += 256) {
+          const uint32_t s_cur = bin_get(gbase, p0, t, x);
+          const bool last = x + 1 == t.bin_len;
+          const uint32_t stop = last ? t.rec_end : bin_get(gbase, p0, t, x + 1);
+          const bool staged = p0 + s_cur >= cs && stop <= t.rec_end && (p0 + stop + kChunkReadAhead <= ss || ss == span);
+          ok &= walk_interval_at(staged ? sbase : gbase, p0, m, t, x, s_cur, stop, [&](uint32_t j, const ItemFields& f) {
+            emit_global(P.out, item_base + j, f, P.seqno_add, P.compact);
+          });
+        }
+        const uint64_t bad = __ballot(!ok);
+        if (bad && lane == (uint32_t)__builtin_ctzll(bad)) atomicOr(const_cast<uint32_t*>(&r->parse_bad), 1u);
+      }
+    } else if (hash && r->nbk) {
+      vm_wait<0>();
+      lds_barrier();
       const uint32_t p0 = m.p0, nbk = r->nbk;
       const uint32_t n0 = min(nbk, cs > p0 ? (cs - p0 + 1023) / 1024 : 0u);
       const uint32_t n1 = min(nbk, ce > p0 ? (ce - p0 + 1023) / 1024 : 0u);
       if (n1 > n0)
         xxh3_kib_contribs(sbase, p0 + 1024 * n0, (n1 - n0) * 1024 + 1, &kLongSecret,
                           L.contrib + 8 * (gload(L.kpre, i) + n0), wave, 4);
-    }
-    if (parse) {
-      const uint64_t item_base = r->item_base;
-      const uint32_t p0 = m.p0;
-      bool ok = true;
-      for (uint32_t x = r0 + tid; x < r1; x += 256) {
-        const uint32_t s_cur = bin_get(gbase, p0, t, x);
-        const bool last = x + 1 == t.bin_len;
-        const uint32_t stop = last ? t.rec_end : bin_get(gbase, p0, t, x + 1);
-        const bool staged = p0 + s_cur >= cs && stop <= t.rec_end && (p0 + stop + kChunkReadAhead <= ss || ss == span);
-        ok &= walk_interval_at(staged ? sbase : gbase, p0, m, t, x, s_cur, stop, [&](uint32_t j, const ItemFields& f) {
-          emit_global(P.out, item_base + j, f, P.seqno_add, P.compact);
-        });
-      }
-      const uint64_t bad = __ballot(!ok);
-      if (bad && lane == (uint32_t)__builtin_ctzll(bad)) atomicOr(const_cast<uint32_t*>(&r->parse_bad), 1u);
     }
     lds_barrier();  // (the next unit rewrites the stage)
   }
@@ -1675,7 +1754,10 @@ hipError_t launch_decode(const DecodeParams& P0, void* ws, size_t ws_bytes, hipS
     hipLaunchKernelGGL(decode_deferred_staged_kernel, dim3(dgrid), dim3(kBigWaves * kWave), big, st, P2);
   }
   if (P.huge_pool && bgrid) {
-    hipLaunchKernelGGL(decode_huge_kernel, dim3(kHugeGrid), dim3(256), kHugeLds, st, P);
+    const void* hk = all ? (const void*)decode_huge_kernel<true> : (const void*)decode_huge_kernel<false>;
+    static uint64_t done_hk[2] = {};
+    if ((e = set_lds_attr(hk, kHugeLds, &done_hk[all ? 1 : 0])) != hipSuccess) return e;
+    if ((e = hipLaunchKernel(hk, dim3(kHugeGrid), dim3(256), args, kHugeLds, st)) != hipSuccess) return e;
     // (an unused 40 KiB LDS request: at most four chain workgroups per CU, one per
     // SIMD, so no two serial chains share a SIMD's quarter-rate multiplies)
     hipLaunchKernelGGL(decode_huge_chain_kernel, dim3(kHugeChainGrid), dim3(64), kHugeChainLds, st, P);

@@ -129,6 +129,8 @@ struct EncodeParams {
   uint32_t hb_valid;
   uint32_t* hb_fix;     // [1] set by E1 when it left keys of more than 16 bytes (kNeedHash)
   unsigned long long* phase;  // diagnostic builds: per-phase cycle totals [16]
+  uint32_t* pfirst;     // [n_blocks + 1] E1p: each block's first record prefix (low 32 bits); [n_blocks] the total
+  uint32_t* e1p_flag;   // [1] E1p: the item_start array is not monotone
   uint8_t* huge_pool;   // workspace past encode_workspace_size (null: E3 one workgroup per block)
   uint64_t huge_pool_bytes;
   uint32_t huge_cap;    // huge-list entries the pool's layout provides
@@ -1502,6 +1504,155 @@ __device__ __forceinline__ void group_barrier_lds() {
 #ifndef LSM_NOVOTE
 #define LSM_NOVOTE 0
 #endif
+// ---------------------------------------- E1p: the plan of huge-block batches
+// Blocks of ~16 Ki items and more (the writer's 1-4 MiB data blocks,
+// writer/mod.rs:193-198) leave encode_plan_kernel one workgroup per block,
+// walking 512-item chunks one after another (60 workgroups for 60 blocks of
+// 4 MiB).  E1p computes the same outputs item-parallel:
+//   lengths  thread per item: fields, shared prefix with its restart head
+//            (encoder.rs:140-143), record length -> erec (for now), shared
+//            length -> hbucket (unused by these batches' E2), per-block exact
+//            record totals and bad flags (wave-aggregated atomics into sizes)
+//   scan     the device scan over every item's record length, in place (low
+//            32 bits: a block's offsets are differences of two prefixes)
+//   blocks   thread per block: the plan, as encode_plan_kernel's epilogue
+//   offsets  thread per item: erec = prefix - its block's first prefix (the
+//            packed word for blocks of <= kGItems items)
+// A non-monotone item_start array rejects every block (the one-workgroup
+// plan rejects the run of blocks its workgroup holds).
+__device__ __forceinline__ uint32_t block_of_item(const EncodeParams& P, uint32_t i) {
+  uint32_t lo = 0, hi = P.n_blocks;  // last b < n_blocks with start[b] <= i
+  while (hi - lo > 1) {
+    const uint32_t mid = (lo + hi) >> 1;
+    if (clamped_start(P, mid) <= i) lo = mid;
+    else hi = mid;
+  }
+  return lo;
+}
+
+constexpr uint64_t kE1pBad = 1ULL << 63;
+
+__device__ __forceinline__ uint64_t shfl_down64(uint64_t v, int o) {
+  return (uint64_t)(uint32_t)__shfl_down((int)(uint32_t)v, o) |
+         ((uint64_t)(uint32_t)__shfl_down((int)(uint32_t)(v >> 32), o) << 32);
+}
+
+__global__ __launch_bounds__(256) void encode_e1p_lengths_kernel(EncodeParams P) {
+  const uint32_t gid = blockIdx.x * 256 + threadIdx.x;
+  if (gid < P.n_blocks && clamped_start(P, gid + 1) < clamped_start(P, gid)) atomicOr(P.e1p_flag, 1u);
+  if ((uint64_t)gid >= P.it.n_items) return;
+  const uint32_t i = gid, i_begin = clamped_start(P, 0), i_end = clamped_start(P, P.n_blocks);
+  const bool in = i >= i_begin && i < i_end;
+  const uint32_t b = in ? block_of_item(P, i) : 0;
+  const uint32_t s = clamped_start(P, b), e = clamped_start(P, b + 1);
+  const bool live = in && s <= i && i < e;  // (not, for a non-monotone array: every block is rejected)
+  const uint32_t ri = P.ri, jj = i - s;
+  const bool head = jj % ri == 0;
+  uint64_t rec = 0;
+  bool bad = false;
+  if (live) {
+    RawItem r = load_raw<false>(P, i);
+    ItemMeta m = cook_item<false>(r, bad);
+    if (!head) {
+      const uint64_t h = (uint64_t)i - jj % ri;
+      const uint64_t hko = P.it.key_off[h];
+      const uint32_t n = min((uint32_t)min(P.it.key_off[h + 1] - hko, (uint64_t)0xFFFF), m.klen);
+      const Win16 wa = gwin16(P.it.keys + hko), wb = gwin16(P.it.keys + m.ko);
+      const uint64_t x0 = wa.lo ^ wb.lo, x1 = wa.hi ^ wb.hi;
+      uint32_t sh;
+      if (x0) sh = min(n, (uint32_t)(__builtin_ctzll(x0) >> 3));
+      else if (x1) sh = min(n, 8 + (uint32_t)(__builtin_ctzll(x1) >> 3));
+      else sh = n <= 16 ? n : lcp_tail(P.it.keys, hko, m.ko, n);
+      m.sh = sh;
+      P.hbucket[i] = (uint16_t)min(sh, 0xFFFFu);
+    }
+    rec = item_record_len(P, m, head);
+  }
+  P.erec[i] = (uint32_t)min(rec, (uint64_t)0xFFFFFFFFu);
+  // per-block exact totals: lanes of one block summed first (blocks are runs of lanes)
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t bb = live ? b : 0xFFFFFFFFu;
+  uint64_t sum = rec | (bad ? kE1pBad : 0);
+  // segmented wave reduction: lanes with the same block, head lane = first of its run
+  for (int o = 1; o < 64; o <<= 1) {
+    const uint64_t v = shfl_down64(sum, o);
+    const uint32_t bo = (uint32_t)__shfl_down((int)bb, o);
+    if ((int)lane + o < 64 && bo == bb) sum = (sum & kE1pBad) | (v & kE1pBad) | ((sum & ~kE1pBad) + (v & ~kE1pBad));
+  }
+  const uint32_t bprev = (uint32_t)__shfl_up((int)bb, 1);
+  if (live && (lane == 0 || bprev != bb)) {
+    if (sum & ~kE1pBad) atomicAdd((unsigned long long*)&P.sizes[b], (unsigned long long)(sum & ~kE1pBad));
+    if (sum & kE1pBad) atomicOr((unsigned long long*)&P.sizes[b], (unsigned long long)kE1pBad);
+  }
+}
+
+// Scan output: each item's record prefix (low 32 bits) in place; the total in pfirst[n_blocks].
+struct E1pOut {
+  uint32_t* erec;
+  uint32_t* total;
+  uint64_t n;
+  __device__ void operator()(uint64_t i, uint64_t prefix) const {
+    if (i < n) erec[i] = (uint32_t)prefix;
+    else *total = (uint32_t)prefix;
+  }
+};
+
+__device__ __forceinline__ uint32_t e1p_prefix(const EncodeParams& P, uint32_t i) {
+  return (uint64_t)i < P.it.n_items ? P.erec[i] : P.pfirst[P.n_blocks];
+}
+
+__global__ __launch_bounds__(256) void encode_e1p_blocks_kernel(EncodeParams P) {
+  const uint32_t b = blockIdx.x * 256 + threadIdx.x;
+  if (b >= P.n_blocks) return;
+  const uint32_t ri = P.ri;
+  const uint32_t s = clamped_start(P, b), e = clamped_start(P, b + 1);
+  const uint64_t acc = P.sizes[b];
+  bool bad = P.e1p_flag[0] || e <= s || (acc & kE1pBad) || start_past_items(P, b + 1);
+  const uint32_t n = bad ? 0 : e - s;
+  const uint64_t recs = bad ? 0 : acc & ~kE1pBad;
+  const uint32_t p_s = bad ? 0 : e1p_prefix(P, s);
+  P.pfirst[b] = p_s;
+  const uint32_t bin_len = n ? (n + ri - 1) / ri : 0;
+  const uint64_t last_head = n ? (uint32_t)(e1p_prefix(P, s + (bin_len - 1) * ri) - p_s) : 0;
+  const uint32_t step = last_head <= 0xFFFF ? 2 : 4;
+  const uint32_t buckets = bucket_count(n, P.ratio);
+  const uint32_t hash_w = (buckets > 0 && bin_len <= kHashMaxPointers) ? buckets : 0;
+  const uint64_t total = kHdrLen + recs + 1 + (uint64_t)bin_len * step + hash_w + kTrailerLen;
+  if (recs > 0xFFFFFFF0ULL || total > 0xFFFFFF00ULL) bad = true;
+  const uint64_t ks = P.it.key_off[s], ke = P.it.key_off[e];
+  const uint64_t vs = P.it.val_off[s], ve = P.it.val_off[e];
+  uint32_t flags = 0;
+  if (bad) {
+    flags = kPlanBad;
+    P.status[b] = ST_BAD_ARG;
+  } else if (!group_fits(n, ke - ks, ve - vs, total, hash_w)) {
+    const uint64_t need = e2_need(total, hash_w);
+    flags = need <= kImgMedium ? kPlanMedium : need <= kImgBig ? kPlanBig : kPlanHuge;
+  }
+  P.plans[b] = BlockPlan{(uint32_t)recs, bin_len, hash_w, step | (flags << 8)};
+  P.sizes[b] = (bad ? 0 : total) | ((flags & (kPlanMedium | kPlanBig | kPlanHuge)) ? kListedOne : 0);
+  P.kspan[b] = ks;
+  P.vspan[b] = vs;
+  if (b + 1 == P.n_blocks) {
+    P.kspan[b + 1] = ke;
+    P.vspan[b + 1] = ve;
+  }
+}
+
+__global__ __launch_bounds__(256) void encode_e1p_offsets_kernel(EncodeParams P) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if ((uint64_t)i >= P.it.n_items || P.e1p_flag[0]) return;
+  const uint32_t i_begin = clamped_start(P, 0), i_end = clamped_start(P, P.n_blocks);
+  if (i < i_begin || i >= i_end) return;
+  const uint32_t b = block_of_item(P, i);
+  if ((P.plans[b].step_flags >> 8) & kPlanBad) return;
+  const uint32_t s = clamped_start(P, b), n = clamped_start(P, b + 1) - s;
+  const uint32_t roff = P.erec[i] - P.pfirst[b], jj = i - s;
+  const bool head = jj % P.ri == 0;
+  const uint32_t x = head ? jj / P.ri : P.hbucket[i];
+  P.erec[i] = n > kGItems ? roff : min(roff, 0x7FFFu) | (head ? kErecHead : 0u) | (min(x, 0xFFFFu) << 16);
+}
+
 // The buckets of the keys E1 left (more than 16 bytes): a wave per block,
 // grid-stride; exits at once when E1 left none.
 __global__ __launch_bounds__(256) void encode_bucket_fixup_kernel(EncodeParams P) {
@@ -2132,7 +2283,8 @@ __global__ __launch_bounds__(kE3Threads) void encode_large_kernel(EncodeParams P
 //   hash     units of kEHugeKib KiB blocks: XXH3 contributions into the pool
 //   chain    eight single-wave chains per block; the last one merges the tail
 //            and writes the header and the status
-constexpr uint32_t kEHugeItems = 1024;  // items per record unit (four per thread)
+constexpr uint32_t kEHugeItems = 1024;  // items per record unit, at most (four per thread)
+constexpr uint32_t kEHugeImg = 2 * 4 * kE3HashChunk;  // LDS image of a record unit (the tail unit's vote arrays)
 constexpr uint32_t kEHugeKib = 32;      // KiB blocks per hash unit (eight per wave)
 constexpr uint32_t kEHugeGrid = 2048;
 
@@ -2141,7 +2293,7 @@ struct EncHuge {
   uint64_t acc[8];
   uint32_t b, s, n, total;
   uint32_t nbk, nru, accepted, done;
-  uint32_t pad[2];
+  uint32_t ipu, pad;  // items per record unit
 };
 static_assert(sizeof(EncHuge) % 16 == 0, "EncHuge layout");
 struct EncHugeHdr {
@@ -2210,7 +2362,10 @@ __global__ __launch_bounds__(1024) void encode_huge_plan_kernel(EncodeParams P) 
       h.total = (uint32_t)(dst_end - h.dst_off);
       acc = dst_end <= P.out_cap;  // (else the one-workgroup E3 reports the overflow)
       nbk = (h.total - kHdrLen - 1) / 1024;  // (payload > 96 KiB: the long path)
-      h.nru = h.n <= kGItems ? 1 : (h.n + kEHugeItems - 1) / kEHugeItems;
+      // items per record unit: about what fills the LDS image at the block's mean record size
+      const uint32_t recs = P.plans[h.b].recs;
+      h.ipu = (uint32_t)min<uint64_t>(kEHugeItems, max<uint64_t>(64, (uint64_t)(kEHugeImg - 96) * h.n / max(recs, 1u)));
+      h.nru = h.n <= kGItems ? 1 : (h.n + h.ipu - 1) / h.ipu;
       nu = acc ? h.nru + 1 : 0;
       nbk = acc ? nbk : 0;
     }
@@ -2249,16 +2404,22 @@ __global__ __launch_bounds__(1024) void encode_huge_plan_kernel(EncodeParams P) 
 }
 
 // Record units (u < nru of a block) and the tail unit (u == nru).
-__global__ __launch_bounds__(256) void encode_huge_records_kernel(EncodeParams P) {
-  __shared__ uint32_t hlo[kE3HashChunk], hhi[kE3HashChunk];
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void encode_huge_records_kernel(EncodeParams P) {
+  __shared__ __attribute__((aligned(16))) uint32_t lbuf[2 * kE3HashChunk];  // record image | vote arrays
+  uint32_t* hlo = lbuf;
+  uint32_t* hhi = lbuf + kE3HashChunk;
   __shared__ uint32_t psum[4];
   const EncHugeLayout L = enc_huge_layout(P);
   const uint32_t n3 = L.hdr->n3;
   if (!n3) return;
   const uint64_t units = L.hdr->total_units;
   const uint32_t tid = threadIdx.x, lane = tid & (kWave - 1), wave = tid >> 6;
-  for (uint64_t u = blockIdx.x; u < units; u += gridDim.x) {
-    const uint32_t i = last_le_u64(L.upre, n3, u);
+  // a run of consecutive units per workgroup: one block search per run
+  const uint64_t per = (units + gridDim.x - 1) / gridDim.x;
+  const uint64_t u_begin = (uint64_t)blockIdx.x * per, u_end = min(units, u_begin + per);
+  uint32_t i = u_begin < u_end ? last_le_u64(L.upre, n3, u_begin) : 0;
+  for (uint64_t u = u_begin; u < u_end; ++u) {
+    while (i + 1 < n3 && L.upre[i + 1] <= u) ++i;
     const EncHuge h = L.rec[i];
     if (!h.accepted) continue;  // (uniform; rejected blocks own no units)
     const uint32_t k = (uint32_t)(u - L.upre[i]);
@@ -2292,16 +2453,41 @@ __global__ __launch_bounds__(256) void encode_huge_records_kernel(EncodeParams P
         }
         __syncthreads();  // (psum is rewritten by the next unit)
       } else {
-        const uint32_t j0 = k * kEHugeItems, j1 = min(h.n, j0 + kEHugeItems);
-        for (uint32_t j = j0 + tid; j < j1; j += 256) {
-          const bool head = j % ri == 0;
-          bool bad = false;
-          const ItemMeta m = load_item_lcp(P, h.s, j, ri, bad);
-          const uint32_t roff = P.erec[h.s + j];
-          RecordCopy rc;
-          rc.issue(P, m, head, p0 + roff);
-          rc.store(P, m, head, img);
-          if (head) store_le(img, p0 + bin_off + (j / ri) * step, roff, step);
+        // records [j0, j1) assembled in LDS (image bytes [a0, a0 + lend)), then copied
+        // out in 16-B pieces; a unit larger than the image writes straight to HBM
+        const uint32_t j0 = k * h.ipu, j1 = min(h.n, j0 + h.ipu);
+        const uint32_t rb = P.erec[h.s + j0], re = j1 < h.n ? P.erec[h.s + j1] : pl.recs;
+        const uint32_t a0 = (p0 + rb) & ~15u, lend = p0 + re - a0;
+        const bool staged = lend + 32 <= kEHugeImg;  // (uniform)
+        uint8_t* limg = reinterpret_cast<uint8_t*>(lbuf) - a0;  // image offset x -> LDS limg + x
+        auto put = [&](uint8_t* dst) {  // (two call sites: LDS and global stores)
+          for (uint32_t j = j0 + tid; j < j1; j += 256) {
+            const bool head = j % ri == 0;
+            bool bad = false;
+            const ItemMeta m = load_item_lcp(P, h.s, j, ri, bad);
+            const uint32_t roff = P.erec[h.s + j];
+            RecordCopy rc;
+            rc.issue(P, m, head, p0 + roff);
+            rc.store(P, m, head, dst);
+            if (head) store_le(img, p0 + bin_off + (j / ri) * step, roff, step);
+          }
+        };
+        if (staged) put(limg);
+        else put(img);
+        if (staged) {
+          __syncthreads();
+          const uint32_t lo = (p0 + rb) - a0, c0 = (lo + 15) >> 4, c1 = lend >> 4;
+          const u32x4* src = reinterpret_cast<const u32x4*>(lbuf);
+          u32x4* dst = reinterpret_cast<u32x4*>(img + a0);
+          for (uint32_t c = c0 + tid; c < c1; c += 256) __builtin_nontemporal_store(src[c], dst + c);
+          // the partial pieces at both ends (shared with the neighbouring units' records)
+          auto* gb = (__attribute__((address_space(1))) uint8_t*)(img + a0);
+          const uint8_t* lb = reinterpret_cast<const uint8_t*>(lbuf);
+          if (tid == 0)
+            for (uint32_t x = lo; x < min(16 * c0, lend); ++x) gb[x] = lb[x];
+          if (tid == kWave && c1 >= c0)
+            for (uint32_t x = 16 * c1; x < lend; ++x) gb[x] = lb[x];
+          __syncthreads();  // (the next unit rewrites the image)
         }
       }
       continue;
@@ -2346,9 +2532,12 @@ __global__ __launch_bounds__(256) void encode_huge_contrib_kernel(EncodeParams P
   const int q = lane & 3, sq = lane >> 2;
   const uint64_t k0 = kLongSecret.acc[sq + 2 * q], k1 = kLongSecret.acc[sq + 2 * q + 1];
   constexpr uint32_t kPer = kEHugeKib / 4;
-  for (uint64_t u = blockIdx.x; u < units; u += gridDim.x) {
+  const uint64_t per = (units + gridDim.x - 1) / gridDim.x;
+  const uint64_t u_begin = (uint64_t)blockIdx.x * per, u_end = min(units, u_begin + per);
+  uint32_t i = u_begin < u_end ? last_le_u64(L.kpre, n3, u_begin * kEHugeKib) : 0;
+  for (uint64_t u = u_begin; u < u_end; ++u) {
     const uint64_t g0 = u * kEHugeKib, g1 = min(tk, g0 + kEHugeKib);
-    uint32_t i = last_le_u64(L.kpre, n3, g0);
+    while (i + 1 < n3 && L.kpre[i + 1] <= g0) ++i;
     const uint8_t* base[kPer];
     uint32_t pos[kPer];
     uint64_t gg[kPer];
@@ -2468,10 +2657,16 @@ static uint32_t plan_blocks_per_wg(uint64_t n_items, uint32_t n_blocks) {
   return (uint32_t)std::min<uint64_t>(kPlanBlocks, std::max<uint64_t>(1, bpw));
 }
 
+// kspan, vspan | sizes | plans | lists | list count + E1p flag | scan tiles (blocks or items) |
+// erec | hbucket | hb_fix | pfirst
+static uint64_t enc_tiles(uint64_t n_items, uint32_t n_blocks) {
+  return std::max<uint64_t>(scan_tiles(n_blocks), scan_tiles(std::max<uint64_t>(n_items, 1)));
+}
 size_t encode_workspace_size(uint64_t n_items, uint32_t n_blocks) {
   return 2 * al256(((size_t)n_blocks + 1) * 8) + al256((size_t)n_blocks * 8) +
          al256((size_t)n_blocks * sizeof(BlockPlan)) + al256((size_t)n_blocks * 4) + 256 +
-         al256(scan_tiles(n_blocks) * 8) + al256((size_t)n_items * 4) + al256((size_t)n_items * 2) + 256;
+         al256(enc_tiles(n_items, n_blocks) * 8) + al256((size_t)n_items * 4) + al256((size_t)n_items * 2) + 256 +
+         al256(((size_t)n_blocks + 1) * 4);
 }
 
 // Huge-list entries for an output of out_cap bytes: a huge block's image
@@ -2521,11 +2716,14 @@ hipError_t launch_encode(const lsm_items& items, const uint32_t* starts, uint32_
   P.sizes = (uint64_t*)w; w += al256((size_t)n_blocks * 8);
   P.plans = (BlockPlan*)w; w += al256((size_t)n_blocks * sizeof(BlockPlan));
   P.lists = (uint32_t*)w; w += al256((size_t)n_blocks * 4);
-  P.list_count = (uint32_t*)w; w += 256;
-  uint64_t* tiles = (uint64_t*)w; w += al256(scan_tiles(n_blocks) * 8);
+  P.list_count = (uint32_t*)w;
+  P.e1p_flag = (uint32_t*)w + 1;
+  w += 256;
+  uint64_t* tiles = (uint64_t*)w; w += al256(enc_tiles(items.n_items, n_blocks) * 8);
   P.erec = (uint32_t*)w; w += al256((size_t)items.n_items * 4);
   P.hbucket = (uint16_t*)w; w += al256((size_t)items.n_items * 2);
-  P.hb_fix = (uint32_t*)w;
+  P.hb_fix = (uint32_t*)w; w += 256;
+  P.pfirst = (uint32_t*)w;
   hipError_t e;
   {  // the whole-GPU E3 pool, when the workspace carries one
     const size_t base = al256(encode_workspace_size(items.n_items, n_blocks));
@@ -2540,7 +2738,22 @@ hipError_t launch_encode(const lsm_items& items, const uint32_t* starts, uint32_
   P.plan_bpw = plan_blocks_per_wg(items.n_items, n_blocks);
   P.hb_valid = 0;
   const dim3 pgrid((n_blocks + P.plan_bpw - 1) / P.plan_bpw);
-  if (P.type == 1)
+#ifndef LSM_NO_E1P
+  const bool e1p = P.type != 1 && P.plan_bpw == 1 && items.n_items > 0 && items.n_items < 0xFFFFFFFFull;
+#else
+  const bool e1p = false;
+#endif
+  if (e1p) {  // batches of huge blocks: the plan item-parallel
+    if ((e = hipMemsetAsync(P.e1p_flag, 0, 4, st)) != hipSuccess) return e;
+    if ((e = hipMemsetAsync(P.sizes, 0, (size_t)n_blocks * 8, st)) != hipSuccess) return e;
+    const dim3 igrid((uint32_t)((std::max<uint64_t>(items.n_items, n_blocks) + 255) / 256));
+    hipLaunchKernelGGL(encode_e1p_lengths_kernel, igrid, dim3(256), 0, st, P);
+    if ((e = launch_excl_scan(P.erec, items.n_items, tiles, E1pOut{P.erec, P.pfirst + n_blocks, items.n_items},
+                              st)) != hipSuccess)
+      return e;
+    hipLaunchKernelGGL(encode_e1p_blocks_kernel, dim3((n_blocks + 255) / 256), dim3(256), 0, st, P);
+    hipLaunchKernelGGL(encode_e1p_offsets_kernel, igrid, dim3(256), 0, st, P);
+  } else if (P.type == 1)
     hipLaunchKernelGGL(encode_plan_kernel<true>, pgrid, dim3(256), 0, st, P);
 #ifndef LSM_PLAN_V1
   // (the wave kernel gives each wave whole blocks: with a few blocks of many items

@@ -325,6 +325,16 @@ struct Lz4OffOut {
   __device__ void operator()(uint64_t i, uint64_t prefix) const { off[i] = prefix; }
 };
 
+// lsm_lz4_plan_capped: an output larger than the caller's arena leaves every
+// range empty (each block whose header verifies then reports LSM_OVERFLOW).
+// One workgroup: every thread reads the total before any range is cleared.
+__global__ __launch_bounds__(1024) void lz4_cap_kernel(uint64_t* __restrict__ off, uint32_t n, uint64_t cap) {
+  const bool over = off[n] > cap;
+  __syncthreads();
+  if (!over) return;
+  for (uint64_t i = threadIdx.x; i <= n; i += 1024) off[i] = 0;
+}
+
 }  // namespace lsmgpu
 
 using namespace lsmgpu;
@@ -361,6 +371,16 @@ extern "C" int lsm_lz4_plan_framed(const uint8_t* d_blocks, const uint64_t* d_bl
                                    size_t workspace_bytes, void* stream) {
   return lz4_plan(d_blocks, d_block_off, n_blocks, max_block_bytes, d_out_off, d_workspace, workspace_bytes, stream,
                   kHdrLen);
+}
+
+extern "C" int lsm_lz4_plan_capped(const uint8_t* d_blocks, const uint64_t* d_block_off, uint32_t n_blocks,
+                                   uint64_t max_block_bytes, int framed, uint64_t out_cap, uint64_t* d_out_off,
+                                   void* d_workspace, size_t workspace_bytes, void* stream) {
+  const int rc = lz4_plan(d_blocks, d_block_off, n_blocks, max_block_bytes, d_out_off, d_workspace, workspace_bytes,
+                          stream, framed ? kHdrLen : 0);
+  if (rc != LSM_OK || n_blocks == 0) return rc;
+  hipLaunchKernelGGL(lz4_cap_kernel, dim3(1), dim3(1024), 0, (hipStream_t)stream, d_out_off, n_blocks, out_cap);
+  return hip_status(hipGetLastError(), "lsm_lz4_plan_capped");
 }
 
 static int lz4_decompress(const uint8_t* d_blocks, const uint64_t* d_block_off, uint32_t n_blocks, uint8_t* d_out,

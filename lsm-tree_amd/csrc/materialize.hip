@@ -32,6 +32,8 @@ struct MatParams {
   uint64_t* lens;
   uint8_t* out;
   const uint64_t* out_off;
+  uint64_t cap;       // lsm_materialize_keys_capped: arena bytes (else ~0)
+  int32_t* result;    // lsm_materialize_keys_capped: LSM_OK / LSM_OVERFLOW (else null)
 };
 
 // Restart interval of an OK block (trailer byte 0, trailer.rs:78-173).
@@ -64,6 +66,11 @@ __global__ __launch_bounds__(kMatWaves * 64) void materialize_kernel(MatParams P
   const uint32_t w = threadIdx.x >> 6;
   const uint32_t b = blockIdx.x * kMatWaves + w;
   const int lane = threadIdx.x & 63;
+  if (P.result) {  // capped arena: all keys or none (the caller sized it without a host sync)
+    const bool fits = P.out_off[P.n_items] <= P.cap;
+    if (blockIdx.x == 0 && threadIdx.x == 0) *P.result = fits ? LSM_OK : LSM_OVERFLOW;
+    if (!fits) return;
+  }
   if (b >= P.n_blocks || P.status[b] != LSM_OK) return;
   const uint64_t s = P.item_start[b], e = min((uint64_t)P.item_start[b + 1], P.n_items);
   const uint8_t* payload = P.blocks + P.block_off[b] + kHdrLen;
@@ -165,6 +172,8 @@ static int mat_params(const uint8_t* d_blocks, const uint64_t* d_block_off, uint
   P.lens = nullptr;
   P.out = nullptr;
   P.out_off = d_key_out_off;
+  P.cap = ~0ULL;
+  P.result = nullptr;
   return LSM_OK;
 }
 
@@ -201,4 +210,26 @@ extern "C" int lsm_materialize_keys(const uint8_t* d_blocks, const uint64_t* d_b
   hipLaunchKernelGGL(materialize_kernel, dim3((n_blocks + kMatWaves - 1) / kMatWaves), dim3(kMatWaves * 64), 0,
                      (hipStream_t)stream, P);
   return hip_status(hipGetLastError(), "lsm_materialize_keys");
+}
+
+extern "C" int lsm_materialize_keys_capped(const uint8_t* d_blocks, const uint64_t* d_block_off, uint32_t n_blocks,
+                                           const uint32_t* d_item_start, const int32_t* d_status,
+                                           const lsm_parsed_items* d_parsed, uint64_t n_items,
+                                           const uint64_t* d_key_out_off, uint8_t* d_key_out, uint64_t key_cap,
+                                           int32_t* d_result, void* stream) {
+  if (!d_result) return LSM_BAD_ARG;
+  MatParams P;
+  int rc = mat_params(d_blocks, d_block_off, n_blocks, d_item_start, d_status, d_parsed, n_items,
+                      const_cast<uint64_t*>(d_key_out_off), P);
+  if (rc != LSM_OK || !d_key_out) return LSM_BAD_ARG;
+  const hipStream_t st = (hipStream_t)stream;
+  if (n_blocks == 0 || n_items == 0) {
+    const int32_t ok = LSM_OK;
+    return hip_status(hipMemcpyAsync(d_result, &ok, 4, hipMemcpyHostToDevice, st), "lsm_materialize_keys_capped");
+  }
+  P.out = d_key_out;
+  P.cap = key_cap;
+  P.result = d_result;
+  hipLaunchKernelGGL(materialize_kernel, dim3((n_blocks + kMatWaves - 1) / kMatWaves), dim3(kMatWaves * 64), 0, st, P);
+  return hip_status(hipGetLastError(), "lsm_materialize_keys_capped");
 }

@@ -31,7 +31,8 @@ __device__ __forceinline__ uint64_t block_excl_scan_u64(uint64_t v, uint64_t* sh
   return wbase + incl - v;
 }
 
-static __global__ __launch_bounds__(kScanThreads) void scan_tile_reduce(const uint64_t* __restrict__ in, uint64_t n,
+template <class T>
+__global__ __launch_bounds__(kScanThreads) void scan_tile_reduce(const T* __restrict__ in, uint64_t n,
                                                                  uint64_t* __restrict__ tile_sums) {
   __shared__ uint64_t sh[kScanThreads / 64];
   const uint64_t base = (uint64_t)blockIdx.x * kScanTile + (uint64_t)threadIdx.x * kScanPerThread;
@@ -58,9 +59,10 @@ static __global__ __launch_bounds__(kScanThreads) void scan_tile_sums(uint64_t* 
   }
 }
 
-// Out(i, prefix) is called for i in [0, n] with the exclusive prefix.
-template <class Out>
-__global__ __launch_bounds__(kScanThreads) void scan_tile_apply(const uint64_t* __restrict__ in, uint64_t n,
+// Out(i, prefix) is called for i in [0, n] with the exclusive prefix.  Each
+// thread reads its inputs before its first Out call, so Out may overwrite in[i].
+template <class T, class Out>
+__global__ __launch_bounds__(kScanThreads) void scan_tile_apply(const T* in, uint64_t n,
                                                                 const uint64_t* __restrict__ tile_offsets,
                                                                 Out out) {
   __shared__ uint64_t sh[kScanThreads / 64];
@@ -84,13 +86,13 @@ __global__ __launch_bounds__(kScanThreads) void scan_tile_apply(const uint64_t* 
 
 inline uint64_t scan_tiles(uint64_t n) { return (n + kScanTile - 1) / kScanTile; }
 
-// Enqueue the scan; `tmp` holds scan_tiles(n) u64.  n >= 1.
-template <class Out>
-inline hipError_t launch_excl_scan(const uint64_t* in, uint64_t n, uint64_t* tmp, Out out, hipStream_t st) {
+// Enqueue the scan (u64 or u32 inputs, u64 prefixes); `tmp` holds scan_tiles(n) u64.  n >= 1.
+template <class T, class Out>
+inline hipError_t launch_excl_scan(const T* in, uint64_t n, uint64_t* tmp, Out out, hipStream_t st) {
   const uint64_t tiles = scan_tiles(n);
-  hipLaunchKernelGGL(scan_tile_reduce, dim3((uint32_t)tiles), dim3(kScanThreads), 0, st, in, n, tmp);
+  hipLaunchKernelGGL(scan_tile_reduce<T>, dim3((uint32_t)tiles), dim3(kScanThreads), 0, st, in, n, tmp);
   hipLaunchKernelGGL(scan_tile_sums, dim3(1), dim3(kScanThreads), 0, st, tmp, tiles);
-  hipLaunchKernelGGL(scan_tile_apply<Out>, dim3((uint32_t)tiles), dim3(kScanThreads), 0, st, in, n,
+  hipLaunchKernelGGL((scan_tile_apply<T, Out>), dim3((uint32_t)tiles), dim3(kScanThreads), 0, st, in, n,
                      (const uint64_t*)tmp, out);
   return hipGetLastError();
 }

@@ -192,6 +192,13 @@ def lib():
         L.lsm_materialize_plan.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p,
                                            C.POINTER(LsmParsed), C.c_uint64, C.c_void_p, C.c_void_p, C.c_size_t,
                                            C.c_void_p]
+        L.lsm_materialize_keys_capped.restype = C.c_int
+        L.lsm_materialize_keys_capped.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p,
+                                                  C.POINTER(LsmParsed), C.c_uint64, C.c_void_p, C.c_void_p,
+                                                  C.c_uint64, C.c_void_p, C.c_void_p]
+        L.lsm_lz4_plan_capped.restype = C.c_int
+        L.lsm_lz4_plan_capped.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_uint64, C.c_int, C.c_uint64,
+                                          C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]
         L.lsm_materialize_keys.restype = C.c_int
         L.lsm_materialize_keys.argtypes = [C.c_void_p, C.c_void_p, C.c_uint32, C.c_void_p, C.c_void_p,
                                            C.POINTER(LsmParsed), C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p]
@@ -209,6 +216,7 @@ EXPORTED_SYMBOLS = ["lsm_abi_version", "lsm_status_name", "lsm_last_error", "lsm
                     "lsm_lz4_plan_workspace_size", "lsm_lz4_plan_output", "lsm_seek_blocks", "lsm_lz4_plan_framed",
                     "lsm_lz4_decompress_framed", "lsm_scan_workspace_size", "lsm_scan_table",
                     "lsm_materialize_workspace_size", "lsm_materialize_plan", "lsm_materialize_keys",
+                    "lsm_materialize_keys_capped", "lsm_lz4_plan_capped",
                     "lsm_xxh3_128_stream_state_size", "lsm_xxh3_128_stream_workspace_size",
                     "lsm_xxh3_128_stream_init", "lsm_xxh3_128_stream_update", "lsm_xxh3_128_stream_digest",
                     "lsm_xxh3_128_stream_init_batch", "lsm_xxh3_128_stream_batch_workspace_size",
@@ -632,7 +640,7 @@ def lz4_decompress_blocks(blocks, block_off, n_blocks=None, max_block_bytes=LZ4_
 
 
 def decode_lz4_blocks(blocks, block_off, n_blocks=None, expect_type=-1, item_cap=None, fields=None,
-                      max_block_bytes=LZ4_MAX_BLOCK, stream=None):
+                      max_block_bytes=LZ4_MAX_BLOCK, stream=None, frames_cap=None):
     """LZ4 blocks end to end: Block::from_reader(Lz4) then DataBlock::new + iter
     (block/mod.rs:104-118, data_block/mod.rs:335,476).  lsm_lz4_plan_framed ->
     lsm_lz4_decompress_framed (frames = Header' || decompressed payload) ->
@@ -641,16 +649,26 @@ def decode_lz4_blocks(blocks, block_off, n_blocks=None, expect_type=-1, item_cap
     "frame_off" and "status" = the decompress status where it is not OK, else the
     decode status ("decode_status": the decode's own statuses: a block whose
     decompression failed has an all-zero frame header, so it is BAD_MAGIC there
-    even without the merge)."""
+    even without the merge).  frames_cap (bytes): size the frame arena without
+    reading the plan back (no host sync; every block whose header verifies reports
+    LSM_OVERFLOW when the frames do not fit, and item_cap defaults to frames_cap // 3)."""
     torch = _torch()
     n = block_off.numel() - 1 if n_blocks is None else n_blocks
     dev = blocks.device
     frame_off = torch.zeros(n + 1, dtype=torch.int64, device=dev)
     if n:
         pws = torch.empty(lib().lsm_lz4_plan_workspace_size(n), dtype=torch.uint8, device=dev)
-        _check(lib().lsm_lz4_plan_framed(_ptr(blocks), _ptr(block_off), n, max_block_bytes, _ptr(frame_off),
-                                         _ptr(pws), pws.numel(), _stream(stream)), "lsm_lz4_plan_framed")
-    total = int(frame_off[-1].item()) if n else 0
+        if frames_cap is not None:
+            _check(lib().lsm_lz4_plan_capped(_ptr(blocks), _ptr(block_off), n, max_block_bytes, 1, frames_cap,
+                                             _ptr(frame_off), _ptr(pws), pws.numel(), _stream(stream)),
+                   "lsm_lz4_plan_capped")
+        else:
+            _check(lib().lsm_lz4_plan_framed(_ptr(blocks), _ptr(block_off), n, max_block_bytes, _ptr(frame_off),
+                                             _ptr(pws), pws.numel(), _stream(stream)), "lsm_lz4_plan_framed")
+    if frames_cap is not None:
+        total = frames_cap
+    else:
+        total = int(frame_off[-1].item()) if n else 0
     frames = padded_bytes(total, dev)
     zst = torch.empty(max(n, 1), dtype=torch.int32, device=dev)
     ws = torch.empty(lib().lsm_lz4_workspace_size(n), dtype=torch.uint8, device=dev)
@@ -669,14 +687,17 @@ def decode_lz4_blocks(blocks, block_off, n_blocks=None, expect_type=-1, item_cap
     return out
 
 
-def materialize_keys(blocks, block_off, n_blocks, out, n_items=None, stream=None):
+def materialize_keys(blocks, block_off, n_blocks, out, n_items=None, stream=None, key_cap=None):
     """DataBlockParsedItem::materialize (data_block/mod.rs:296-315) of decode output `out`
     (dict from decode_blocks / scan_table) -> (keys uint8 cuda arena, key_off int64 cuda
-    [n_items+1]); values stay (val_off, val_len) sub-slices of each payload."""
+    [n_items+1]); values stay (val_off, val_len) sub-slices of each payload.
+    key_cap (bytes): no host sync (n_items defaults to the parsed arrays' capacity,
+    lsm_materialize_keys_capped); returns (keys, key_off, result) with result a
+    device int32 [1]: LSM_OK, or LSM_OVERFLOW when the keys exceed key_cap (none written)."""
     torch = _torch()
     dev = blocks.device
     if n_items is None:
-        n_items = int(out["item_start"][n_blocks].item())
+        n_items = out["key_off"].numel() if key_cap is not None else int(out["item_start"][n_blocks].item())
     key_off = torch.zeros(n_items + 1, dtype=torch.int64, device=dev)
     ps = LsmParsed()
     for f, _ in PARSED_FIELDS:
@@ -685,6 +706,12 @@ def materialize_keys(blocks, block_off, n_blocks, out, n_items=None, stream=None
     args = (_ptr(blocks), _ptr(block_off), n_blocks, _ptr(out["item_start"]), _ptr(out["status"]), C.byref(ps), n_items)
     _check(lib().lsm_materialize_plan(*args, _ptr(key_off), _ptr(ws), ws.numel(), _stream(stream)),
            "lsm_materialize_plan")
+    if key_cap is not None:
+        keys = padded_bytes(key_cap, dev)
+        result = torch.empty(1, dtype=torch.int32, device=dev)
+        _check(lib().lsm_materialize_keys_capped(*args, _ptr(key_off), _ptr(keys), key_cap, _ptr(result),
+                                                 _stream(stream)), "lsm_materialize_keys_capped")
+        return keys, key_off, result
     total = int(key_off[-1].item()) if n_items else 0
     keys = padded_bytes(total, dev)
     _check(lib().lsm_materialize_keys(*args, _ptr(key_off), _ptr(keys), _stream(stream)), "lsm_materialize_keys")

@@ -69,3 +69,25 @@ def test_encode_backward_key_offsets(gpu, ratio):
     buf, off, st = _encode(gpu, bad_items, starts, 4, ratio)
     # blocks other than 5 only use offsets of their own items, unchanged
     _check(items, starts, buf, off, st, {5}, 4, ratio)
+
+
+@pytest.mark.parametrize("ratio", [0.0, 1.33])
+def test_encode_huge_batch_args(gpu, ratio):
+    """A batch of ~20 Ki items per block (the item-parallel plan, E1p): a
+    40 000-item block, an empty one, a 50-item one, a 59 950-item one and one
+    past n_items: the empty and the out-of-range blocks are BAD_ARG, the others
+    bit-exact."""
+    items = counter_items(100000, seed=23)
+    starts = np.array([0, 40000, 40000, 40050, 99000 + 1000, 100005], np.int64)
+    starts[4] = 100000 - 1000  # (block 3: 58 950 items)
+    buf, off, st = _encode(gpu, items, starts, 16, ratio)
+    _check(items, starts, buf, off, st, {1, 4}, 16, ratio)
+
+
+def test_encode_huge_batch_not_monotone(gpu):
+    """E1p: an item_start array that goes backwards rejects every block."""
+    items = counter_items(100000, seed=24)
+    starts = np.array([0, 40000, 30000, 100000], np.int64)
+    _, off, st = _encode(gpu, items, starts, 16, 0.0)
+    assert (st == BAD_ARG).all(), st
+    assert (off == 0).all()

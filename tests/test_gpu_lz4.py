@@ -184,3 +184,30 @@ def test_lz4_chained_parse(gpu):
     # the frame header is a well-formed uncompressed-size header of the stored checksum
     st0, h = pyoracle.header_decode(frames[foff[0]:foff[0] + 33].tobytes())
     assert st0 == 0 and h.data_length == len(raws[0]) == h.uncompressed_length
+
+
+def test_lz4_chain_capped_no_sync(gpu):
+    """lsm_lz4_plan_capped (framed): a frame arena sized without reading the plan
+    back.  Exactly large enough: the same statuses and fields as the synchronising
+    chain; one byte short: every block reports OVERFLOW and no frame is written."""
+    import torch
+    raws = [_payloads(52, 16, "counter", 200 + s) for s in range(20)] + [_payloads(820, 4, "random", 7)]
+    blocks = [_frame(lz4_compress(r), len(r)) for r in raws]
+    off = np.zeros(len(blocks) + 1, np.int64)
+    off[1:] = np.cumsum([len(b) for b in blocks])
+    buf = gpu.to_device_bytes(np.frombuffer(b"".join(blocks), np.uint8))
+    d_off = torch.from_numpy(off).cuda()
+    ref = gpu.decode_lz4_blocks(buf, d_off, expect_type=0)
+    torch.cuda.synchronize()
+    total = int(ref["frame_off"][-1].item())
+    n_items = int(ref["item_start"][len(blocks)].item())
+    got = gpu.decode_lz4_blocks(buf, d_off, expect_type=0, frames_cap=total)
+    torch.cuda.synchronize()
+    assert (got["status"][:len(blocks)] == 0).all() and (ref["status"][:len(blocks)] == 0).all()
+    assert torch.equal(got["frame_off"], ref["frame_off"])
+    for f in ("seqno", "key_off", "val_off", "val_len", "key_len", "prefix_len", "vtype"):
+        assert torch.equal(got[f][:n_items], ref[f][:n_items]), f
+    short = gpu.decode_lz4_blocks(buf, d_off, expect_type=0, frames_cap=total - 1)
+    torch.cuda.synchronize()
+    assert (short["status"][:len(blocks)] == 6).all()  # LSM_OVERFLOW
+    assert (short["frame_off"] == 0).all() and int((short["frames"] != 0).sum().item()) == 0

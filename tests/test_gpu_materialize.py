@@ -105,3 +105,31 @@ def test_materialize_output_past_2gib(gpu):
     assert int(key_off[n].item()) == n * 1000 and n * 1000 > (1 << 31) + (1 << 28)
     assert torch.equal(key_off[:n + 1], torch.arange(n + 1, device=key_off.device, dtype=key_off.dtype) * 1000)
     assert torch.equal(keys[:n * 1000], items["keys"][:n * 1000])
+
+
+def test_materialize_capped_no_sync(gpu, oracle):
+    """lsm_materialize_keys_capped: an arena sized without reading the plan back.
+    Large enough: the keys and offsets equal the two-call path's (items past
+    item_start[n_blocks], up to the parsed arrays' capacity, get empty keys);
+    one byte short: LSM_OVERFLOW on the device and nothing written."""
+    import torch
+    blocks = _blocks(oracle)
+    buf, off = pack(blocks)
+    d_blocks = gpu.to_device_bytes(buf)
+    d_off = torch.from_numpy(off.astype(np.int64)).cuda()
+    n = len(blocks)
+    out = gpu.decode_blocks(d_blocks, d_off, n)
+    keys, key_off = gpu.materialize_keys(d_blocks, d_off, n, out)
+    torch.cuda.synchronize()
+    total = int(key_off[-1].item())
+    n_items = key_off.numel() - 1
+    k2, o2, res = gpu.materialize_keys(d_blocks, d_off, n, out, key_cap=total)
+    torch.cuda.synchronize()
+    assert int(res.item()) == 0
+    assert o2.numel() == out["key_off"].numel() + 1
+    assert torch.equal(o2[:n_items + 1], key_off) and (o2[n_items:] == total).all()
+    assert torch.equal(k2[:total], keys[:total])
+    k3, o3, res3 = gpu.materialize_keys(d_blocks, d_off, n, out, key_cap=total - 1)
+    torch.cuda.synchronize()
+    assert int(res3.item()) == 6  # LSM_OVERFLOW
+    assert int((k3[:total - 1] != 0).sum().item()) == 0  # (padded_bytes zero-fills; nothing written)
