@@ -182,6 +182,10 @@ def lib():
         L.lsm_lz4_decompress_framed.argtypes = L.lsm_lz4_decompress_blocks.argtypes
         L.lsm_scan_workspace_size.restype = C.c_size_t
         L.lsm_scan_workspace_size.argtypes = [C.c_uint32]
+        L.lsm_scan_table_async.restype = C.c_int
+        L.lsm_scan_table_async.argtypes = [C.c_void_p, C.c_uint64, C.POINTER(LsmTableScan), C.c_void_p, C.c_uint32,
+                                           C.c_uint32, C.POINTER(LsmParsed), C.c_uint64, C.c_void_p, C.c_void_p,
+                                           C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]
         L.lsm_scan_table.restype = C.c_int
         L.lsm_scan_table.argtypes = [C.c_void_p, C.c_uint64, C.POINTER(LsmTableScan), C.c_void_p, C.c_uint32,
                                      C.POINTER(LsmParsed), C.c_uint64, C.c_void_p, C.c_void_p,
@@ -214,7 +218,7 @@ EXPORTED_SYMBOLS = ["lsm_abi_version", "lsm_status_name", "lsm_last_error", "lsm
                     "lsm_bloom_calculate_m", "lsm_bloom_shape", "lsm_bloom_filter_size", "lsm_hash64_keys",
                     "lsm_bloom_build", "lsm_bloom_contains", "lsm_lz4_workspace_size", "lsm_lz4_decompress_blocks",
                     "lsm_lz4_plan_workspace_size", "lsm_lz4_plan_output", "lsm_seek_blocks", "lsm_lz4_plan_framed",
-                    "lsm_lz4_decompress_framed", "lsm_scan_workspace_size", "lsm_scan_table",
+                    "lsm_lz4_decompress_framed", "lsm_scan_workspace_size", "lsm_scan_table", "lsm_scan_table_async",
                     "lsm_materialize_workspace_size", "lsm_materialize_plan", "lsm_materialize_keys",
                     "lsm_materialize_keys_capped", "lsm_lz4_plan_capped",
                     "lsm_xxh3_128_stream_state_size", "lsm_xxh3_128_stream_workspace_size",
@@ -719,10 +723,13 @@ def materialize_keys(blocks, block_off, n_blocks, out, n_items=None, stream=None
 
 
 def scan_table(file, file_len, tli_off, tli_size, two_level=False, global_seqno=0, block_count=0, cap_blocks=None,
-               item_cap=None, fields=None, stream=None):
+               item_cap=None, fields=None, stream=None, sync=True, data_blocks_hint=0):
     """Scanner over a table file image (scanner.rs:24-92): file = padded uint8 cuda tensor.
     Returns dict: table_status (int), n_blocks (int), block_off (int64 cuda [n+1]),
-    the parsed fields, item_start and status (as decode_blocks)."""
+    the parsed fields, item_start and status (as decode_blocks).
+    sync=False: lsm_scan_table_async (no host synchronisation): table_status and
+    n_blocks are device int32 / uint32 tensors of one element, block_off holds
+    cap_blocks + 1 entries (data_blocks_hint bounds the data decode, e.g. block_count)."""
     torch = _torch()
     dev = file.device
     if cap_blocks is None:
@@ -736,6 +743,15 @@ def scan_table(file, file_len, tli_off, tli_size, two_level=False, global_seqno=
     for f, _ in PARSED_FIELDS:
         setattr(ps, f, out[f].data_ptr() if f in out else None)
     t = LsmTableScan(tli_off, tli_size, int(bool(two_level)), global_seqno & (2 ** 64 - 1), block_count)
+    if not sync:
+        d_nb = torch.zeros(1, dtype=torch.int32, device=dev)
+        d_ts = torch.zeros(1, dtype=torch.int32, device=dev)
+        _check(lib().lsm_scan_table_async(_ptr(file), file_len, C.byref(t), _ptr(block_off), cap_blocks,
+                                          data_blocks_hint, C.byref(ps), item_cap, _ptr(out["item_start"]),
+                                          _ptr(out["status"]), _ptr(d_nb), _ptr(d_ts), _ptr(ws), ws.numel(),
+                                          _stream(stream)), "lsm_scan_table_async")
+        out["table_status"], out["n_blocks"], out["block_off"] = d_ts, d_nb, block_off
+        return out
     nb, tst = C.c_uint32(), C.c_int32()
     _check(lib().lsm_scan_table(_ptr(file), file_len, C.byref(t), _ptr(block_off), cap_blocks, C.byref(ps), item_cap,
                                 _ptr(out["item_start"]), _ptr(out["status"]), C.byref(nb), C.byref(tst), _ptr(ws),

@@ -14,15 +14,22 @@ from helpers import FIELD_VIEW, counter_items, prefix_items, random_sorted_items
 pytestmark = pytest.mark.gpu
 
 
-def _scan(L, t, global_seqno=0, block_count=None, cap_blocks=None, file=None):
+def _scan(L, t, global_seqno=0, block_count=None, cap_blocks=None, file=None, sync=True, hint=0):
+    """sync=False: lsm_scan_table_async, its device results read back here and
+    shaped like the synchronising call's (block_off cut to n_blocks + 1)."""
     import torch
     data = t["file"] if file is None else file
     d_file = L.to_device_bytes(data)
     bc = t["block_count"] if block_count is None else block_count
     out = L.scan_table(d_file, len(data), t["tli_off"], t["tli_size"], two_level=t.get("two_level", False),
-                       global_seqno=global_seqno, block_count=bc, cap_blocks=cap_blocks)
+                       global_seqno=global_seqno, block_count=bc, cap_blocks=cap_blocks, sync=sync,
+                       data_blocks_hint=hint)
     torch.cuda.synchronize()
     res = {k: (v.cpu().numpy() if hasattr(v, "cpu") else v) for k, v in out.items()}
+    if not sync:
+        res["table_status"] = int(res["table_status"][0])
+        res["n_blocks"] = int(res["n_blocks"][0])
+        res["block_off"] = res["block_off"][:res["n_blocks"] + 1]
     return res
 
 
@@ -151,3 +158,40 @@ def test_scan_table_level_errors(gpu, oracle):
     bad = dict(t)
     bad["tli_off"], bad["tli_size"] = 0, int(t["block_off"][1])
     assert _scan(gpu, bad)["table_status"] == 7
+
+
+@pytest.mark.parametrize("two_level", [False, True])
+def test_scan_async_matches(gpu, oracle, two_level):
+    """lsm_scan_table_async (no host synchronisation, counts on the device): the
+    same blocks, items and statuses as the Scanner, with a cap of about 4x the
+    blocks and with the exact block count as the data hint."""
+    t = _table(oracle, counter_items(52 * 600, seed=12, tomb_frac=0.05), two_level)
+    for cap, hint in ((4 * t["block_count"], 0), (4 * t["block_count"], t["block_count"])):
+        g = _scan(gpu, t, 9, cap_blocks=cap, sync=False, hint=hint)
+        _check_against_scanner(oracle, g, t, 9)
+    data = bytearray(t["file"])
+    data[int(t["block_off"][23]) + 100] ^= 0x40
+    g = _scan(gpu, t, 0, file=bytes(data), cap_blocks=2 * t["block_count"], sync=False)
+    _check_against_scanner(oracle, g, t, 0, data=bytes(data))
+
+
+def test_scan_async_level_errors(gpu, oracle):
+    """The table statuses of test_scan_table_level_errors through the async call
+    (n_blocks 0 for a failed table), plus a data hint below the block count."""
+    t = _table(oracle, counter_items(52 * 50, seed=6), False)
+    cap = 4 * t["block_count"]
+    data = bytearray(t["file"])
+    data[t["tli_off"] + 40] ^= 1
+    g = _scan(gpu, t, file=bytes(data), cap_blocks=cap, sync=False)
+    assert g["table_status"] == 4 and g["n_blocks"] == 0
+    assert _scan(gpu, t, block_count=t["block_count"] + 1, cap_blocks=cap, sync=False)["table_status"] == 5
+    assert _scan(gpu, t, cap_blocks=10, sync=False)["table_status"] == 6
+    assert _scan(gpu, t, cap_blocks=cap, hint=t["block_count"] - 1, sync=False)["table_status"] == 6
+    bad = dict(t)
+    bad["tli_size"] = t["tli_size"] + 1
+    assert _scan(gpu, bad, cap_blocks=cap, sync=False)["table_status"] == 8
+    bad = dict(t)
+    bad["tli_off"], bad["tli_size"] = 0, int(t["block_off"][1])
+    assert _scan(gpu, bad, cap_blocks=cap, sync=False)["table_status"] == 7
+    t2 = _table(oracle, counter_items(52 * 50, seed=6), True)
+    assert _scan(gpu, t2, cap_blocks=4 * t2["block_count"], sync=False)["table_status"] == 0
