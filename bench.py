@@ -446,9 +446,9 @@ def bench_config5(torch, lsmgpu, steps, rank, world, dist, dev, threads, total_b
 def bench_large_blocks(torch, lsmgpu, threads, steps=5):
     """Data blocks above the general path's 72 KiB stage (the writer's data_block_size
     goes up to 4 MiB, writer/mod.rs:193-198): 240 x 1 MiB and 60 x 4 MiB blocks of
-    16 B counter keys / 64 B values, encoded on the device (E3), decoded through
-    the stage in 64 KiB chunks (decode_chunked); every block checked against the
-    oracle (encoded bytes and decoded fields)."""
+    16 B counter keys / 64 B values, encoded and decoded across the whole GPU (the
+    wrappers hand the workspace pool for batches of such blocks); every block
+    checked against the oracle (encoded bytes and decoded fields)."""
     res = {}
     for name, nb, ipb, bs in (("1MiB", 240, 13108, 1 << 20), ("4MiB", 60, 52429, 4 << 20)):
         check_cut_rule(lsmgpu, ipb, 16, 64, bs)  # = the writer's cut at that data_block_size
@@ -472,8 +472,10 @@ def bench_large_blocks(torch, lsmgpu, threads, steps=5):
                      "decode_GiB_per_s": round(total / (dec_ms * 1e-3) / 2 ** 30, 2), "oracle_checked_blocks": nb}
         del items, enc, out, ref_buf
         torch.cuda.empty_cache()
-    res["note"] = ("encode: plan workgroups of ~16 Ki items, then one 8-wave workgroup per block straight in HBM (encode_large_kernel: record per thread at its E1 offset, per-KiB XXH3 contributions on every wave, chain on one); decode: 4-wave workgroup per "
-                   "block through a 72 KiB stage in 64 KiB chunks (XXH3 chain carried across chunks)")
+    res["note"] = ("the workspace pool (lsm_*_workspace_size_ex) spreads each block over the GPU: encode = "
+                   "item-parallel plan (E1p), record units assembled in LDS + 16-B copy-out, KiB contribution "
+                   "units, eight XXH3 chains per block; decode = 32 KiB staged windows (phase A/B or interval "
+                   "walks, KiB contributions), eight chains per block, finish")
     return res
 
 
@@ -706,7 +708,21 @@ def bench_lz4(torch, lsmgpu, enc, n_blocks, reps=5, sample=131072):
         lsmgpu.decode_lz4_blocks(dbuf, doff, expect_type=0, item_cap=nb * 52, fields=DATA_FIELDS)
     torch.cuda.synchronize()
     ms_chain = (time.perf_counter() - t0) * 1e3 / reps
+    # the same chain without the host sync: the frame arena sized by the caller (raw bytes
+    # + one 33-B frame header per block: what the plan would find), lsm_lz4_plan_capped
+    fcap = raw_total + 33 * nb
+    ch = lsmgpu.decode_lz4_blocks(dbuf, doff, expect_type=0, item_cap=nb * 52, fields=DATA_FIELDS, frames_cap=fcap)
+    torch.cuda.synchronize()
+    assert int((ch["status"][:nb] != 0).sum().item()) == 0, "lz4 capped chain: status"
+    del ch
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        lsmgpu.decode_lz4_blocks(dbuf, doff, expect_type=0, item_cap=nb * 52, fields=DATA_FIELDS, frames_cap=fcap)
+    torch.cuda.synchronize()
+    ms_capped = (time.perf_counter() - t0) * 1e3 / reps
     return {"blocks": nb, "stored_bytes": int(loff[-1]), "raw_bytes": raw_total, "ms": round(ms, 4),
+            "chain_capped_ms": round(ms_capped, 4),
+            "chain_capped_GiB_per_s_raw": round(raw_total / (ms_capped * 1e-3) / 2 ** 30, 1),
             "GiB_per_s_raw": round(raw_total / (ms * 1e-3) / 2 ** 30, 1),
             "note": "plan (verified headers -> output offsets) + header / xxh3_128 verify + LZ4 decode, every "
                     "decompressed byte checked",
@@ -773,10 +789,28 @@ def bench_table_scan(torch, lsmgpu, items, enc, nb, n_items, ref_out, reps=3, pa
         lsmgpu.scan_table(f, file_len, tli_off, tli.numel(), **kw)
     torch.cuda.synchronize()
     ms = (time.perf_counter() - t0) * 1e3 / reps
+    # without host synchronisation: lsm_scan_table_async, bounds from the metadata's block
+    # count and the TLI size (at most one partition handle per 4 TLI bytes)
+    kwa = dict(kw, sync=False, data_blocks_hint=nb, index_blocks_hint=int(tli.numel()) // 4)
+    outa = lsmgpu.scan_table(f, file_len, tli_off, tli.numel(), **kwa)
+    torch.cuda.synchronize()
+    assert int(outa["table_status"].item()) == 0 and int(outa["n_blocks"].item()) == nb
+    assert torch.equal(outa["block_off"][:nb + 1], boff) and int((outa["status"][:nb] != 0).sum().item()) == 0
+    assert torch.equal(outa["seqno"][:n_items], ref_out["seqno"][:n_items] + 1000)
+    for fld in DATA_FIELDS[1:]:
+        assert torch.equal(outa[fld][:n_items], ref_out[fld][:n_items]), fld
+    del outa
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        lsmgpu.scan_table(f, file_len, tli_off, tli.numel(), **kwa)
+    torch.cuda.synchronize()
+    ms_a = (time.perf_counter() - t0) * 1e3 / reps
     return {"data_blocks": nb, "index_partitions": npart, "tli_bytes": int(tli.numel()), "file_bytes": file_len,
             "ms": round(ms, 4), "GiB_per_s": round(file_len / (ms * 1e-3) / 2 ** 30, 1),
+            "async_ms": round(ms_a, 4), "async_GiB_per_s": round(file_len / (ms_a * 1e-3) / 2 ** 30, 1),
             "note": "host-timed lsm_scan_table call (2 index levels, one stream sync each, then the data decode); "
-                    "every item equal to the plain decode with global_seqno 1000 added"}
+                    "async: lsm_scan_table_async (no host sync; partitions bounded by tli_size / 4, data blocks by "
+                    "the block count); every item equal to the plain decode with global_seqno 1000 added"}
 
 
 def bench_materialize(torch, lsmgpu, enc, nb, out, n_items, reps=5):
@@ -793,9 +827,23 @@ def bench_materialize(torch, lsmgpu, enc, nb, out, n_items, reps=5):
     b.record()
     torch.cuda.synchronize()
     ms = a.elapsed_time(b) / reps
+    # the sync-free form: an arena the caller sized (here: exactly), lsm_materialize_keys_capped
+    k2, o2, res = lsmgpu.materialize_keys(enc["buf"], enc["block_off"], nb, out, n_items, key_cap=total)
+    torch.cuda.synchronize()
+    assert int(res.item()) == 0 and torch.equal(o2, key_off) and torch.equal(k2[:total], keys[:total])
+    del k2
+    a.record()
+    for _ in range(reps):
+        lsmgpu.materialize_keys(enc["buf"], enc["block_off"], nb, out, n_items, key_cap=total)
+    b.record()
+    torch.cuda.synchronize()
+    ms_c = a.elapsed_time(b) / reps
     return keys[:total], {"items": n_items, "key_bytes": total, "ms": round(ms, 4),
                           "GiB_per_s_keys": round(total / (ms * 1e-3) / 2 ** 30, 1),
-                          "note": "plan (lengths + scan) + copy, host-synchronised once for the arena size"}
+                          "capped_ms": round(ms_c, 4), "capped_GiB_per_s_keys": round(total / (ms_c * 1e-3) / 2 ** 30, 1),
+                          "note": "plan (lengths + scan) + copy, host-synchronised once for the arena size; capped: "
+                                  "lsm_materialize_keys_capped into an arena sized by the caller, no host sync, "
+                                  "same keys"}
 
 
 # ----------------------------------------------------------- host-inclusive

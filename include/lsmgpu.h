@@ -499,17 +499,19 @@ int lsm_scan_table(const uint8_t* d_file, uint64_t file_len, const lsm_table_sca
                    uint32_t* d_item_start, int32_t* d_status, uint32_t* n_blocks, int32_t* table_status,
                    void* d_workspace, size_t workspace_bytes, void* stream);
 /* lsm_scan_table without host synchronisation: the entry counts stay on the
- * device and every level is launched for the caller's bounds (cap_blocks + 1
- * index blocks; data_blocks_hint data blocks, e.g. the metadata's
+ * device and every level is launched for the caller's bounds (index_blocks_hint
+ * index partitions of a two-level index, e.g. the TLI size / 4, else
+ * cap_blocks; data_blocks_hint data blocks, e.g. the metadata's
  * data_block_count, else cap_blocks: keep them tight, the ranges past the real
- * count are decoded as empty blocks).  *d_n_blocks / *d_table_status (device)
+ * counts are decoded as empty blocks; a level with more entries than its bound
+ * gets LSM_OVERFLOW).  *d_n_blocks / *d_table_status (device)
  * receive what lsm_scan_table returns in *n_blocks / *table_status; a table
  * with more data blocks than the hint gets LSM_OVERFLOW.  d_item_start /
  * d_status hold data_blocks_hint (or cap_blocks) + 1 / entries: those past
  * *d_n_blocks are not meaningful.  Same workspace as lsm_scan_table. */
 int lsm_scan_table_async(const uint8_t* d_file, uint64_t file_len, const lsm_table_scan* table,
-                         uint64_t* d_block_off, uint32_t cap_blocks, uint32_t data_blocks_hint,
-                         const lsm_parsed_items* d_out, uint64_t item_cap, uint32_t* d_item_start, int32_t* d_status,
+                         uint64_t* d_block_off, uint32_t cap_blocks, uint32_t index_blocks_hint,
+                         uint32_t data_blocks_hint, const lsm_parsed_items* d_out, uint64_t item_cap, uint32_t* d_item_start, int32_t* d_status,
                          uint32_t* d_n_blocks, int32_t* d_table_status, void* d_workspace, size_t workspace_bytes,
                          void* stream);
 

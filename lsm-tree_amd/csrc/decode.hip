@@ -47,9 +47,6 @@ constexpr uint32_t kMaxGroup = LSM_DEC_MAX_GROUP;  // blocks per staged group
 // decode_deferred_staged_kernel, the general path with the LEB cursor; that
 // one writes the final status.
 constexpr int32_t ST_DEFER = 0x7F;
-#ifndef LSM_PB32
-#define LSM_PB32 0
-#endif
 constexpr uint32_t kStagePad = 256;  // readable LDS bytes past the span (fast parsers read <= 138)
 
 // Record descriptor (one u64 per group item, LDS), written by phase A, read
@@ -409,17 +406,7 @@ __device__ __forceinline__ int parse_data_shape(const uint8_t* base, uint32_t p0
   uint32_t n4, vl;
   bool vl_ok;
   rec_value(vt, read_u16_unaligned(base, p0 + min(pos + q, end)), n4, vl, vl_ok);
-#if LSM_PB32
-  // (n1 + n2 + 2 <= 8 bytes of header: the shared varint is at most 3 bytes, decoded in 32 bits)
-  uint32_t shared = 0;
-  if (!restart) {
-    uint32_t x = (uint32_t)(h >> (8 * (n1 + 1)));
-    x &= n2 >= 4 ? ~0u : (1u << (8 * n2)) - 1;
-    shared = ((x & 0x7F) | ((x >> 1) & 0x3F80) | ((x >> 2) & 0x1FC000) | ((x >> 3) & 0xFE00000)) & 0xFFFF;
-  }
-#else
   const uint32_t shared = restart ? 0u : (uint32_t)leb_val8(h >> (8 * (n1 + 1)), n2) & 0xFFFF;
-#endif
   const uint32_t val_off = pos + q + n4;
   f.seqno = leb_val8(h >> 8, n1);
   f.handle_off = 0;
@@ -430,13 +417,8 @@ __device__ __forceinline__ int parse_data_shape(const uint8_t* base, uint32_t p0
   f.val_len = vl;
   f.vtype = (uint8_t)vt;
   next = val_off + vl;
-#if LSM_PB32
-  // (positions < 2^23, vl < 2^14, shared < 2^16: no 32-bit overflow)
-  const bool bad = (pos + q + n4 > end) || (val_off + vl > end) || (!restart && base_key_off + shared > end);
-#else
   const bool bad = (pos + q + n4 > end) || ((uint64_t)val_off + vl > end) ||
                    (!restart && (uint64_t)base_key_off + shared > end);
-#endif
   return !valid_vtype(vt) ? -1 : (!vl_ok ? 0 : (bad ? -1 : 1));
 }
 
@@ -857,7 +839,10 @@ constexpr uint32_t kHugeOwner = kHugeMeta + 80;
 constexpr uint32_t kHugeRec = kHugeOwner + kHugeMaxIv;
 constexpr uint32_t kHugeLds = 64 + kHugeRec + 8 * (kHugeTile + 1);
 constexpr uint32_t kHugeGrid = 2048;
-constexpr uint32_t kHugeChainGrid = 1024, kHugeChainLds = 40 * 1024;
+#ifndef LSM_CHAIN_LDS  // an unused LDS request that spreads the chain workgroups one per SIMD (0: none)
+#define LSM_CHAIN_LDS 0  // (40 KiB: 0.29-0.33 vs 0.29-0.31 ms for the large-block legs, r04 A/B)
+#endif
+constexpr uint32_t kHugeChainLds = LSM_CHAIN_LDS, kHugeChainGrid = kHugeChainLds ? 1024 : 2048;
 
 struct HugeRec {
   BlockMeta m;         // header view, trailer fields merged in: m.st = trailer status (header checks passed)

@@ -1537,13 +1537,30 @@ __device__ __forceinline__ uint64_t shfl_down64(uint64_t v, int o) {
          ((uint64_t)(uint32_t)__shfl_down((int)(uint32_t)(v >> 32), o) << 32);
 }
 
+// The block of item i from the workgroup's first item's block (one binary search
+// per workgroup, by thread 0): blocks of >= 16 Ki items on average leave at most
+// a step or two per thread.
+__device__ __forceinline__ uint32_t wg_block_of_item(const EncodeParams& P, uint32_t i, uint32_t* sh) {
+  const uint32_t i_begin = clamped_start(P, 0), i_end = clamped_start(P, P.n_blocks);
+  if (threadIdx.x == 0) {
+    const uint32_t first = max(blockIdx.x * 256u, i_begin);
+    *sh = first < i_end ? block_of_item(P, first) : 0;
+  }
+  __syncthreads();
+  uint32_t b = *sh;
+  while (b + 1 < P.n_blocks && clamped_start(P, b + 1) <= i) ++b;
+  return b;
+}
+
 __global__ __launch_bounds__(256) void encode_e1p_lengths_kernel(EncodeParams P) {
+  __shared__ uint32_t sb;
   const uint32_t gid = blockIdx.x * 256 + threadIdx.x;
   if (gid < P.n_blocks && clamped_start(P, gid + 1) < clamped_start(P, gid)) atomicOr(P.e1p_flag, 1u);
-  if ((uint64_t)gid >= P.it.n_items) return;
   const uint32_t i = gid, i_begin = clamped_start(P, 0), i_end = clamped_start(P, P.n_blocks);
   const bool in = i >= i_begin && i < i_end;
-  const uint32_t b = in ? block_of_item(P, i) : 0;
+  const uint32_t bw = wg_block_of_item(P, in ? i : 0, &sb);  // (every thread: it holds a barrier)
+  if ((uint64_t)gid >= P.it.n_items) return;
+  const uint32_t b = in ? bw : 0;
   const uint32_t s = clamped_start(P, b), e = clamped_start(P, b + 1);
   const bool live = in && s <= i && i < e;  // (not, for a non-monotone array: every block is rejected)
   const uint32_t ri = P.ri, jj = i - s;
@@ -1640,11 +1657,12 @@ __global__ __launch_bounds__(256) void encode_e1p_blocks_kernel(EncodeParams P) 
 }
 
 __global__ __launch_bounds__(256) void encode_e1p_offsets_kernel(EncodeParams P) {
+  __shared__ uint32_t sb;
   const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-  if ((uint64_t)i >= P.it.n_items || P.e1p_flag[0]) return;
   const uint32_t i_begin = clamped_start(P, 0), i_end = clamped_start(P, P.n_blocks);
-  if (i < i_begin || i >= i_end) return;
-  const uint32_t b = block_of_item(P, i);
+  const bool in = i >= i_begin && i < i_end;
+  const uint32_t b = wg_block_of_item(P, in ? i : 0, &sb);  // (every thread: it holds a barrier)
+  if ((uint64_t)i >= P.it.n_items || P.e1p_flag[0] || !in) return;
   if ((P.plans[b].step_flags >> 8) & kPlanBad) return;
   const uint32_t s = clamped_start(P, b), n = clamped_start(P, b + 1) - s;
   const uint32_t roff = P.erec[i] - P.pfirst[b], jj = i - s;
@@ -2287,6 +2305,9 @@ constexpr uint32_t kEHugeItems = 1024;  // items per record unit, at most (four 
 constexpr uint32_t kEHugeImg = 2 * 4 * kE3HashChunk;  // LDS image of a record unit (the tail unit's vote arrays)
 constexpr uint32_t kEHugeKib = 32;      // KiB blocks per hash unit (eight per wave)
 constexpr uint32_t kEHugeGrid = 2048;
+#ifndef LSM_CHAIN_LDS  // an unused LDS request that spreads the chain workgroups one per SIMD (0: none)
+#define LSM_CHAIN_LDS 0
+#endif
 
 struct EncHuge {
   uint64_t dst_off;
@@ -2804,7 +2825,7 @@ hipError_t launch_encode(const lsm_items& items, const uint32_t* starts, uint32_
     hipLaunchKernelGGL(encode_huge_records_kernel, dim3(kEHugeGrid), dim3(256), 0, st, P);
     hipLaunchKernelGGL(encode_huge_contrib_kernel, dim3(kEHugeGrid), dim3(256), 0, st, P);
     // (an unused 40 KiB LDS request: one chain workgroup per SIMD)
-    hipLaunchKernelGGL(encode_huge_chain_kernel, dim3(1024), dim3(64), 40 * 1024, st, P);
+    hipLaunchKernelGGL(encode_huge_chain_kernel, dim3(LSM_CHAIN_LDS ? 1024 : 2048), dim3(64), LSM_CHAIN_LDS, st, P);
     hipLaunchKernelGGL(encode_huge_finish_kernel, dim3(256), dim3(256), 0, st, P);
   }
   hipLaunchKernelGGL(encode_large_kernel, dim3(512), dim3(kE3Threads), 0, st, P);

@@ -309,14 +309,16 @@ extern "C" int lsm_scan_table(const uint8_t* d_file, uint64_t file_len, const ls
 
 // The Scanner walk without host synchronisation (see lsm_scan_table_async in lsmgpu.h).
 extern "C" int lsm_scan_table_async(const uint8_t* d_file, uint64_t file_len, const lsm_table_scan* table,
-                                    uint64_t* d_block_off, uint32_t cap_blocks, uint32_t data_blocks_hint,
-                                    const lsm_parsed_items* d_out, uint64_t item_cap, uint32_t* d_item_start,
+                                    uint64_t* d_block_off, uint32_t cap_blocks, uint32_t index_blocks_hint,
+                                    uint32_t data_blocks_hint, const lsm_parsed_items* d_out, uint64_t item_cap, uint32_t* d_item_start,
                                     int32_t* d_status, uint32_t* d_n_blocks, int32_t* d_table_status,
                                     void* d_workspace, size_t workspace_bytes, void* stream) {
   if (!d_file || !table || !d_block_off || !d_out || !d_item_start || !d_status || !d_n_blocks || !d_table_status ||
       !d_workspace || ((uintptr_t)d_file & 15) || cap_blocks == 0 || cap_blocks >= 0xFFFFFFF0u ||
-      table->two_level > 1 || workspace_bytes < lsm_scan_workspace_size(cap_blocks) || data_blocks_hint > cap_blocks)
+      table->two_level > 1 || workspace_bytes < lsm_scan_workspace_size(cap_blocks) || data_blocks_hint > cap_blocks ||
+      index_blocks_hint > cap_blocks)
     return LSM_BAD_ARG;
+  const uint32_t icap = index_blocks_hint ? index_blocks_hint : cap_blocks;  // the partition level's bound
   const hipStream_t st = (hipStream_t)stream;
   ScanWs w;
   scan_ws_size(cap_blocks, &w, (uint8_t*)d_workspace);
@@ -331,18 +333,18 @@ extern "C" int lsm_scan_table_async(const uint8_t* d_file, uint64_t file_len, co
   const uint32_t levels = 1 + table->two_level;
   const uint32_t hgrid = min((cap_blocks + 256) / 256, 4096u);
   for (uint32_t lvl = 0; lvl < levels; ++lvl) {
-    const uint32_t n_host = lvl == 0 ? 1 : cap_blocks + 1;  // (bound on the level's blocks)
+    const uint32_t n_host = lvl == 0 ? 1 : icap;  // (bound on the level's blocks)
     DecodeParams P = index_params(d_file, w.lvl_off, n_host, w, cap_blocks + 1);
     if ((e = launch_decode(P, w.dec_ws, w.dec_bytes, st)) != hipSuccess) return fail(e);
     const bool data_level = lvl + 1 == levels;
-    // (the data level's entries must fit the data decode's ranges: the hint, else the cap)
-    const uint32_t lvl_cap = data_level && data_blocks_hint ? data_blocks_hint : cap_blocks;
+    // (a level's entries must fit the next decode's ranges: the hints, else the cap)
+    const uint32_t lvl_cap = data_level ? (data_blocks_hint ? data_blocks_hint : cap_blocks) : icap;
     hipLaunchKernelGGL(scan_level_check_kernel, dim3(1), dim3(256), 0, st, w.state, w.lvl_status, w.lvl_start,
                        lvl_cap, table->block_count, data_level ? 1u : 0u);
     if ((e = hipMemsetAsync(w.flag, 0xFF, 16, st)) != hipSuccess) return fail(e);
     uint64_t* dst = data_level ? d_block_off : w.lvl_off;
-    // ranges [0, last]: the data decode reads cap + 1 offsets, the next index level cap + 2
-    const uint32_t last = data_level ? cap_blocks : cap_blocks + 1;
+    // ranges [0, last]: the data decode reads up to cap + 1 offsets, the partition level icap + 1
+    const uint32_t last = data_level ? cap_blocks : icap;
     hipLaunchKernelGGL(scan_handles_kernel, dim3(hgrid), dim3(256), 0, st, w.state, w.h_off, w.h_size, last,
                        file_len, data_level ? 0ULL : ~0ULL, dst, w.flag);
     hipLaunchKernelGGL(scan_handles_fail_kernel, dim3(1), dim3(256), 0, st, w.state, w.flag, last, dst);

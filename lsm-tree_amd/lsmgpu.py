@@ -63,6 +63,9 @@ class LsmTableScan(C.Structure):
 
 ABI_VERSION = 6
 DECODE_ITEM_START_VALID = 1
+# Mean block size (bytes) from which the wrappers hand the workspace pool for
+# blocks spread over the GPU (blocks > 72 KiB decode, > 96 KiB images encode).
+HUGE_AUTO_MEAN = 32 << 10
 DECODE_PAYLOAD_VERIFIED = 2
 
 
@@ -184,7 +187,7 @@ def lib():
         L.lsm_scan_workspace_size.argtypes = [C.c_uint32]
         L.lsm_scan_table_async.restype = C.c_int
         L.lsm_scan_table_async.argtypes = [C.c_void_p, C.c_uint64, C.POINTER(LsmTableScan), C.c_void_p, C.c_uint32,
-                                           C.c_uint32, C.POINTER(LsmParsed), C.c_uint64, C.c_void_p, C.c_void_p,
+                                           C.c_uint32, C.c_uint32, C.POINTER(LsmParsed), C.c_uint64, C.c_void_p, C.c_void_p,
                                            C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]
         L.lsm_scan_table.restype = C.c_int
         L.lsm_scan_table.argtypes = [C.c_void_p, C.c_uint64, C.POINTER(LsmTableScan), C.c_void_p, C.c_uint32,
@@ -304,12 +307,17 @@ class Decoder:
         return out
 
     def decode(self, blocks, block_off, n_blocks, out, item_cap, expect_type=-1, tuning=None, stream=None,
-               compact=False, pool=True, workspace_bytes=None):
+               compact=False, pool=None, workspace_bytes=None):
         """Enqueue lsm_decode_blocks (compact: lsm_decode_blocks16 into 16-bit
         offset arrays from alloc_outputs(..., compact=True)).  blocks: uint8 cuda
-        (padded); block_off: int64 cuda [n+1].  pool=False: the base workspace
-        only (blocks > 72 KiB on one workgroup each); workspace_bytes: pass
+        (padded); block_off: int64 cuda [n+1].  pool=True: the workspace carries
+        the pool that spreads blocks > 72 KiB over the GPU; False: the base
+        workspace only (those blocks on one workgroup each); None (default): the
+        pool when the batch's mean block is 32 KiB or more (its kernels cost a few
+        microseconds per call even with no such block); workspace_bytes: pass
         exactly that much workspace (tests of a pool too small for the batch)."""
+        if pool is None:
+            pool = blocks.numel() >= HUGE_AUTO_MEAN * max(n_blocks, 1)
         if tuning is None and os.environ.get("LSMGPU_DECODE_TUNING"):  # diagnostic override
             tuning = tuple(int(x, 0) for x in os.environ["LSMGPU_DECODE_TUNING"].split(","))
         ws = self.workspace(n_blocks, blocks.numel() if pool else 0)
@@ -345,7 +353,7 @@ class Decoder:
 
 
 def decode_blocks(blocks, block_off, n_blocks=None, expect_type=-1, item_cap=None, fields=None, tuning=None,
-                  compact=False, pool=True, workspace_bytes=None):
+                  compact=False, pool=None, workspace_bytes=None):
     """Convenience: decode device blocks, returns dict of device tensors
     (compact: the 19 B/item lsm_parsed_items16 layout)."""
     n_blocks = (block_off.numel() - 1) if n_blocks is None else n_blocks
@@ -363,10 +371,11 @@ class Encoder:
         self.ws = None
 
     def encode(self, items, starts, n_blocks, restart_interval=16, hash_ratio=0.0, block_type=BLOCK_DATA,
-               out=None, stream=None, pool=True):
+               out=None, stream=None, pool=None):
         """items: dict of cuda tensors keys(u8, padded) key_off(i64 n+1) vals(u8, padded) val_off(i64 n+1)
         seqno(i64) vtype(u8) [handle_off(i64) handle_size(i32)]; starts: int32 cuda [n_blocks+1].
-        pool=False: the base workspace only (blocks > 96 KiB on one workgroup each)."""
+        pool=False: the base workspace only (blocks > 96 KiB on one workgroup each);
+        None (default): the pool when the output bound averages 32 KiB per block or more."""
         torch = _torch()
         n_items = items["seqno"].numel()
         it = LsmItems()
@@ -383,6 +392,8 @@ class Encoder:
         key_bytes = int(items["keys"].numel())
         val_bytes = int(items["vals"].numel()) if "vals" in items else 0
         bound = lib().lsm_encode_bound(n_items, n_blocks, key_bytes, val_bytes, C.byref(params))
+        if pool is None:
+            pool = bound >= HUGE_AUTO_MEAN * max(n_blocks, 1)
         need = (lib().lsm_encode_workspace_size_ex(n_items, n_blocks, bound) if pool
                 else lib().lsm_encode_workspace_size(n_items, n_blocks))
         if self.ws is None or self.ws.numel() < need:
@@ -723,13 +734,14 @@ def materialize_keys(blocks, block_off, n_blocks, out, n_items=None, stream=None
 
 
 def scan_table(file, file_len, tli_off, tli_size, two_level=False, global_seqno=0, block_count=0, cap_blocks=None,
-               item_cap=None, fields=None, stream=None, sync=True, data_blocks_hint=0):
+               item_cap=None, fields=None, stream=None, sync=True, data_blocks_hint=0, index_blocks_hint=0):
     """Scanner over a table file image (scanner.rs:24-92): file = padded uint8 cuda tensor.
     Returns dict: table_status (int), n_blocks (int), block_off (int64 cuda [n+1]),
     the parsed fields, item_start and status (as decode_blocks).
     sync=False: lsm_scan_table_async (no host synchronisation): table_status and
     n_blocks are device int32 / uint32 tensors of one element, block_off holds
-    cap_blocks + 1 entries (data_blocks_hint bounds the data decode, e.g. block_count)."""
+    cap_blocks + 1 entries (data_blocks_hint bounds the data decode, e.g. block_count;
+    index_blocks_hint the partitions of a two-level index, e.g. tli_size // 4)."""
     torch = _torch()
     dev = file.device
     if cap_blocks is None:
@@ -747,7 +759,7 @@ def scan_table(file, file_len, tli_off, tli_size, two_level=False, global_seqno=
         d_nb = torch.zeros(1, dtype=torch.int32, device=dev)
         d_ts = torch.zeros(1, dtype=torch.int32, device=dev)
         _check(lib().lsm_scan_table_async(_ptr(file), file_len, C.byref(t), _ptr(block_off), cap_blocks,
-                                          data_blocks_hint, C.byref(ps), item_cap, _ptr(out["item_start"]),
+                                          index_blocks_hint, data_blocks_hint, C.byref(ps), item_cap, _ptr(out["item_start"]),
                                           _ptr(out["status"]), _ptr(d_nb), _ptr(d_ts), _ptr(ws), ws.numel(),
                                           _stream(stream)), "lsm_scan_table_async")
         out["table_status"], out["n_blocks"], out["block_off"] = d_ts, d_nb, block_off

@@ -14,7 +14,7 @@ from helpers import FIELD_VIEW, counter_items, prefix_items, random_sorted_items
 pytestmark = pytest.mark.gpu
 
 
-def _scan(L, t, global_seqno=0, block_count=None, cap_blocks=None, file=None, sync=True, hint=0):
+def _scan(L, t, global_seqno=0, block_count=None, cap_blocks=None, file=None, sync=True, hint=0, ihint=0):
     """sync=False: lsm_scan_table_async, its device results read back here and
     shaped like the synchronising call's (block_off cut to n_blocks + 1)."""
     import torch
@@ -23,7 +23,7 @@ def _scan(L, t, global_seqno=0, block_count=None, cap_blocks=None, file=None, sy
     bc = t["block_count"] if block_count is None else block_count
     out = L.scan_table(d_file, len(data), t["tli_off"], t["tli_size"], two_level=t.get("two_level", False),
                        global_seqno=global_seqno, block_count=bc, cap_blocks=cap_blocks, sync=sync,
-                       data_blocks_hint=hint)
+                       data_blocks_hint=hint, index_blocks_hint=ihint)
     torch.cuda.synchronize()
     res = {k: (v.cpu().numpy() if hasattr(v, "cpu") else v) for k, v in out.items()}
     if not sync:
@@ -166,8 +166,9 @@ def test_scan_async_matches(gpu, oracle, two_level):
     same blocks, items and statuses as the Scanner, with a cap of about 4x the
     blocks and with the exact block count as the data hint."""
     t = _table(oracle, counter_items(52 * 600, seed=12, tomb_frac=0.05), two_level)
-    for cap, hint in ((4 * t["block_count"], 0), (4 * t["block_count"], t["block_count"])):
-        g = _scan(gpu, t, 9, cap_blocks=cap, sync=False, hint=hint)
+    for cap, hint, ihint in ((4 * t["block_count"], 0, 0), (4 * t["block_count"], t["block_count"],
+                                                             t["tli_size"] // 4 if two_level else 0)):
+        g = _scan(gpu, t, 9, cap_blocks=cap, sync=False, hint=hint, ihint=ihint)
         _check_against_scanner(oracle, g, t, 9)
     data = bytearray(t["file"])
     data[int(t["block_off"][23]) + 100] ^= 0x40
@@ -193,5 +194,6 @@ def test_scan_async_level_errors(gpu, oracle):
     bad = dict(t)
     bad["tli_off"], bad["tli_size"] = 0, int(t["block_off"][1])
     assert _scan(gpu, bad, cap_blocks=cap, sync=False)["table_status"] == 7
-    t2 = _table(oracle, counter_items(52 * 50, seed=6), True)
+    t2 = _table(oracle, counter_items(52 * 50, seed=6), True, partition_size=256)
     assert _scan(gpu, t2, cap_blocks=4 * t2["block_count"], sync=False)["table_status"] == 0
+    assert _scan(gpu, t2, cap_blocks=4 * t2["block_count"], ihint=1, sync=False)["table_status"] == 6
