@@ -828,11 +828,14 @@ __global__ __launch_bounds__(kBigWaves * kWave) void decode_deferred_staged_kern
 //          merges the tail, compares the checksum and writes the status
 // A block whose header fails, or that no longer fits the pool, goes to the
 // general path (defer2) as before: statuses and outputs are the same on both.
-constexpr uint32_t kHugeWin = 32 * 1024;               // span bytes per unit
+#ifndef LSM_HUGE_WIN_KIB
+#define LSM_HUGE_WIN_KIB 32
+#endif
+constexpr uint32_t kHugeWin = LSM_HUGE_WIN_KIB * 1024;  // span bytes per unit
 constexpr uint32_t kHugeOverlap = 8 * 1024 - 256;      // staged past the window (intervals that straddle it)
 constexpr uint32_t kHugeStage = kHugeWin + kHugeOverlap;
 constexpr uint32_t kHugeMaxIv = 512;                   // intervals per window for phase A / B (else thread walks)
-constexpr uint32_t kHugeTile = 1024;                   // items per window for phase A / B
+constexpr uint32_t kHugeTile = 32 * LSM_HUGE_WIN_KIB;  // items per window for phase A / B
 constexpr uint32_t kHugeBix = kHugeStage + kStagePad;  // LDS: the window's binary-index entries
 constexpr uint32_t kHugeMeta = kHugeBix + 4 * (kHugeMaxIv + 4);
 constexpr uint32_t kHugeOwner = kHugeMeta + 80;

@@ -2563,20 +2563,29 @@ __global__ __launch_bounds__(256) void encode_huge_contrib_kernel(EncodeParams P
     uint32_t pos[kPer];
     uint64_t gg[kPer];
     bool live[kPer];
+    // (a unit inside one block, the common case: one block lookup for all its KiB blocks)
+    // (blocks the plan turned away for the pool's capacity keep their numbers but own
+    // no contributions: the one-workgroup E3 hashes them)
+    const uint64_t kb = L.kpre[i], ke = L.kpre[i + 1];
+    const bool one = g1 <= ke;
+    const bool acc0 = L.rec[i].accepted != 0;
+    const uint64_t dabs0 = (uint64_t)(uintptr_t)P.out + L.rec[i].dst_off;
 #pragma unroll
     for (uint32_t j = 0; j < kPer; ++j) {
       const uint64_t g = g0 + wave + 4 * j;
-      live[j] = g < g1;
+      live[j] = g < g1 && acc0;
       gg[j] = g;
-      base[j] = P.out;
-      pos[j] = 0;
-      if (live[j]) {
+      base[j] = reinterpret_cast<const uint8_t*>(dabs0 & ~15ULL);
+      pos[j] = (uint32_t)(dabs0 & 15) + kHdrLen + (uint32_t)(g - kb) * 1024 + 16 * lane;
+      if (g < g1 && !one) {
         while (L.kpre[i + 1] <= g) ++i;
         const uint64_t dabs = (uint64_t)(uintptr_t)P.out + L.rec[i].dst_off;
+        live[j] = L.rec[i].accepted != 0;
         base[j] = reinterpret_cast<const uint8_t*>(dabs & ~15ULL);
         pos[j] = (uint32_t)(dabs & 15) + kHdrLen + (uint32_t)(g - L.kpre[i]) * 1024 + 16 * lane;
       }
     }
+    if (!one) i = last_le_u64(L.kpre, n3, g1 - 1);  // (the next unit starts at or after this block)
     Win16 w[kPer];
 #pragma unroll
     for (uint32_t j = 0; j < kPer; ++j) w[j] = live[j] ? read_win16(base[j], pos[j]) : Win16{0, 0};

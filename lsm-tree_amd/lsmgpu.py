@@ -371,11 +371,12 @@ class Encoder:
         self.ws = None
 
     def encode(self, items, starts, n_blocks, restart_interval=16, hash_ratio=0.0, block_type=BLOCK_DATA,
-               out=None, stream=None, pool=None):
+               out=None, stream=None, pool=None, workspace_bytes=None):
         """items: dict of cuda tensors keys(u8, padded) key_off(i64 n+1) vals(u8, padded) val_off(i64 n+1)
         seqno(i64) vtype(u8) [handle_off(i64) handle_size(i32)]; starts: int32 cuda [n_blocks+1].
         pool=False: the base workspace only (blocks > 96 KiB on one workgroup each);
-        None (default): the pool when the output bound averages 32 KiB per block or more."""
+        None (default): the pool when the output bound averages 32 KiB per block or more;
+        workspace_bytes: pass exactly that much workspace (tests of a pool too small)."""
         torch = _torch()
         n_items = items["seqno"].numel()
         it = LsmItems()
@@ -396,6 +397,8 @@ class Encoder:
             pool = bound >= HUGE_AUTO_MEAN * max(n_blocks, 1)
         need = (lib().lsm_encode_workspace_size_ex(n_items, n_blocks, bound) if pool
                 else lib().lsm_encode_workspace_size(n_items, n_blocks))
+        if workspace_bytes is not None:
+            need = workspace_bytes
         if self.ws is None or self.ws.numel() < need:
             self.ws = torch.empty(max(need, 256), dtype=torch.uint8, device=self.device)
         if out is None or out["buf"].numel() < bound:

@@ -1,10 +1,9 @@
 #!/bin/bash
-# One GPU call for several checks (GPU slots are scarce): the tests touched by the
-# current change, the whole suite and the bench.
+# One GPU call for several checks (GPU slots are scarce).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
+V=lsm-tree_amd/.variants
 bash scripts/gpu_steps.sh \
-  "new:200:python -u -m pytest tests/test_gpu_table_scan.py tests/test_gpu_lz4.py tests/test_gpu_materialize.py tests/test_gpu_large_blocks.py -x -q --timeout 120 --timeout-method thread" \
-  "tests:300:python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread" \
-  "ab:200:python -u scripts/ab_large.py --which 256KiB,1MiB,4MiB" \
-  "bench:400:python -u bench.py > gpurun_out/bench_line.json"
+  "new:200:python -u -m pytest tests/test_gpu_large_blocks.py tests/test_gpu_encode_args.py -x -q --timeout 120 --timeout-method thread" \
+  "ab:300:python -u scripts/ab_large.py --which 256KiB,1MiB,4MiB && LSMGPU_LIB=$V/libw16.so python -u scripts/ab_large.py --which 256KiB,1MiB,4MiB && LSMGPU_LIB=$V/libw24.so python -u scripts/ab_large.py --which 256KiB,1MiB,4MiB" \
+  "kt:200:bash scripts/prof_steps.sh large 'rocprofv3 --kernel-trace --stats -d gpurun_out/kt_large -o run --output-format csv -- python3 scripts/ab_large.py --which 1MiB,4MiB --steps 2'"

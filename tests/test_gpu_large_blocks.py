@@ -192,3 +192,27 @@ def test_huge_index_blocks_encode(gpu, pool):
     off = out["block_off"].cpu().numpy().view(np.uint64)
     assert (out["status"].cpu().numpy()[:3] == 0).all() and (off == ref_off).all()
     assert out["buf"].cpu().numpy()[:int(off[-1])].tobytes() == ref_buf.tobytes()
+
+
+def test_huge_encode_pool_sizes(gpu):
+    """Encode with a pool too small for every huge block of the batch: the blocks
+    past the pool's capacity are written by the one-workgroup E3; bytes unchanged."""
+    import torch
+    items = counter_items(80000, seed=19)
+    starts = np.array([0, 3300, 16400, 30000, 47000, 78200, 80000], np.uint32)
+    ref_buf, ref_off = pyoracle.encode_blocks(items, starts)
+    d_items = gpu.items_to_device(items)
+    d_starts = torch.from_numpy(starts.astype(np.int32)).cuda()
+    nb = len(starts) - 1
+    n = items.n
+    import ctypes
+    bound = gpu.lib().lsm_encode_bound(n, nb, int(d_items["keys"].numel()), int(d_items["vals"].numel()),
+                                       ctypes.byref(gpu.LsmBlockParams(16, gpu.BLOCK_DATA, 0, 0, 0.0)))
+    base = gpu.lib().lsm_encode_workspace_size(n, nb)
+    full = gpu.lib().lsm_encode_workspace_size_ex(n, nb, bound)
+    for extra in (0, 5000, 60000, 300_000, 1_500_000, full - base):
+        out = gpu.Encoder().encode(d_items, d_starts, nb, workspace_bytes=base + extra, pool=True)
+        torch.cuda.synchronize()
+        off = out["block_off"].cpu().numpy().view(np.uint64)
+        assert (out["status"].cpu().numpy()[:nb] == 0).all() and (off == ref_off).all(), extra
+        assert out["buf"].cpu().numpy()[:int(off[-1])].tobytes() == ref_buf.tobytes(), extra
