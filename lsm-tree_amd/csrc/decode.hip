@@ -823,9 +823,9 @@ __global__ __launch_bounds__(kBigWaves * kWave) void decode_deferred_staged_kern
 //          oracle check, the LEB cursor for rare shapes; from HBM when one
 //          runs past the staged bytes) and computes the XXH3 contributions
 //          of the KiB blocks that start in the window, from LDS too
-//   chain  (decode_huge_chain_kernel): eight single-wave chains per block
-//          (accumulator k on wave k, xxh3_chain_wave), the last one to finish
-//          merges the tail, compares the checksum and writes the status
+//   chain  (decode_huge_chain_kernel): one wave per block, the eight
+//          accumulator chains on lanes 0..7 (xxh3_chain8)
+//   finish (decode_huge_finish_kernel): tail merge, checksum compare, status
 // A block whose header fails, or that no longer fits the pool, goes to the
 // general path (defer2) as before: statuses and outputs are the same on both.
 #ifndef LSM_HUGE_WIN_KIB
@@ -842,10 +842,8 @@ constexpr uint32_t kHugeOwner = kHugeMeta + 80;
 constexpr uint32_t kHugeRec = kHugeOwner + kHugeMaxIv;
 constexpr uint32_t kHugeLds = 64 + kHugeRec + 8 * (kHugeTile + 1);
 constexpr uint32_t kHugeGrid = 2048;
-#ifndef LSM_CHAIN_LDS  // an unused LDS request that spreads the chain workgroups one per SIMD (0: none)
-#define LSM_CHAIN_LDS 0  // (40 KiB: 0.29-0.33 vs 0.29-0.31 ms for the large-block legs, r04 A/B)
-#endif
-constexpr uint32_t kHugeChainLds = LSM_CHAIN_LDS, kHugeChainGrid = kHugeChainLds ? 1024 : 2048;
+constexpr uint32_t kChainRing = 16;     // xxh3_chain8: KiB of contribution rows in flight per chain wave
+constexpr uint32_t kHugeChainGrid = 1024;  // chain workgroups (one block each, grid-stride)
 
 struct HugeRec {
   BlockMeta m;         // header view, trailer fields merged in: m.st = trailer status (header checks passed)
@@ -1382,24 +1380,25 @@ __global__ __launch_bounds__(256) void decode_huge_kernel(DecodeParams P) {
   }
 }
 
-// Chains of the huge blocks: single-wave workgroup pairs (block i, accumulator
-// k).  The merge runs in decode_huge_finish_kernel: the kernel boundary makes
-// the eight results visible (an agent-scope fence per chain would write back
-// the XCD's whole L2).
+// Chains of the huge blocks: a single-wave workgroup per block, its eight
+// accumulators on lanes 0..7 (xxh3_chain8).  The merge runs in
+// decode_huge_finish_kernel: the kernel boundary makes the eight results
+// visible (an agent-scope fence per chain would write back the XCD's whole L2).
 __global__ __launch_bounds__(64) void decode_huge_chain_kernel(DecodeParams P) {
+  __shared__ __attribute__((aligned(16))) uint8_t ring[kChainRing * 1024];
   const HugeHdr* hp = reinterpret_cast<const HugeHdr*>(P.huge_pool);
   const uint32_t n = hp->n3;
   if (!n || (P.flags & LSM_DECODE_PAYLOAD_VERIFIED)) return;
   const HugeLayout L = huge_layout(P, n);
-  for (uint64_t p = blockIdx.x; p < 8ULL * n; p += gridDim.x) {
-    const uint32_t i = (uint32_t)(p >> 3), k = (uint32_t)(p & 7);
+  const uint32_t k = threadIdx.x & 7;
+  for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
     HugeRec* r = L.rec + i;
-    if (!r->accepted) continue;
+    if (!r->accepted || !r->nbk) continue;
     uint64_t a0, a1;
     xxh3_acc_init((int)(k >> 1), a0, a1);
-    const uint64_t x = xxh3_chain_wave(L.contrib + 8 * gload(L.kpre, i), r->nbk, k, (k & 1) ? a1 : a0,
-                                       kLongSecret.acc[16 + k]);
-    if ((threadIdx.x & 63) == 0) r->acc[k] = x;
+    const uint64_t x = xxh3_chain8<kChainRing>(L.contrib + 8 * gload(L.kpre, i), r->nbk, (k & 1) ? a1 : a0,
+                                               kLongSecret.acc[16 + k], ring);
+    if (threadIdx.x < 8) r->acc[k] = x;
   }
 }
 
@@ -1766,7 +1765,7 @@ hipError_t launch_decode(const DecodeParams& P0, void* ws, size_t ws_bytes, hipS
     if ((e = hipLaunchKernel(hk, dim3(kHugeGrid), dim3(256), args, kHugeLds, st)) != hipSuccess) return e;
     // (an unused 40 KiB LDS request: at most four chain workgroups per CU, one per
     // SIMD, so no two serial chains share a SIMD's quarter-rate multiplies)
-    hipLaunchKernelGGL(decode_huge_chain_kernel, dim3(kHugeChainGrid), dim3(64), kHugeChainLds, st, P);
+    hipLaunchKernelGGL(decode_huge_chain_kernel, dim3(kHugeChainGrid), dim3(64), 0, st, P);
     hipLaunchKernelGGL(decode_huge_finish_kernel, dim3(256), dim3(256), 0, st, P);
   }
   return hipGetLastError();

@@ -17,6 +17,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "lds_dma.hpp"
+
 namespace lsmgpu {
 
 constexpr int kWave = 64;
@@ -643,6 +645,98 @@ __device__ __forceinline__ uint64_t xxh3_chain_wave(const uint64_t* __restrict__
            ((uint64_t)(uint32_t)__builtin_amdgcn_readlane((int)hi, (int)t) << 32));
   }
   step(0);  // the last block's scramble, nothing added after it
+  return y;
+}
+
+// The eight scramble chains of one block on one wave: lane k = lane & 7 runs
+// accumulator k (lanes 8.. repeat lanes 0..7), y = scramble(y) + c_i over the
+// block's n >= 1 contribution rows (64 B each, row i = c[8 i .. 8 i + 7]) from
+// acc, and returns scramble(y).  The instruction stream is that of one chain
+// (xxh3_chain_wave needs eight waves on eight SIMDs for the same work), with
+// no v_readlane: rows arrive by LDS-DMA into ring (kRing KiB of this wave's
+// LDS), 16 rows per wave instruction, kRing instructions in flight (counted
+// vmcnt, lds_dma.hpp), and each lane reads its accumulator's word with one
+// ds_read_b64 per step, a chunk ahead of its steps.
+template <uint32_t kRing = 16>
+__device__ __forceinline__ uint64_t xxh3_chain8(const uint64_t* __restrict__ c, uint64_t n_in, uint64_t acc, uint64_t s,
+                                                uint8_t* ring) {
+  static_assert(kRing >= 2 && kRing <= 32, "chunks in flight");
+  const uint32_t lane = threadIdx.x & 63, k = lane & 7;
+  const uint32_t s_lo = (uint32_t)s, s_hi = (uint32_t)(s >> 32);
+  // every compiler-visible load waited for here: the waits the compiler would
+  // put in the loop (it does not see the DMA) would drain the ring
+  asm volatile("" ::"v"(s_lo), "v"(s_hi), "v"(acc));
+  const uint64_t n = ((uint64_t)__builtin_amdgcn_readfirstlane((uint32_t)(n_in >> 32)) << 32) |
+                     (uint32_t)__builtin_amdgcn_readfirstlane((uint32_t)n_in);
+  const uint64_t nc = (n + 15) / 16;  // 1-KiB chunks of 16 rows
+  const uint8_t* src = reinterpret_cast<const uint8_t*>(c);
+  const uint32_t rbase = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)ring;
+  auto dma = [&](uint64_t q, uint32_t slot) {  // (past the last chunk: the last one again, so the count stays)
+    const uint64_t qq = q < nc ? q : nc - 1;
+    if (16 * qq + lane / 4 < n) dma16<false>(src + 1024 * qq + 16 * lane, rbase + 1024 * slot);
+  };
+  const __attribute__((address_space(3))) uint64_t* rw =
+      (const __attribute__((address_space(3))) uint64_t*)ring + k;  // row r of slot q: rw[128 q + 8 r]
+  uint64_t y;
+  const uint32_t p1 = __builtin_amdgcn_readfirstlane(P32_1);
+  auto step = [&](uint64_t cn) {  // y = scramble(y) + cn: two quarter-rate multiplies, five plain ops
+    const uint32_t hi = (uint32_t)(y >> 32);
+    const uint32_t lo = (uint32_t)y ^ (hi >> 15) ^ s_lo;
+    uint32_t hm;  // (asm: left to itself the compiler spends a third v_mad_u64_u32 on the 64-bit addend)
+    asm("v_mul_lo_u32 %0, %1, %2" : "=v"(hm) : "v"(hi ^ s_hi), "s"(p1));
+    const uint64_t add = ((uint64_t)(hm + (uint32_t)(cn >> 32)) << 32) | (uint32_t)cn;
+    uint64_t cc;  // (the carry-out nobody reads)
+    asm("v_mad_u64_u32 %0, %1, %2, %3, %4" : "=v"(y), "=s"(cc) : "v"(lo), "s"(p1), "v"(add));
+  };
+#pragma unroll
+  for (uint32_t q = 0; q < kRing; ++q) dma(q, q);
+  // rows of two chunks in registers, ping-pong (no copies): one chunk's steps
+  // run while the next one's rows come out of the ring
+  uint64_t A[16], B[16];
+  vm_wait<kRing - 1>();  // chunk 0
+#pragma unroll
+  for (int r = 0; r < 16; ++r) A[r] = rw[8 * r];
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  dma(kRing, 0);
+  y = acc + A[0];  // row 0 seeds y
+  // in flight at chunk q: chunks q + 1 .. q + kRing; read chunk q + 1 into nb,
+  // the steps of chunk q (cb) from row r0, then chunk q + 1's slot refilled
+  auto chunk = [&](uint64_t* cb, uint64_t* nb, uint64_t q, int r0) {
+    const uint32_t ns = (uint32_t)((q + 1) % kRing);
+    vm_wait<kRing - 1>();
+#pragma unroll
+    for (int r = 0; r < 16; ++r) nb[r] = rw[128 * ns + 8 * r];
+#pragma unroll
+    for (int r = 0; r < 16; ++r)
+      if (r >= r0) step(cb[r]);
+    asm volatile("s_waitcnt lgkmcnt(0)" : "+v"(y)::"memory");  // (y ties the wait to the steps)
+    dma(q + 1 + kRing, ns);
+  };
+  auto tail = [&](const uint64_t* cb, uint32_t r0, uint32_t rn) {
+#pragma unroll
+    for (uint32_t r = 0; r < 16; ++r)
+      if (r >= r0 && r < rn) step(cb[r]);
+  };
+  const uint64_t full = n / 16;  // whole chunks
+  const uint32_t rn = (uint32_t)(n - 16 * full);
+  if (full == 0) {
+    tail(A, 1, rn);
+  } else {
+    chunk(A, B, 0, 1);
+    uint64_t q = 1;
+    for (; q + 2 <= full; q += 2) {
+      chunk(B, A, q, 0);
+      chunk(A, B, q + 1, 0);
+    }
+    if (q < full) {
+      chunk(B, A, q, 0);
+      tail(A, 0, rn);
+    } else {
+      tail(B, 0, rn);
+    }
+  }
+  vm_wait<0>();  // (no DMA may land in the ring after this chain)
+  step(0);       // the last block's scramble, nothing added after it
   return y;
 }
 

@@ -127,10 +127,12 @@ struct EncodeParams {
   uint16_t* hbucket;    // [n_items] E1 -> E2 (hash-index batches, when hb_valid): the key's bucket
                         // in its block (kNoBucket for blocks of >= kNeedHash buckets, never group-class)
   uint32_t hb_valid;
+  uint32_t hb_sh;       // hbucket holds every non-head item's shared prefix length (E1p ran)
   uint32_t* hb_fix;     // [1] set by E1 when it left keys of more than 16 bytes (kNeedHash)
   unsigned long long* phase;  // diagnostic builds: per-phase cycle totals [16]
   uint32_t* pfirst;     // [n_blocks + 1] E1p: each block's first record prefix (low 32 bits); [n_blocks] the total
   uint32_t* e1p_flag;   // [1] E1p: the item_start array is not monotone
+  uint64_t* wpart;      // [2 per wave of items] E1p: record totals of the blocks crossing a wave's ends
   uint8_t* huge_pool;   // workspace past encode_workspace_size (null: E3 one workgroup per block)
   uint64_t huge_pool_bytes;
   uint32_t huge_cap;    // huge-list entries the pool's layout provides
@@ -1505,17 +1507,19 @@ __device__ __forceinline__ void group_barrier_lds() {
 #define LSM_NOVOTE 0
 #endif
 // ---------------------------------------- E1p: the plan of huge-block batches
-// Blocks of ~16 Ki items and more (the writer's 1-4 MiB data blocks,
-// writer/mod.rs:193-198) leave encode_plan_kernel one workgroup per block,
-// walking 512-item chunks one after another (60 workgroups for 60 blocks of
-// 4 MiB).  E1p computes the same outputs item-parallel:
+// Blocks of ~4 Ki items and more on average (the writer's 1-4 MiB data blocks,
+// writer/mod.rs:193-198) leave encode_plan_kernel one workgroup per one to four
+// blocks, walking 512-item chunks one after another (60 workgroups for 60 blocks
+// of 4 MiB: 0.21 ms for 240 x 1 MiB).  E1p computes the same outputs item-parallel:
 //   lengths  thread per item: fields, shared prefix with its restart head
 //            (encoder.rs:140-143), record length -> erec (for now), shared
 //            length -> hbucket (unused by these batches' E2), per-block exact
-//            record totals and bad flags (wave-aggregated atomics into sizes)
+//            record totals and bad flags (wave-segmented sums: a block's total,
+//            or the parts at a wave's two ends)
 //   scan     the device scan over every item's record length, in place (low
 //            32 bits: a block's offsets are differences of two prefixes)
-//   blocks   thread per block: the plan, as encode_plan_kernel's epilogue
+//   blocks   wave per block: its total from the wave parts, the plan as
+//            encode_plan_kernel's epilogue
 //   offsets  thread per item: erec = prefix - its block's first prefix (the
 //            packed word for blocks of <= kGItems items)
 // A non-monotone item_start array rejects every block (the one-workgroup
@@ -1531,6 +1535,11 @@ __device__ __forceinline__ uint32_t block_of_item(const EncodeParams& P, uint32_
 }
 
 constexpr uint64_t kE1pBad = 1ULL << 63;
+constexpr uint32_t kE1pMaxBpw = 4;  // E1p for batches of >= 4 Ki items per block on average
+// Sum of two (record bytes | bad flag) words.
+__device__ __forceinline__ uint64_t e1p_add(uint64_t a, uint64_t b) {
+  return ((a | b) & kE1pBad) | ((a + b) & ~kE1pBad);
+}
 
 __device__ __forceinline__ uint64_t shfl_down64(uint64_t v, int o) {
   return (uint64_t)(uint32_t)__shfl_down((int)(uint32_t)v, o) |
@@ -1538,7 +1547,7 @@ __device__ __forceinline__ uint64_t shfl_down64(uint64_t v, int o) {
 }
 
 // The block of item i from the workgroup's first item's block (one binary search
-// per workgroup, by thread 0): blocks of >= 16 Ki items on average leave at most
+// per workgroup, by thread 0): blocks of >= 4 Ki items on average leave at most
 // a step or two per thread.
 __device__ __forceinline__ uint32_t wg_block_of_item(const EncodeParams& P, uint32_t i, uint32_t* sh) {
   const uint32_t i_begin = clamped_start(P, 0), i_end = clamped_start(P, P.n_blocks);
@@ -1557,9 +1566,8 @@ __global__ __launch_bounds__(256) void encode_e1p_lengths_kernel(EncodeParams P)
   const uint32_t gid = blockIdx.x * 256 + threadIdx.x;
   if (gid < P.n_blocks && clamped_start(P, gid + 1) < clamped_start(P, gid)) atomicOr(P.e1p_flag, 1u);
   const uint32_t i = gid, i_begin = clamped_start(P, 0), i_end = clamped_start(P, P.n_blocks);
-  const bool in = i >= i_begin && i < i_end;
+  const bool in = i >= i_begin && i < i_end && (uint64_t)gid < P.it.n_items;
   const uint32_t bw = wg_block_of_item(P, in ? i : 0, &sb);  // (every thread: it holds a barrier)
-  if ((uint64_t)gid >= P.it.n_items) return;
   const uint32_t b = in ? bw : 0;
   const uint32_t s = clamped_start(P, b), e = clamped_start(P, b + 1);
   const bool live = in && s <= i && i < e;  // (not, for a non-monotone array: every block is rejected)
@@ -1585,21 +1593,26 @@ __global__ __launch_bounds__(256) void encode_e1p_lengths_kernel(EncodeParams P)
     }
     rec = item_record_len(P, m, head);
   }
-  P.erec[i] = (uint32_t)min(rec, (uint64_t)0xFFFFFFFFu);
-  // per-block exact totals: lanes of one block summed first (blocks are runs of lanes)
+  if ((uint64_t)gid < P.it.n_items) P.erec[i] = (uint32_t)min(rec, (uint64_t)0xFFFFFFFFu);
+  // per-block exact totals without same-address atomics (a 4-MiB block's ~800
+  // waves would serialise on one word): lanes of one block summed first (blocks
+  // are runs of lanes); a block inside this wave stores its total, one that began
+  // in an earlier wave its part as this wave's head, one that goes on past this
+  // wave its part as this wave's tail (encode_e1p_blocks_kernel adds them up)
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t bb = live ? b : 0xFFFFFFFFu;
   uint64_t sum = rec | (bad ? kE1pBad : 0);
-  // segmented wave reduction: lanes with the same block, head lane = first of its run
-  for (int o = 1; o < 64; o <<= 1) {
+  for (int o = 1; o < 64; o <<= 1) {  // segmented wave reduction: run heads end with their run's total
     const uint64_t v = shfl_down64(sum, o);
     const uint32_t bo = (uint32_t)__shfl_down((int)bb, o);
-    if ((int)lane + o < 64 && bo == bb) sum = (sum & kE1pBad) | (v & kE1pBad) | ((sum & ~kE1pBad) + (v & ~kE1pBad));
+    if ((int)lane + o < 64 && bo == bb) sum = e1p_add(sum, v);
   }
   const uint32_t bprev = (uint32_t)__shfl_up((int)bb, 1);
   if (live && (lane == 0 || bprev != bb)) {
-    if (sum & ~kE1pBad) atomicAdd((unsigned long long*)&P.sizes[b], (unsigned long long)(sum & ~kE1pBad));
-    if (sum & kE1pBad) atomicOr((unsigned long long*)&P.sizes[b], (unsigned long long)kE1pBad);
+    const uint32_t w0 = gid - lane;
+    if (s >= w0 && e - w0 <= 64) P.sizes[b] = sum;
+    else if (s < w0) P.wpart[2 * (uint64_t)(w0 / 64)] = sum;
+    else P.wpart[2 * (uint64_t)(w0 / 64) + 1] = sum;
   }
 }
 
@@ -1618,12 +1631,28 @@ __device__ __forceinline__ uint32_t e1p_prefix(const EncodeParams& P, uint32_t i
   return (uint64_t)i < P.it.n_items ? P.erec[i] : P.pfirst[P.n_blocks];
 }
 
+// Wave per block: its record total from the lengths kernel's per-wave parts,
+// then the plan (encode_plan_kernel's epilogue) on lane 0.
 __global__ __launch_bounds__(256) void encode_e1p_blocks_kernel(EncodeParams P) {
-  const uint32_t b = blockIdx.x * 256 + threadIdx.x;
-  if (b >= P.n_blocks) return;
+  const uint32_t lane = threadIdx.x & 63;
+  const uint64_t bq = ((uint64_t)blockIdx.x * 256 + threadIdx.x) / 64;
+  if (bq >= P.n_blocks) return;  // (wave-uniform)
+  const uint32_t b = (uint32_t)bq;
   const uint32_t ri = P.ri;
   const uint32_t s = clamped_start(P, b), e = clamped_start(P, b + 1);
-  const uint64_t acc = P.sizes[b];
+  uint64_t acc = 0;
+  if (e > s && !P.e1p_flag[0]) {
+    const uint32_t ws = s / 64, we = (e - 1) / 64;
+    if (ws == we) {
+      acc = P.sizes[b];
+    } else {
+      uint64_t x = lane == 0 ? P.wpart[2 * (uint64_t)ws + 1] : 0;
+      for (uint64_t w = (uint64_t)ws + 1 + lane; w <= we; w += 64) x = e1p_add(x, P.wpart[2 * w]);
+      for (int o = 32; o; o >>= 1) x = e1p_add(x, shfl_xor64(x, o));
+      acc = x;
+    }
+  }
+  if (lane) return;
   bool bad = P.e1p_flag[0] || e <= s || (acc & kE1pBad) || start_past_items(P, b + 1);
   const uint32_t n = bad ? 0 : e - s;
   const uint64_t recs = bad ? 0 : acc & ~kE1pBad;
@@ -2298,16 +2327,14 @@ __global__ __launch_bounds__(kE3Threads) void encode_large_kernel(EncodeParams P
 //            offset; blocks of <= kGItems items: one unit with a workgroup
 //            scan), then one tail unit per block (hash-index votes, marker,
 //            trailer)
-//   hash     units of kEHugeKib KiB blocks: XXH3 contributions into the pool
-//   chain    eight single-wave chains per block; the last one merges the tail
-//            and writes the header and the status
+//            (the contributions of the KiB blocks wholly inside a unit's LDS
+//            image come from the image, flagged done)
+//   hash     XXH3 contributions of the other KiB blocks into the pool
+//   chain    one wave per block, the eight accumulator chains on lanes 0..7
+//   finish   wave per block: tail merge, header, status
 constexpr uint32_t kEHugeItems = 1024;  // items per record unit, at most (four per thread)
 constexpr uint32_t kEHugeImg = 2 * 4 * kE3HashChunk;  // LDS image of a record unit (the tail unit's vote arrays)
-constexpr uint32_t kEHugeKib = 32;      // KiB blocks per hash unit (eight per wave)
 constexpr uint32_t kEHugeGrid = 2048;
-#ifndef LSM_CHAIN_LDS  // an unused LDS request that spreads the chain workgroups one per SIMD (0: none)
-#define LSM_CHAIN_LDS 0
-#endif
 
 struct EncHuge {
   uint64_t dst_off;
@@ -2323,7 +2350,8 @@ struct EncHugeHdr {
   uint32_t n3;         // planned entries
   uint64_t total_units;
 };
-// Pool: [hdr | 256][list u32 x cap][kpre u64 x (cap + 1)][upre u64 x (cap + 1)][EncHuge x cap][contributions]
+// Pool: [hdr | 256][list u32 x cap][kpre u64 x (cap + 1)][upre u64 x (cap + 1)][EncHuge x cap]
+// [contributions, 64 B per KiB block][done flags, 1 B per KiB block]
 struct EncHugeLayout {
   EncHugeHdr* hdr;
   uint32_t* list;
@@ -2331,6 +2359,7 @@ struct EncHugeLayout {
   uint64_t* upre;
   EncHuge* rec;
   uint64_t* contrib;
+  uint8_t* kdone;  // KiB block's contribution computed by the records kernel (from its LDS image)
   uint64_t cap_kib;
 };
 __host__ __device__ __forceinline__ uint64_t enc_huge_fixed_bytes(uint64_t cap) {
@@ -2347,7 +2376,8 @@ __device__ __forceinline__ EncHugeLayout enc_huge_layout(const EncodeParams& P) 
   L.rec = reinterpret_cast<EncHuge*>(L.upre + (cap + 1));
   const uint64_t fixed = enc_huge_fixed_bytes(cap);
   L.contrib = reinterpret_cast<uint64_t*>(b + fixed);
-  L.cap_kib = (P.huge_pool_bytes - fixed) / 64;
+  L.cap_kib = (P.huge_pool_bytes - fixed) / 65;
+  L.kdone = reinterpret_cast<uint8_t*>(L.contrib + 8 * L.cap_kib);
   return L;
 }
 
@@ -2383,9 +2413,11 @@ __global__ __launch_bounds__(1024) void encode_huge_plan_kernel(EncodeParams P) 
       h.total = (uint32_t)(dst_end - h.dst_off);
       acc = dst_end <= P.out_cap;  // (else the one-workgroup E3 reports the overflow)
       nbk = (h.total - kHdrLen - 1) / 1024;  // (payload > 96 KiB: the long path)
-      // items per record unit: about what fills the LDS image at the block's mean record size
+      // items per record unit: 7/8 of the LDS image at the block's mean record size (a unit over
+      // the image goes straight to HBM and leaves its hash to the contrib kernel: the margin keeps
+      // nearly every unit staged)
       const uint32_t recs = P.plans[h.b].recs;
-      h.ipu = (uint32_t)min<uint64_t>(kEHugeItems, max<uint64_t>(64, (uint64_t)(kEHugeImg - 96) * h.n / max(recs, 1u)));
+      h.ipu = (uint32_t)min<uint64_t>(kEHugeItems, max<uint64_t>(64, (uint64_t)(kEHugeImg * 7 / 8) * h.n / max(recs, 1u)));
       h.nru = h.n <= kGItems ? 1 : (h.n + h.ipu - 1) / h.ipu;
       nu = acc ? h.nru + 1 : 0;
       nbk = acc ? nbk : 0;
@@ -2422,10 +2454,20 @@ __global__ __launch_bounds__(1024) void encode_huge_plan_kernel(EncodeParams P) 
     L.hdr->total_units = sh[33];
     L.hdr->n3 = n;
   }
+  // the records kernel's done flags start clear (the numbers of accepted blocks' KiB blocks are < cap_kib)
+  const uint64_t nf = min(sh[32], L.cap_kib);
+  for (uint64_t x = tid; 16 * x < nf; x += 1024) {
+    if (16 * x + 16 <= nf) reinterpret_cast<u32x4*>(L.kdone)[x] = u32x4{0, 0, 0, 0};
+    else
+      for (uint64_t y = 16 * x; y < nf; ++y) L.kdone[y] = 0;
+  }
 }
 
 // Record units (u < nru of a block) and the tail unit (u == nru).
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void encode_huge_records_kernel(EncodeParams P) {
+#ifndef LSM_REC_WPE
+#define LSM_REC_WPE 4
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LSM_REC_WPE))) void encode_huge_records_kernel(EncodeParams P) {
   __shared__ __attribute__((aligned(16))) uint32_t lbuf[2 * kE3HashChunk];  // record image | vote arrays
   uint32_t* hlo = lbuf;
   uint32_t* hhi = lbuf + kE3HashChunk;
@@ -2485,7 +2527,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
           for (uint32_t j = j0 + tid; j < j1; j += 256) {
             const bool head = j % ri == 0;
             bool bad = false;
-            const ItemMeta m = load_item_lcp(P, h.s, j, ri, bad);
+            // (after E1p the shared prefix is in hbucket: no key reads before the copy)
+            ItemMeta m = P.hb_sh ? load_item(P, (uint64_t)h.s + j, bad) : load_item_lcp(P, h.s, j, ri, bad);
+            if (P.hb_sh && !head) m.sh = P.hbucket[(uint64_t)h.s + j];
             const uint32_t roff = P.erec[h.s + j];
             RecordCopy rc;
             rc.issue(P, m, head, p0 + roff);
@@ -2497,6 +2541,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
         else put(img);
         if (staged) {
           __syncthreads();
+          if (h.nbk) {  // the KiB blocks wholly inside these records: contributions from the image
+            const uint32_t g0 = (rb + 1023) / 1024, g1 = min(h.nbk, re / 1024);
+            if (g1 > g0) {
+              const uint64_t kg = L.kpre[i] + g0;
+              xxh3_kib_contribs(limg, p0 + 1024 * g0, (g1 - g0) * 1024 + 1, &kLongSecret, L.contrib + 8 * kg, wave, 4);
+              for (uint32_t g = tid; g < g1 - g0; g += 256) L.kdone[kg + g] = 1;
+            }
+          }
           const uint32_t lo = (p0 + rb) - a0, c0 = (lo + 15) >> 4, c1 = lend >> 4;
           const u32x4* src = reinterpret_cast<const u32x4*>(lbuf);
           u32x4* dst = reinterpret_cast<u32x4*>(img + a0);
@@ -2542,83 +2594,101 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
   }
 }
 
-// Hash units: contributions of kEHugeKib KiB blocks of the written payloads.
+// The contributions the records kernel left (KiB blocks across two record
+// units or into the index / trailer, units over the LDS image, one-pass
+// blocks): a workgroup per range of kECRange KiB blocks reads their done
+// flags, lists the others in LDS and hashes them from the written payloads,
+// four per wave at a time (block lookup in an LDS copy of kpre).
+constexpr uint32_t kECRange = 256;
+constexpr uint32_t kECKpre = 2048;  // kpre entries staged in LDS (more blocks: the lookup reads HBM)
 __global__ __launch_bounds__(256) void encode_huge_contrib_kernel(EncodeParams P) {
+  __shared__ uint64_t kp[kECKpre + 1];
+  __shared__ uint32_t todo[kECRange];
+  __shared__ uint32_t ntodo;
   const EncHugeLayout L = enc_huge_layout(P);
   const uint32_t n3 = L.hdr->n3;
   if (!n3) return;
-  const uint64_t tk = L.hdr->total_kib;
-  const uint64_t units = (tk + kEHugeKib - 1) / kEHugeKib;
+  const uint64_t tk = min(L.hdr->total_kib, L.cap_kib);  // (accepted blocks' KiB numbers are below cap_kib)
+  if ((uint64_t)blockIdx.x * kECRange >= tk) return;
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
   const int q = lane & 3, sq = lane >> 2;
   const uint64_t k0 = kLongSecret.acc[sq + 2 * q], k1 = kLongSecret.acc[sq + 2 * q + 1];
-  constexpr uint32_t kPer = kEHugeKib / 4;
-  const uint64_t per = (units + gridDim.x - 1) / gridDim.x;
-  const uint64_t u_begin = (uint64_t)blockIdx.x * per, u_end = min(units, u_begin + per);
-  uint32_t i = u_begin < u_end ? last_le_u64(L.kpre, n3, u_begin * kEHugeKib) : 0;
-  for (uint64_t u = u_begin; u < u_end; ++u) {
-    const uint64_t g0 = u * kEHugeKib, g1 = min(tk, g0 + kEHugeKib);
-    while (i + 1 < n3 && L.kpre[i + 1] <= g0) ++i;
-    const uint8_t* base[kPer];
-    uint32_t pos[kPer];
-    uint64_t gg[kPer];
-    bool live[kPer];
-    // (a unit inside one block, the common case: one block lookup for all its KiB blocks)
-    // (blocks the plan turned away for the pool's capacity keep their numbers but own
-    // no contributions: the one-workgroup E3 hashes them)
-    const uint64_t kb = L.kpre[i], ke = L.kpre[i + 1];
-    const bool one = g1 <= ke;
-    const bool acc0 = L.rec[i].accepted != 0;
-    const uint64_t dabs0 = (uint64_t)(uintptr_t)P.out + L.rec[i].dst_off;
+  const bool lds_kp = n3 <= kECKpre;
+  if (lds_kp)
+    for (uint32_t x = tid; x <= n3; x += 256) kp[x] = L.kpre[x];
+  auto kpre = [&](uint32_t x) { return lds_kp ? kp[x] : L.kpre[x]; };
+  for (uint64_t G0 = (uint64_t)blockIdx.x * kECRange; G0 < tk; G0 += (uint64_t)gridDim.x * kECRange) {
+    if (tid == 0) ntodo = 0;
+    __syncthreads();
+    for (uint32_t x = tid; x < kECRange; x += 256) {
+      const uint64_t g = G0 + x;
+      if (g < tk && !L.kdone[g]) todo[atomicAdd(&ntodo, 1u)] = x;
+    }
+    __syncthreads();
+    const uint32_t nt = ntodo;
+    for (uint32_t t0 = 4 * wave; t0 < nt; t0 += 16) {
+      uint64_t g[4];
+      uint32_t bi[4];
 #pragma unroll
-    for (uint32_t j = 0; j < kPer; ++j) {
-      const uint64_t g = g0 + wave + 4 * j;
-      live[j] = g < g1 && acc0;
-      gg[j] = g;
-      base[j] = reinterpret_cast<const uint8_t*>(dabs0 & ~15ULL);
-      pos[j] = (uint32_t)(dabs0 & 15) + kHdrLen + (uint32_t)(g - kb) * 1024 + 16 * lane;
-      if (g < g1 && !one) {
-        while (L.kpre[i + 1] <= g) ++i;
-        const uint64_t dabs = (uint64_t)(uintptr_t)P.out + L.rec[i].dst_off;
-        live[j] = L.rec[i].accepted != 0;
+      for (int j = 0; j < 4; ++j) {
+        g[j] = t0 + j < nt ? G0 + todo[t0 + j] : G0 + todo[t0];
+        uint32_t lo = 0, hi = n3;  // the last block i with kpre[i] <= g
+        while (hi - lo > 1) {
+          const uint32_t mid = (lo + hi) >> 1;
+          if (kpre(mid) <= g[j]) lo = mid;
+          else hi = mid;
+        }
+        bi[j] = lo;
+      }
+      bool live[4];
+      const uint8_t* base[4];
+      uint32_t pos[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const EncHuge* r = L.rec + bi[j];
+        live[j] = t0 + j < nt && r->accepted != 0;
+        const uint64_t dabs = (uint64_t)(uintptr_t)P.out + r->dst_off;
         base[j] = reinterpret_cast<const uint8_t*>(dabs & ~15ULL);
-        pos[j] = (uint32_t)(dabs & 15) + kHdrLen + (uint32_t)(g - L.kpre[i]) * 1024 + 16 * lane;
+        pos[j] = (uint32_t)(dabs & 15) + kHdrLen + (uint32_t)(g[j] - kpre(bi[j])) * 1024 + 16 * lane;
+      }
+      Win16 w[4];
+#pragma unroll
+      for (int j = 0; j < 4; ++j) w[j] = live[j] ? read_win16(base[j], pos[j]) : Win16{0, 0};
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        uint64_t c0 = 0, c1 = 0;
+        stripe_part(w[j], k0, k1, c0, c1);
+        c0 = quad_group_sum64(c0);
+        c1 = quad_group_sum64(c1);
+        if (live[j] && lane < 4) {
+          L.contrib[8 * g[j] + 2 * q] = c0;
+          L.contrib[8 * g[j] + 2 * q + 1] = c1;
+        }
       }
     }
-    if (!one) i = last_le_u64(L.kpre, n3, g1 - 1);  // (the next unit starts at or after this block)
-    Win16 w[kPer];
-#pragma unroll
-    for (uint32_t j = 0; j < kPer; ++j) w[j] = live[j] ? read_win16(base[j], pos[j]) : Win16{0, 0};
-#pragma unroll
-    for (uint32_t j = 0; j < kPer; ++j) {
-      uint64_t c0 = 0, c1 = 0;
-      stripe_part(w[j], k0, k1, c0, c1);
-      c0 = quad_group_sum64(c0);
-      c1 = quad_group_sum64(c1);
-      if (live[j] && lane < 4) {
-        L.contrib[8 * gg[j] + 2 * q] = c0;
-        L.contrib[8 * gg[j] + 2 * q + 1] = c1;
-      }
-    }
+    __syncthreads();  // (todo / ntodo are rewritten for the next range)
   }
 }
 
-// (block i, accumulator k) per single-wave workgroup.  The merge and the
-// header run in encode_huge_finish_kernel: the kernel boundary makes the eight
-// results visible (an agent-scope fence per chain would write back the XCD's
-// whole L2).
+// A single-wave workgroup per block, its eight accumulators on lanes 0..7
+// (xxh3_chain8).  The merge and the header run in encode_huge_finish_kernel:
+// the kernel boundary makes the eight results visible (an agent-scope fence
+// per chain would write back the XCD's whole L2).
+constexpr uint32_t kEChainRing = 16;
 __global__ __launch_bounds__(64) void encode_huge_chain_kernel(EncodeParams P) {
+  __shared__ __attribute__((aligned(16))) uint8_t ring[kEChainRing * 1024];
   const EncHugeLayout L = enc_huge_layout(P);
   const uint32_t n3 = L.hdr->n3;
   if (!n3) return;
-  for (uint64_t p = blockIdx.x; p < 8ULL * n3; p += gridDim.x) {
-    const uint32_t i = (uint32_t)(p >> 3), k = (uint32_t)(p & 7);
+  const uint32_t k = threadIdx.x & 7;
+  for (uint32_t i = blockIdx.x; i < n3; i += gridDim.x) {
     EncHuge* r = L.rec + i;
     if (!r->accepted) continue;
     uint64_t a0, a1;
     xxh3_acc_init((int)(k >> 1), a0, a1);
-    const uint64_t x = xxh3_chain_wave(L.contrib + 8 * L.kpre[i], r->nbk, k, (k & 1) ? a1 : a0, kLongSecret.acc[16 + k]);
-    if ((threadIdx.x & 63) == 0) r->acc[k] = x;
+    const uint64_t x =
+        xxh3_chain8<kEChainRing>(L.contrib + 8 * L.kpre[i], r->nbk, (k & 1) ? a1 : a0, kLongSecret.acc[16 + k], ring);
+    if (threadIdx.x < 8) r->acc[k] = x;
   }
 }
 
@@ -2688,7 +2758,7 @@ static uint32_t plan_blocks_per_wg(uint64_t n_items, uint32_t n_blocks) {
 }
 
 // kspan, vspan | sizes | plans | lists | list count + E1p flag | scan tiles (blocks or items) |
-// erec | hbucket | hb_fix | pfirst
+// erec | hbucket | hb_fix | pfirst | wpart
 static uint64_t enc_tiles(uint64_t n_items, uint32_t n_blocks) {
   return std::max<uint64_t>(scan_tiles(n_blocks), scan_tiles(std::max<uint64_t>(n_items, 1)));
 }
@@ -2696,7 +2766,7 @@ size_t encode_workspace_size(uint64_t n_items, uint32_t n_blocks) {
   return 2 * al256(((size_t)n_blocks + 1) * 8) + al256((size_t)n_blocks * 8) +
          al256((size_t)n_blocks * sizeof(BlockPlan)) + al256((size_t)n_blocks * 4) + 256 +
          al256(enc_tiles(n_items, n_blocks) * 8) + al256((size_t)n_items * 4) + al256((size_t)n_items * 2) + 256 +
-         al256(((size_t)n_blocks + 1) * 4);
+         al256(((size_t)n_blocks + 1) * 4) + al256((n_items / 64 + 1) * 16);
 }
 
 // Huge-list entries for an output of out_cap bytes: a huge block's image
@@ -2708,7 +2778,7 @@ static uint64_t enc_huge_cap(uint32_t n_blocks, uint64_t out_cap) {
 
 size_t encode_workspace_size_ex(uint64_t n_items, uint32_t n_blocks, uint64_t out_cap) {
   return encode_workspace_size(n_items, n_blocks) + enc_huge_fixed_bytes(enc_huge_cap(n_blocks, out_cap)) +
-         64 * (out_cap / 1024 + 1) + 256;
+         65 * (out_cap / 1024 + 1) + 256;
 }
 
 uint64_t encode_bound(uint64_t n_items, uint32_t n_blocks, uint64_t key_bytes, uint64_t val_bytes,
@@ -2753,13 +2823,14 @@ hipError_t launch_encode(const lsm_items& items, const uint32_t* starts, uint32_
   P.erec = (uint32_t*)w; w += al256((size_t)items.n_items * 4);
   P.hbucket = (uint16_t*)w; w += al256((size_t)items.n_items * 2);
   P.hb_fix = (uint32_t*)w; w += 256;
-  P.pfirst = (uint32_t*)w;
+  P.pfirst = (uint32_t*)w; w += al256(((size_t)n_blocks + 1) * 4);
+  P.wpart = (uint64_t*)w;
   hipError_t e;
   {  // the whole-GPU E3 pool, when the workspace carries one
     const size_t base = al256(encode_workspace_size(items.n_items, n_blocks));
     const uint64_t cap = enc_huge_cap(n_blocks, out_cap);
     const uint64_t fixed = enc_huge_fixed_bytes(cap);
-    const bool pool = cap && ws_bytes >= base + fixed + 64 * 128;
+    const bool pool = cap && ws_bytes >= base + fixed + 65 * 128;
     P.huge_pool = pool ? (uint8_t*)ws + base : nullptr;
     P.huge_pool_bytes = pool ? ws_bytes - base : 0;
     P.huge_cap = pool ? (uint32_t)cap : 0;
@@ -2767,21 +2838,22 @@ hipError_t launch_encode(const lsm_items& items, const uint32_t* starts, uint32_
   }
   P.plan_bpw = plan_blocks_per_wg(items.n_items, n_blocks);
   P.hb_valid = 0;
+  P.hb_sh = 0;
   const dim3 pgrid((n_blocks + P.plan_bpw - 1) / P.plan_bpw);
 #ifndef LSM_NO_E1P
-  const bool e1p = P.type != 1 && P.plan_bpw == 1 && items.n_items > 0 && items.n_items < 0xFFFFFFFFull;
+  const bool e1p = P.type != 1 && P.plan_bpw <= kE1pMaxBpw && items.n_items > 0 && items.n_items < 0xFFFFFFFFull;
 #else
   const bool e1p = false;
 #endif
   if (e1p) {  // batches of huge blocks: the plan item-parallel
+    P.hb_sh = 1;
     if ((e = hipMemsetAsync(P.e1p_flag, 0, 4, st)) != hipSuccess) return e;
-    if ((e = hipMemsetAsync(P.sizes, 0, (size_t)n_blocks * 8, st)) != hipSuccess) return e;
     const dim3 igrid((uint32_t)((std::max<uint64_t>(items.n_items, n_blocks) + 255) / 256));
     hipLaunchKernelGGL(encode_e1p_lengths_kernel, igrid, dim3(256), 0, st, P);
     if ((e = launch_excl_scan(P.erec, items.n_items, tiles, E1pOut{P.erec, P.pfirst + n_blocks, items.n_items},
                               st)) != hipSuccess)
       return e;
-    hipLaunchKernelGGL(encode_e1p_blocks_kernel, dim3((n_blocks + 255) / 256), dim3(256), 0, st, P);
+    hipLaunchKernelGGL(encode_e1p_blocks_kernel, dim3((uint32_t)(((uint64_t)n_blocks + 3) / 4)), dim3(256), 0, st, P);
     hipLaunchKernelGGL(encode_e1p_offsets_kernel, igrid, dim3(256), 0, st, P);
   } else if (P.type == 1)
     hipLaunchKernelGGL(encode_plan_kernel<true>, pgrid, dim3(256), 0, st, P);
@@ -2834,7 +2906,7 @@ hipError_t launch_encode(const lsm_items& items, const uint32_t* starts, uint32_
     hipLaunchKernelGGL(encode_huge_records_kernel, dim3(kEHugeGrid), dim3(256), 0, st, P);
     hipLaunchKernelGGL(encode_huge_contrib_kernel, dim3(kEHugeGrid), dim3(256), 0, st, P);
     // (an unused 40 KiB LDS request: one chain workgroup per SIMD)
-    hipLaunchKernelGGL(encode_huge_chain_kernel, dim3(LSM_CHAIN_LDS ? 1024 : 2048), dim3(64), LSM_CHAIN_LDS, st, P);
+    hipLaunchKernelGGL(encode_huge_chain_kernel, dim3(1024), dim3(64), 0, st, P);
     hipLaunchKernelGGL(encode_huge_finish_kernel, dim3(256), dim3(256), 0, st, P);
   }
   hipLaunchKernelGGL(encode_large_kernel, dim3(512), dim3(kE3Threads), 0, st, P);
