@@ -815,10 +815,13 @@ __global__ __launch_bounds__(kBigWaves * kWave) void decode_deferred_staged_kern
 //          per huge block the header (incl. its checksum) and trailer views
 //          from HBM, its KiB-block and parse-unit counts, prefix sums of both
 //          over the list (contributions in the workspace pool: 64 B per KiB)
+//   units  (decode_huge_units_kernel, thread per restart interval): per unit
+//          the first interval that starts in it and that interval's offset
 //   work   (decode_huge_kernel, every CU): units = kHugeWin-byte windows of a
 //          block's span.  A unit stages its window (+ kHugeOverlap) in LDS by
-//          LDS-DMA, finds the restart intervals that start in it (a 256-way
-//          search of the binary index in HBM, two or three round trips),
+//          LDS-DMA, takes the restart intervals that start in it from the unit
+//          table (a block whose binary index is not monotone: a 256-way search
+//          of the index in HBM, two or three round trips),
 //          walks them from LDS (thread per interval, walk_interval_at: every
 //          oracle check, the LEB cursor for rare shapes; from HBM when one
 //          runs past the staged bytes) and computes the XXH3 contributions
@@ -844,13 +847,16 @@ constexpr uint32_t kHugeLds = 64 + kHugeRec + 8 * (kHugeTile + 1);
 constexpr uint32_t kHugeGrid = 2048;
 constexpr uint32_t kChainRing = 16;     // xxh3_chain8: KiB of contribution rows in flight per chain wave
 constexpr uint32_t kHugeChainGrid = 1024;  // chain workgroups (one block each, grid-stride)
+constexpr uint32_t kHugeUnitsGrid = 1024;  // unit-table workgroups (thread per restart interval, grid-stride)
 
 struct HugeRec {
   BlockMeta m;         // header view, trailer fields merged in: m.st = trailer status (header checks passed)
   uint64_t span0, item_base;
   uint64_t acc[8];     // chain results (accumulator k from chain wave k)
   uint32_t b, nbk, accepted, parse_bad;
-  uint32_t done, span, pad[2];  // span: the block's 16-B-aligned byte span
+  uint32_t done, span;  // span: the block's 16-B-aligned byte span
+  uint32_t nonmono;     // its binary index is not monotone (units kernel): the units search it
+  uint32_t pad;
 };
 static_assert(sizeof(HugeRec) % 16 == 0, "HugeRec layout");
 
@@ -858,20 +864,24 @@ struct HugeHdr {
   uint64_t total_kib;  // contributions over every accepted block
   uint32_t n3;         // listed huge blocks (HugeRec entries)
   uint32_t total_pu;   // work units (kHugeWin windows)
+  uint64_t total_iv;   // restart intervals + 1 per parsed block (units kernel threads)
 };
 
-// Pool: [HugeHdr | 256][kpre u64 x (n + 1)][upre u64 x (n + 1)][HugeRec x n][contributions, 64 B per KiB].
+// Pool: [HugeHdr | 256][kpre, ppre, ipre: u64 x (n + 1) each][HugeRec x n][contributions, 64 B per KiB
+// from the front] .. [unit table, 8 B per unit, from the back: entry u at uend[-1 - u]].
 struct HugeLayout {
   HugeHdr* hdr;
   uint64_t* kpre;
   uint64_t* ppre;
+  uint64_t* ipre;
   HugeRec* rec;
   uint64_t* contrib;
-  uint64_t cap_kib;
+  uint2* uend;    // unit u: {first restart interval starting in it, that interval's payload offset}
+  uint64_t rest;  // pool bytes after the fixed part
   bool ok;
 };
 __host__ __device__ __forceinline__ uint64_t huge_fixed_bytes(uint64_t n) {
-  return (256 + 16 * (n + 1) + sizeof(HugeRec) * n + 255) & ~255ULL;
+  return (256 + 24 * (n + 1) + sizeof(HugeRec) * n + 255) & ~255ULL;
 }
 __device__ __forceinline__ HugeLayout huge_layout(const DecodeParams& P, uint32_t n) {
   HugeLayout L;
@@ -879,11 +889,13 @@ __device__ __forceinline__ HugeLayout huge_layout(const DecodeParams& P, uint32_
   L.hdr = reinterpret_cast<HugeHdr*>(b);
   L.kpre = reinterpret_cast<uint64_t*>(b + 256);
   L.ppre = L.kpre + (n + 1);
-  L.rec = reinterpret_cast<HugeRec*>(L.ppre + (n + 1));
+  L.ipre = L.ppre + (n + 1);
+  L.rec = reinterpret_cast<HugeRec*>(L.ipre + (n + 1));
   const uint64_t fixed = huge_fixed_bytes(n);
   L.contrib = reinterpret_cast<uint64_t*>(b + fixed);
   L.ok = b != nullptr && fixed <= P.huge_pool_bytes;
-  L.cap_kib = L.ok ? (P.huge_pool_bytes - fixed) / 64 : 0;
+  L.rest = L.ok ? (P.huge_pool_bytes - fixed) & ~7ULL : 0;
+  L.uend = reinterpret_cast<uint2*>(b + fixed + L.rest);
   return L;
 }
 
@@ -893,7 +905,7 @@ __device__ __forceinline__ void defer3_block(const DecodeParams& P, uint32_t b) 
 }
 
 // Plan over the huge list, by one workgroup of nthr threads (nthr / 64 <= 16
-// waves); sh: 40 u64 of LDS.  Blocks it does not accept go to defer2.
+// waves); sh: 56 u64 of LDS.  Blocks it does not accept go to defer2.
 __device__ void huge_plan(const DecodeParams& P, uint64_t* sh, uint32_t nthr) {
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = nthr >> 6;
   const uint32_t n = gload(P.defer3_count, 0);
@@ -904,15 +916,16 @@ __device__ void huge_plan(const DecodeParams& P, uint64_t* sh, uint32_t nthr) {
       L.hdr->n3 = 0;
       L.hdr->total_pu = 0;
       L.hdr->total_kib = 0;
+      L.hdr->total_iv = 0;
     }
     return;
   }
   const bool hash = !(P.flags & LSM_DECODE_PAYLOAD_VERIFIED);
-  if (tid == 0) sh[32] = 0, sh[33] = 0;
+  if (tid == 0) sh[48] = 0, sh[49] = 0, sh[50] = 0;
   __syncthreads();
   for (uint32_t c = 0; c < n; c += nthr) {
     const uint32_t i = c + tid;
-    uint64_t nbk = 0, npu = 0;
+    uint64_t nbk = 0, npu = 0, niv = 0;
     bool acc = false;
     uint32_t b = 0;
     BlockMeta m{};
@@ -932,21 +945,25 @@ __device__ void huge_plan(const DecodeParams& P, uint64_t* sh, uint32_t nthr) {
         meta_trailer(gbase, P.expect_type, cap, m, P.compact);  // (after the payload checksum in oracle order)
         span = ((max(end, off) + 15) & ~15ULL) - span0;
         npu = (nbk || m.st == ST_OK) ? (span + kHugeWin - 1) / kHugeWin : 0;
+        niv = m.st == ST_OK ? trailer_of(m).bin_len + 1 : 0;  // (+1: the units kernel's end-of-block thread)
       }
     }
-    const uint64_t ik = wave_incl_scan_u64(nbk), ip = wave_incl_scan_u64(npu);
-    if (lane == 63) sh[wave] = ik, sh[16 + wave] = ip;
+    const uint64_t ik = wave_incl_scan_u64(nbk), ip = wave_incl_scan_u64(npu), ii = wave_incl_scan_u64(niv);
+    if (lane == 63) sh[wave] = ik, sh[16 + wave] = ip, sh[32 + wave] = ii;
     __syncthreads();
-    uint64_t bk = sh[32], bp = sh[33], tk = 0, tp = 0;
+    uint64_t bk = sh[48], bp = sh[49], bi = sh[50], tk = 0, tp = 0, ti = 0;
     for (uint32_t w = 0; w < nw; ++w) {
       bk += w < wave ? sh[w] : 0;
       bp += w < wave ? sh[16 + w] : 0;
+      bi += w < wave ? sh[32 + w] : 0;
       tk += sh[w];
       tp += sh[16 + w];
+      ti += sh[32 + w];
     }
-    const uint64_t kp = bk + ik - nbk, pp = bp + ip - npu;
+    const uint64_t kp = bk + ik - nbk, pp = bp + ip - npu, ivp = bi + ii - niv;
     if (i < n) {
-      acc = acc && kp + nbk <= L.cap_kib;  // (the pool holds the contributions of a prefix of the list)
+      // (the pool holds the contributions, front, and unit entries, back, of a prefix of the list)
+      acc = acc && 64 * (kp + nbk) + 8 * (pp + npu) <= L.rest;
       HugeRec* r = L.rec + i;
       r->m = m;
       r->span0 = span0;
@@ -957,25 +974,29 @@ __device__ void huge_plan(const DecodeParams& P, uint64_t* sh, uint32_t nthr) {
       r->parse_bad = 0;
       r->done = 0;
       r->span = (uint32_t)span;
+      r->nonmono = 0;
       gstore(L.kpre, i, kp);
       gstore(L.ppre, i, pp);
+      gstore(L.ipre, i, ivp);
       if (!acc) defer2_block(P, b);
     }
     __syncthreads();
-    if (tid == 0) sh[32] += tk, sh[33] += tp;
+    if (tid == 0) sh[48] += tk, sh[49] += tp, sh[50] += ti;
     __syncthreads();
   }
   if (tid == 0) {
-    gstore(L.kpre, n, sh[32]);
-    gstore(L.ppre, n, sh[33]);
-    L.hdr->total_kib = sh[32];
-    L.hdr->total_pu = (uint32_t)sh[33];
+    gstore(L.kpre, n, sh[48]);
+    gstore(L.ppre, n, sh[49]);
+    gstore(L.ipre, n, sh[50]);
+    L.hdr->total_kib = sh[48];
+    L.hdr->total_pu = (uint32_t)sh[49];
+    L.hdr->total_iv = sh[50];
     L.hdr->n3 = n;
   }
 }
 
 __global__ __launch_bounds__(1024) void decode_huge_plan_kernel(DecodeParams P) {
-  __shared__ uint64_t sh[40];
+  __shared__ uint64_t sh[56];
   huge_plan(P, sh, 1024);
 }
 
@@ -1210,6 +1231,45 @@ __device__ __forceinline__ uint32_t last_le(const uint64_t* a, uint32_t n, uint6
   return lo;
 }
 
+// The unit table of the parsed huge blocks: thread per restart interval x of
+// block i (plus one past its last), start s_x (span offset).  Unit u (window
+// [uW, uW + W)) gets the first interval that starts at or after uW, and that
+// interval's payload offset (the bound the window's last walk stops at): x
+// writes the units in (floor(s_{x-1} / W), floor(s_x / W)].  For a monotone
+// binary index every unit of the block is written once; a block whose index
+// is not monotone is flagged, and the work kernel searches its index instead.
+__global__ __launch_bounds__(256) void decode_huge_units_kernel(DecodeParams P) {
+  __shared__ uint32_t sb;
+  const HugeHdr* hp = reinterpret_cast<const HugeHdr*>(P.huge_pool);
+  const uint32_t n = hp->n3;
+  if (!n) return;
+  const HugeLayout L = huge_layout(P, n);
+  const uint64_t tiv = hp->total_iv;
+  for (uint64_t t0 = (uint64_t)blockIdx.x * 256; t0 < tiv; t0 += (uint64_t)gridDim.x * 256) {
+    if (threadIdx.x == 0) sb = last_le(L.ipre, n, t0);
+    __syncthreads();
+    const uint64_t tt = t0 + threadIdx.x;
+    uint32_t i = sb;
+    __syncthreads();  // (sb is rewritten in the next round)
+    if (tt >= tiv) continue;
+    while (i + 1 < n && gload(L.ipre, i + 1) <= tt) ++i;
+    HugeRec* r = L.rec + i;
+    if (!r->accepted) continue;
+    const BlockMeta m = r->m;
+    const TrailerInfo t = trailer_of(m);
+    const uint32_t x = (uint32_t)(tt - gload(L.ipre, i)), nint = t.bin_len;
+    const uint8_t* gbase = P.blocks + r->span0;
+    const uint64_t ub = gload(L.ppre, i);
+    const int64_t npu = (int64_t)(gload(L.ppre, i + 1) - ub);
+    const uint32_t sv = x < nint ? bin_get(gbase, m.p0, t, x) : t.rec_end;  // payload offset
+    const uint32_t sp = x > 0 ? bin_get(gbase, m.p0, t, x - 1) : 0;
+    if (x > 0 && x < nint && sv < sp) __hip_atomic_store(&r->nonmono, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    const int64_t ulo = x > 0 ? (int64_t)((m.p0 + (uint64_t)sp) / kHugeWin) + 1 : 0;
+    const int64_t uhi = x < nint ? min((int64_t)((m.p0 + (uint64_t)sv) / kHugeWin), npu - 1) : npu - 1;
+    for (int64_t u = ulo; u <= uhi; ++u) L.uend[-1 - (int64_t)(ub + u)] = make_uint2(x, sv);
+  }
+}
+
 // Huge-block work units (see huge_plan): unit u = window c of block i.  Data
 // windows whose intervals are all staged take phase A / B (decode_big_kernel's
 // record walk: lane = interval for the boundaries, thread = record for the
@@ -1235,7 +1295,16 @@ __global__ __launch_bounds__(256) void decode_huge_kernel(DecodeParams P) {
   const uint32_t u_begin = blockIdx.x * per, u_end = min(units, u_begin + per);
   uint32_t i = u_begin < u_end ? last_le(L.ppre, n, u_begin) : 0;
   uint32_t carry_u = 0xFFFFFFFFu, carry_r = 0;  // unit whose r1 search answer is carry_r (block i)
+#if defined(LSM_DIAG) && !defined(LSM_DIAG_NOTIME)
+  // diagnostic builds: per-phase s_memtime totals of wave 0 (g_dec_phase[8..13], units in [14])
+  uint64_t t_last = __builtin_amdgcn_s_memtime(), ph[8] = {};
+  uint32_t nunits = 0;
+#define HUGE_PHASE(k) DEC_PHASE(k)
+#else
+#define HUGE_PHASE(k)
+#endif
   for (uint32_t u = u_begin; u < u_end; ++u) {
+    HUGE_PHASE(6);
     while (i + 1 < n && gload(L.ppre, i + 1) <= u) ++i, carry_u = 0xFFFFFFFFu;
     const HugeRec* r = L.rec + i;
     if (!r->accepted) continue;  // (uniform)
@@ -1252,10 +1321,19 @@ __global__ __launch_bounds__(256) void decode_huge_kernel(DecodeParams P) {
         if (c * kWave + lane < chunks)
           __builtin_amdgcn_global_load_lds((gbl_void_t*)(src + 1024 * c), (lds_void_t*)(stage + 1024 * c), 16, 0, 0);
     }
-    // the intervals that start in [cs, ce): [r0, r1), by a 256-way search of the binary index (HBM)
+    // the intervals that start in [cs, ce): [r0, r1), from the unit table, or (a binary index
+    // that is not monotone) by a 256-way search of the binary index (HBM)
     const bool parse = m.st == ST_OK;
-    uint32_t r0 = 0, r1 = 0;
-    if (parse) {
+    const bool table = !r->nonmono;
+    uint32_t r0 = 0, r1 = 0, stop1 = 0;  // stop1: payload offset where the window's last interval ends
+    if (parse && table) {
+      const uint2 e0 = L.uend[-1 - (int64_t)u];
+      const bool last = ce == span;
+      const uint2 e1 = last ? make_uint2(t.bin_len, t.rec_end) : L.uend[-2 - (int64_t)u];
+      r0 = cs == 0 ? 0 : e0.x;
+      r1 = last ? t.bin_len : e1.x;
+      stop1 = e1.y;
+    } else if (parse) {
       const uint32_t nint = t.bin_len, p0 = m.p0;
       uint32_t lo0 = 0, hi0 = nint, lo1 = 0, hi1 = nint;  // r0 in [lo0, hi0], r1 in [lo1, hi1]
       if (carry_u + 1 == u) lo0 = hi0 = carry_r;
@@ -1292,13 +1370,16 @@ __global__ __launch_bounds__(256) void decode_huge_kernel(DecodeParams P) {
       carry_r = lo1;
     }
     const uint8_t* sbase = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(stage) - cs);  // span-relative
+    HUGE_PHASE(0);
     if (parse) {
       const uint64_t item_base = r->item_base;
       const uint32_t p0 = m.p0, ri = t.ri, niv = r1 - r0;
       const uint32_t items_w = niv ? min(r1 * ri, t.item_count) - r0 * ri : 0;
       // phase A / B when every interval of the window is staged (a wave-uniform vote)
       bool fast = m.type != 1 && niv <= kHugeMaxIv && items_w <= kHugeTile;
-      if (fast) {
+      if (fast && table) {  // (monotone: every interval of the window ends by stop1)
+        fast = r1 == r0 || (stop1 <= t.rec_end && (p0 + stop1 + kChunkReadAhead <= ss || ss == span));
+      } else if (fast) {
         bool mine = true;
         for (uint32_t x = r0 + tid; x < r1; x += 256) {
           const uint32_t s_cur = bin_get(gbase, p0, t, x);
@@ -1332,17 +1413,28 @@ __global__ __launch_bounds__(256) void decode_huge_kernel(DecodeParams P) {
           *wmeta = w;
         }
       }
+      HUGE_PHASE(1);
       vm_wait<0>();
       lds_barrier();
-      if (fast) phase_a<true>(stage, wmeta, owner, rec, wave * kWave, 4 * kWave, niv, kHugeTile);
-      if (hash && r->nbk) {  // the KiB blocks that start in [cs, ce)
+      HUGE_PHASE(2);
+      // phase A (serial LDS walks: latency) on wave 0, the contributions (VALU) on the
+      // other waves meanwhile; without phase A on all four
+#ifndef LSM_HUGE_SPLIT
+#define LSM_HUGE_SPLIT 1
+#endif
+      const bool split = LSM_HUGE_SPLIT && fast;
+      if (fast && (split ? wave == 0 : true))
+        phase_a<true>(stage, wmeta, owner, rec, split ? 0 : wave * kWave, split ? kWave : 4 * kWave, niv, kHugeTile);
+      HUGE_PHASE(3);
+      if (hash && r->nbk && (!split || wave != 0)) {  // the KiB blocks that start in [cs, ce)
         const uint32_t nbk = r->nbk;
         const uint32_t n0 = min(nbk, cs > p0 ? (cs - p0 + 1023) / 1024 : 0u);
         const uint32_t n1 = min(nbk, ce > p0 ? (ce - p0 + 1023) / 1024 : 0u);
         if (n1 > n0)
           xxh3_kib_contribs(sbase, p0 + 1024 * n0, (n1 - n0) * 1024 + 1, &kLongSecret,
-                            L.contrib + 8 * (gload(L.kpre, i) + n0), wave, 4);
+                            L.contrib + 8 * (gload(L.kpre, i) + n0), split ? wave - 1 : wave, split ? 3 : 4);
       }
+      HUGE_PHASE(4);
       bool walk = !fast;
       if (fast) {
         lds_barrier();
@@ -1376,8 +1468,19 @@ __global__ __launch_bounds__(256) void decode_huge_kernel(DecodeParams P) {
         xxh3_kib_contribs(sbase, p0 + 1024 * n0, (n1 - n0) * 1024 + 1, &kLongSecret,
                           L.contrib + 8 * (gload(L.kpre, i) + n0), wave, 4);
     }
+    HUGE_PHASE(5);
     lds_barrier();  // (the next unit rewrites the stage)
+#if defined(LSM_DIAG) && !defined(LSM_DIAG_NOTIME)
+    ++nunits;
+#endif
   }
+#if defined(LSM_DIAG) && !defined(LSM_DIAG_NOTIME)
+  if (threadIdx.x == 0) {
+    for (int k = 0; k < 7; ++k) atomicAdd(&g_dec_phase[8 + k], (unsigned long long)ph[k]);
+    atomicAdd(&g_dec_phase[15], (unsigned long long)nunits);
+  }
+#endif
+#undef HUGE_PHASE
 }
 
 // Chains of the huge blocks: a single-wave workgroup per block, its eight
@@ -1675,11 +1778,13 @@ size_t decode_workspace_size(uint32_t n_blocks) {
 }
 
 // + the huge-block pool for a batch of blocks_bytes bytes: every huge block
-// spans more than kBigStage bytes, contributions 64 B per KiB.
+// spans more than kBigStage bytes, contributions 64 B per KiB, unit entries
+// 8 B per kHugeWin window (and one more per block).
 size_t decode_workspace_size_ex(uint32_t n_blocks, uint64_t blocks_bytes) {
   const uint64_t most = blocks_bytes / kBigStage + 1;
   const uint64_t n3 = most < n_blocks ? most : n_blocks;
-  return decode_workspace_size(n_blocks) + huge_fixed_bytes(n3) + 64 * (blocks_bytes / 1024 + 1) + 256;
+  return decode_workspace_size(n_blocks) + huge_fixed_bytes(n3) + 64 * (blocks_bytes / 1024 + 1) +
+         8 * (blocks_bytes / kHugeWin + n3 + 1) + 256;
 }
 
 uint32_t decode_lds_bytes(uint32_t stage_bytes, uint32_t tile_items, uint32_t blocks_per_wave) {
@@ -1762,9 +1867,8 @@ hipError_t launch_decode(const DecodeParams& P0, void* ws, size_t ws_bytes, hipS
     const void* hk = all ? (const void*)decode_huge_kernel<true> : (const void*)decode_huge_kernel<false>;
     static uint64_t done_hk[2] = {};
     if ((e = set_lds_attr(hk, kHugeLds, &done_hk[all ? 1 : 0])) != hipSuccess) return e;
+    hipLaunchKernelGGL(decode_huge_units_kernel, dim3(kHugeUnitsGrid), dim3(256), 0, st, P);
     if ((e = hipLaunchKernel(hk, dim3(kHugeGrid), dim3(256), args, kHugeLds, st)) != hipSuccess) return e;
-    // (an unused 40 KiB LDS request: at most four chain workgroups per CU, one per
-    // SIMD, so no two serial chains share a SIMD's quarter-rate multiplies)
     hipLaunchKernelGGL(decode_huge_chain_kernel, dim3(kHugeChainGrid), dim3(64), 0, st, P);
     hipLaunchKernelGGL(decode_huge_finish_kernel, dim3(256), dim3(256), 0, st, P);
   }

@@ -511,13 +511,92 @@ __device__ __forceinline__ void xxh3_128_wave_long(const uint8_t* base, uint32_t
   out_hi = xxh3_avalanche(~((uint64_t)len * P64_2) + thi);
 }
 
+__device__ __forceinline__ uint64_t u64_of(uint32_t lo, uint32_t hi) { return (uint64_t)lo | ((uint64_t)hi << 32); }
+// Lanes with lane bit `bit` clear keep a's sum over the lane pair (lane, lane ^ 2^bit),
+// the others b's (bit 5: v_permlane32_swap, bit 4: v_permlane16_swap).
+template <int kBit>
+__device__ __forceinline__ uint64_t pair_swap_sum64(uint64_t a, uint64_t b) {
+  const uint32_t alo = (uint32_t)a, ahi = (uint32_t)(a >> 32), blo = (uint32_t)b, bhi = (uint32_t)(b >> 32);
+  if constexpr (kBit == 5) {
+    const auto l = __builtin_amdgcn_permlane32_swap(alo, blo, false, false);
+    const auto h = __builtin_amdgcn_permlane32_swap(ahi, bhi, false, false);
+    return u64_of(l[0], h[0]) + u64_of(l[1], h[1]);
+  } else {
+    const auto l = __builtin_amdgcn_permlane16_swap(alo, blo, false, false);
+    const auto h = __builtin_amdgcn_permlane16_swap(ahi, bhi, false, false);
+    return u64_of(l[0], h[0]) + u64_of(l[1], h[1]);
+  }
+}
+
+// XXH3 contributions of cnt <= kB (4 or 8) KiB blocks n0 .. n0 + cnt - 1 of
+// base[pos ..] by one wave (lane l: bytes [16 l, 16 l + 16) of each, stripe
+// l >> 2, accumulator pair l & 3) into contrib[8 n ..].  The 16-lane sums of
+// all of them as one reduce-scatter: lane bits 5 and 4 by permlane32 /
+// permlane16 swaps (each halves the values a lane holds), then DPP row
+// rotates (kB = 8: bit 3 a scatter, bit 2 a sum; kB = 4: both sums): about
+// 10 VALU per KiB block against 32 for a quad_group_sum64 pair.
+template <int kB>
+__device__ __forceinline__ void xxh3_kib_contribs_b(const uint8_t* base, uint32_t pos, uint32_t n0, uint32_t cnt,
+                                                    uint64_t k0, uint64_t k1, uint64_t* contrib) {
+  static_assert(kB == 4 || kB == 8, "batch");
+  const int lane = threadIdx.x & 63, q = lane & 3;
+  uint64_t c0[kB], c1[kB];
+#pragma unroll
+  for (int j = 0; j < kB; ++j) {
+    c0[j] = c1[j] = 0;
+    if ((uint32_t)j < cnt) {
+      const Win16 w = read_win16(base, pos + (n0 + j) * 1024 + 16 * lane);
+      stripe_part(w, k0, k1, c0[j], c1[j]);
+    }
+  }
+  constexpr int h5 = kB / 2, h4 = kB / 4;
+#pragma unroll
+  for (int j = 0; j < h5; ++j) {  // lanes with bit 5 set keep block j + h5
+    c0[j] = pair_swap_sum64<5>(c0[j], c0[j + h5]);
+    c1[j] = pair_swap_sum64<5>(c1[j], c1[j + h5]);
+  }
+#pragma unroll
+  for (int j = 0; j < h4; ++j) {  // bit 4 set: j + h4
+    c0[j] = pair_swap_sum64<4>(c0[j], c0[j + h4]);
+    c1[j] = pair_swap_sum64<4>(c1[j], c1[j + h4]);
+  }
+  uint64_t x0, x1;
+  uint32_t n;
+  if constexpr (kB == 8) {  // bit 3 set: block 1 of the remaining two
+    const bool b3 = (lane & 8) != 0;
+    auto lvl3 = [&](uint64_t a, uint64_t b) {
+      const uint64_t keep = b3 ? b : a, send = b3 ? a : b;
+      return keep + u64_of(dpp_ror8((uint32_t)send), dpp_ror8((uint32_t)(send >> 32)));
+    };
+    x0 = lvl3(c0[0], c0[1]);
+    x1 = lvl3(c1[0], c1[1]);
+    n = ((lane >> 5) & 1) * 4 + ((lane >> 4) & 1) * 2 + ((lane >> 3) & 1);
+  } else {
+    x0 = c0[0] + u64_of(dpp_ror8((uint32_t)c0[0]), dpp_ror8((uint32_t)(c0[0] >> 32)));
+    x1 = c1[0] + u64_of(dpp_ror8((uint32_t)c1[0]), dpp_ror8((uint32_t)(c1[0] >> 32)));
+    n = ((lane >> 5) & 1) * 2 + ((lane >> 4) & 1);
+  }
+  // (row_ror:4 hands lane i the value of lane i - 4 of its row: the partner for lanes with bit 2 set)
+  x0 += u64_of(dpp_ror4((uint32_t)x0), dpp_ror4((uint32_t)(x0 >> 32)));
+  x1 += u64_of(dpp_ror4((uint32_t)x1), dpp_ror4((uint32_t)(x1 >> 32)));
+  const bool st = kB == 8 ? (lane & 4) != 0 : (lane & 12) == 4;
+  if (st && n < cnt) {
+    contrib[8 * (uint64_t)(n0 + n) + 2 * q] = x0;
+    contrib[8 * (uint64_t)(n0 + n) + 2 * q + 1] = x1;
+  }
+}
+
+#ifndef LSM_KIB_BATCH
+#define LSM_KIB_BATCH 4  // KiB blocks per reduce-scatter (1: a quad_group_sum64 pair per block)
+#endif
 // XXH3-128 long path split across the waves of a workgroup.  The per-KiB
 // contributions of the accumulate loop do not depend on the accumulators, so
-// wave w of nw reduces KiB blocks w, w + nw, ... into contrib[8 n ..] (LDS);
-// after a workgroup barrier one wave runs the serial scramble chain over
-// them and the tail (xxh3_128_wave_finish).  len > 240.
-// With `ready`, KiB block n's contribution is published to a concurrent
-// xxh3_128_wave_finish by ready[n] = tag (LDS, workgroup release).
+// wave w of nw reduces runs of LSM_KIB_BATCH KiB blocks (starting at B w,
+// B (w + nw), ...) into contrib[8 n ..]; after a workgroup barrier one wave
+// runs the serial scramble chain over them and the tail
+// (xxh3_128_wave_finish).  len > 240.  With `ready`, KiB block n's
+// contribution is published to a concurrent xxh3_128_wave_finish by
+// ready[n] = tag (LDS, workgroup release).
 __device__ __forceinline__ void xxh3_kib_contribs(const uint8_t* base, uint32_t pos, uint32_t len,
                                                   const LongSecret* __restrict__ ls, uint64_t* contrib, uint32_t w,
                                                   uint32_t nw, uint32_t* ready = nullptr, uint32_t tag = 0) {
@@ -525,6 +604,17 @@ __device__ __forceinline__ void xxh3_kib_contribs(const uint8_t* base, uint32_t 
   const int q = lane & 3, s = lane >> 2;
   const uint64_t k0 = ls->acc[s + 2 * q], k1 = ls->acc[s + 2 * q + 1];
   const uint32_t nb_blocks = (len - 1) / 1024;
+#if LSM_KIB_BATCH > 1
+  constexpr uint32_t B = LSM_KIB_BATCH;
+  for (uint32_t n0 = B * w; n0 < nb_blocks; n0 += B * nw) {
+    const uint32_t cnt = min(B, nb_blocks - n0);
+    xxh3_kib_contribs_b<B>(base, pos, n0, cnt, k0, k1, contrib);
+    if (ready) {
+      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
+      if ((uint32_t)lane < cnt) __hip_atomic_store(&ready[n0 + lane], tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+    }
+  }
+#else
   // two KiB blocks per step (both windows read before either is reduced)
   for (uint32_t n = w; n < nb_blocks; n += 2 * nw) {
     const bool two = n + nw < nb_blocks;
@@ -553,6 +643,7 @@ __device__ __forceinline__ void xxh3_kib_contribs(const uint8_t* base, uint32_t 
       }
     }
   }
+#endif
 }
 
 // With `ready`, the chain consumes the contributions as xxh3_kib_contribs

@@ -89,6 +89,40 @@ def test_large_blocks_few_items(gpu, ratio, pool):
     compare_decode(g, parsed, item_start, status)
 
 
+@pytest.mark.parametrize("pool", [True, False])
+def test_huge_blocks_bad_binary_index(gpu, pool):
+    """Re-sealed 1 MiB blocks whose binary index lies: two entries swapped (not
+    monotone: the work kernel searches the index instead of the unit table),
+    an entry moved to the next restart head's record, the last entry past the
+    records, an entry 40 KiB late (past its next entries).  Statuses and fields
+    match the oracle's."""
+    items = counter_items(20000, seed=9)
+    starts = np.array([0, 16400, 20000], np.uint32)
+    buf, off = pyoracle.encode_blocks(items, starts)
+    blocks = [bytes(buf[int(off[i]):int(off[i + 1])]) for i in range(2)]
+    rec = bytes(blocks[0][33:])
+    step, nint = rec[-30], int.from_bytes(rec[-29:-25], "little")  # trailer.rs:118-163
+    bin_off = int.from_bytes(rec[-25:-21], "little")
+
+    def ent(r, k):
+        return int.from_bytes(r[bin_off + step * k:bin_off + step * (k + 1)], "little")
+
+    def put(r, k, v):
+        r[bin_off + step * k:bin_off + step * (k + 1)] = v.to_bytes(step, "little")
+
+    cases = []
+    r = bytearray(rec); a, b = ent(r, 300), ent(r, 301); put(r, 300, b); put(r, 301, a); cases.append(r)
+    r = bytearray(rec); put(r, 500, ent(r, 501)); cases.append(r)
+    r = bytearray(rec); put(r, nint - 1, bin_off + 8); cases.append(r)
+    r = bytearray(rec); put(r, 640, ent(r, 640) + 40 * 1024); cases.append(r)
+    tests = blocks + [pyoracle.block_write(bytes(c), 0) for c in cases]
+    buf2, off2 = pack(tests)
+    g = gpu_decode(gpu, buf2, off2, pool=pool)
+    parsed, item_start, status = pyoracle.decode_blocks(buf2, off2)
+    assert (status[:2] == 0).all() and (status[2:] != 0).all(), status
+    compare_decode(g, parsed, item_start, status)
+
+
 def _mixed_batch(seed=5):
     """48 blocks of 80-400 KiB between 4 KiB blocks, and corrupted copies of
     some: header checksum (HDR_CKSUM), payload bit (CKSUM), broken record
