@@ -835,7 +835,10 @@ __global__ __launch_bounds__(kBigWaves * kWave) void decode_deferred_staged_kern
 #define LSM_HUGE_WIN_KIB 32
 #endif
 constexpr uint32_t kHugeWin = LSM_HUGE_WIN_KIB * 1024;  // span bytes per unit
-constexpr uint32_t kHugeOverlap = 8 * 1024 - 256;      // staged past the window (intervals that straddle it)
+#ifndef LSM_HUGE_OVL
+#define LSM_HUGE_OVL (8 * 1024 - 256)
+#endif
+constexpr uint32_t kHugeOverlap = LSM_HUGE_OVL;  // staged past the window (intervals that straddle it)
 constexpr uint32_t kHugeStage = kHugeWin + kHugeOverlap;
 constexpr uint32_t kHugeMaxIv = 512;                   // intervals per window for phase A / B (else thread walks)
 constexpr uint32_t kHugeTile = 32 * LSM_HUGE_WIN_KIB;  // items per window for phase A / B
@@ -1431,7 +1434,7 @@ __global__ __launch_bounds__(256) void decode_huge_kernel(DecodeParams P) {
         const uint32_t n0 = min(nbk, cs > p0 ? (cs - p0 + 1023) / 1024 : 0u);
         const uint32_t n1 = min(nbk, ce > p0 ? (ce - p0 + 1023) / 1024 : 0u);
         if (n1 > n0)
-          xxh3_kib_contribs(sbase, p0 + 1024 * n0, (n1 - n0) * 1024 + 1, &kLongSecret,
+          xxh3_kib_contribs(stage, p0 + 1024 * n0 - cs, (n1 - n0) * 1024 + 1, &kLongSecret,
                             L.contrib + 8 * (gload(L.kpre, i) + n0), split ? wave - 1 : wave, split ? 3 : 4);
       }
       HUGE_PHASE(4);
@@ -1465,7 +1468,7 @@ __global__ __launch_bounds__(256) void decode_huge_kernel(DecodeParams P) {
       const uint32_t n0 = min(nbk, cs > p0 ? (cs - p0 + 1023) / 1024 : 0u);
       const uint32_t n1 = min(nbk, ce > p0 ? (ce - p0 + 1023) / 1024 : 0u);
       if (n1 > n0)
-        xxh3_kib_contribs(sbase, p0 + 1024 * n0, (n1 - n0) * 1024 + 1, &kLongSecret,
+        xxh3_kib_contribs(stage, p0 + 1024 * n0 - cs, (n1 - n0) * 1024 + 1, &kLongSecret,
                           L.contrib + 8 * (gload(L.kpre, i) + n0), wave, 4);
     }
     HUGE_PHASE(5);

@@ -35,6 +35,18 @@ template <class T>
 __device__ __forceinline__ T gload(const T* p, uint64_t i) {
   return ((const __attribute__((address_space(1))) T*)p)[i];
 }
+// A trivially copyable struct element by explicit global loads (gload cannot
+// copy a struct through an address-space-qualified lvalue).
+template <class T>
+__device__ __forceinline__ T gload_pod(const T* p, uint64_t i) {
+  static_assert(sizeof(T) % 8 == 0, "8-byte multiple");
+  T r;
+  const __attribute__((address_space(1))) uint64_t* src = (const __attribute__((address_space(1))) uint64_t*)(p + i);
+  uint64_t* dst = reinterpret_cast<uint64_t*>(&r);
+#pragma unroll
+  for (uint32_t k = 0; k < sizeof(T) / 8; ++k) dst[k] = src[k];
+  return r;
+}
 constexpr uint32_t kHdrLen = 33;
 constexpr uint32_t kTrailerLen = 31;
 constexpr uint8_t kTrailerMarker = 0xFF;
@@ -154,6 +166,16 @@ __device__ __forceinline__ Win16 read_win16(const uint8_t* base, uint32_t pos) {
   uint32_t e0 = alignbyte(d1, d0, s), e1 = alignbyte(d2, d1, s), e2 = alignbyte(d3, d2, s),
            e3 = alignbyte(d4, d3, s);
   return {(uint64_t)e0 | ((uint64_t)e1 << 32), (uint64_t)e2 | ((uint64_t)e3 << 32)};
+}
+// The same from an LDS pointer (explicit address space: ds_read even where
+// the compiler cannot tell that a generic pointer is LDS).
+__device__ __forceinline__ Win16 read_win16_lds(const uint8_t* base_generic, uint32_t pos) {
+  const __attribute__((address_space(3))) uint32_t* b =
+      (const __attribute__((address_space(3))) uint32_t*)(const __attribute__((address_space(3))) uint8_t*)base_generic;
+  const uint32_t a = pos >> 2, s = pos & 3u;
+  const uint32_t d0 = b[a], d1 = b[a + 1], d2 = b[a + 2], d3 = b[a + 3], d4 = b[a + 4];
+  return {(uint64_t)alignbyte(d1, d0, s) | ((uint64_t)alignbyte(d2, d1, s) << 32),
+          (uint64_t)alignbyte(d3, d2, s) | ((uint64_t)alignbyte(d4, d3, s) << 32)};
 }
 __device__ __forceinline__ uint32_t read_u32_unaligned(const uint8_t* base, uint32_t pos) {
   const uint32_t a = pos & ~3u, s = pos & 3u;
@@ -529,13 +551,13 @@ __device__ __forceinline__ uint64_t pair_swap_sum64(uint64_t a, uint64_t b) {
 }
 
 // XXH3 contributions of cnt <= kB (4 or 8) KiB blocks n0 .. n0 + cnt - 1 of
-// base[pos ..] by one wave (lane l: bytes [16 l, 16 l + 16) of each, stripe
+// base[pos ..] (kLds: an LDS image, else HBM) by one wave (lane l: bytes [16 l, 16 l + 16) of each, stripe
 // l >> 2, accumulator pair l & 3) into contrib[8 n ..].  The 16-lane sums of
 // all of them as one reduce-scatter: lane bits 5 and 4 by permlane32 /
 // permlane16 swaps (each halves the values a lane holds), then DPP row
 // rotates (kB = 8: bit 3 a scatter, bit 2 a sum; kB = 4: both sums): about
 // 10 VALU per KiB block against 32 for a quad_group_sum64 pair.
-template <int kB>
+template <int kB, bool kLds>
 __device__ __forceinline__ void xxh3_kib_contribs_b(const uint8_t* base, uint32_t pos, uint32_t n0, uint32_t cnt,
                                                     uint64_t k0, uint64_t k1, uint64_t* contrib) {
   static_assert(kB == 4 || kB == 8, "batch");
@@ -545,7 +567,8 @@ __device__ __forceinline__ void xxh3_kib_contribs_b(const uint8_t* base, uint32_
   for (int j = 0; j < kB; ++j) {
     c0[j] = c1[j] = 0;
     if ((uint32_t)j < cnt) {
-      const Win16 w = read_win16(base, pos + (n0 + j) * 1024 + 16 * lane);
+      const uint32_t at = pos + (n0 + j) * 1024 + 16 * lane;
+      const Win16 w = kLds ? read_win16_lds(base, at) : read_win16(base, at);
       stripe_part(w, k0, k1, c0[j], c1[j]);
     }
   }
@@ -594,9 +617,10 @@ __device__ __forceinline__ void xxh3_kib_contribs_b(const uint8_t* base, uint32_
 // wave w of nw reduces runs of LSM_KIB_BATCH KiB blocks (starting at B w,
 // B (w + nw), ...) into contrib[8 n ..]; after a workgroup barrier one wave
 // runs the serial scramble chain over them and the tail
-// (xxh3_128_wave_finish).  len > 240.  With `ready`, KiB block n's
+// (xxh3_128_wave_finish).  len > 240; kLds: base is LDS.  With `ready`, KiB block n's
 // contribution is published to a concurrent xxh3_128_wave_finish by
 // ready[n] = tag (LDS, workgroup release).
+template <bool kLds = true>
 __device__ __forceinline__ void xxh3_kib_contribs(const uint8_t* base, uint32_t pos, uint32_t len,
                                                   const LongSecret* __restrict__ ls, uint64_t* contrib, uint32_t w,
                                                   uint32_t nw, uint32_t* ready = nullptr, uint32_t tag = 0) {
@@ -608,7 +632,7 @@ __device__ __forceinline__ void xxh3_kib_contribs(const uint8_t* base, uint32_t 
   constexpr uint32_t B = LSM_KIB_BATCH;
   for (uint32_t n0 = B * w; n0 < nb_blocks; n0 += B * nw) {
     const uint32_t cnt = min(B, nb_blocks - n0);
-    xxh3_kib_contribs_b<B>(base, pos, n0, cnt, k0, k1, contrib);
+    xxh3_kib_contribs_b<B, kLds>(base, pos, n0, cnt, k0, k1, contrib);
     if (ready) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
       if ((uint32_t)lane < cnt) __hip_atomic_store(&ready[n0 + lane], tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);

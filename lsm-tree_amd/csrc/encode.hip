@@ -213,6 +213,18 @@ struct ByteWriter {
   }
 };
 
+// Destination pointers of the record writers: LDS images (lds8_t) or HBM
+// (gbl8_t), explicit so that the stores compile to ds_write / global_store
+// (a generic pointer gives flat stores, which also count on lgkmcnt: every
+// later LDS wait then waits for the loads in flight too).
+typedef __attribute__((address_space(3))) uint8_t lds8_t;
+typedef __attribute__((address_space(1))) uint8_t gbl8_t;
+__device__ __forceinline__ void st_u32(lds8_t* p, uint32_t v) { *(__attribute__((address_space(3))) uint32_t*)p = v; }
+__device__ __forceinline__ void st_u32(gbl8_t* p, uint32_t v) { *(__attribute__((address_space(1))) uint32_t*)p = v; }
+__device__ __forceinline__ void st_u32(uint8_t* p, uint32_t v) { *reinterpret_cast<uint32_t*>(p) = v; }
+__device__ __forceinline__ lds8_t* as_lds(uint8_t* p) { return (lds8_t*)p; }
+__device__ __forceinline__ gbl8_t* as_gbl(uint8_t* p) { return (gbl8_t*)p; }
+
 // Span copy src (HBM, any alignment) -> dst[d .. d + n) (any alignment), in
 // two steps so that all loads of a record are issued before its stores:
 // load() reads the aligned 16-B windows that hold bytes of the span (the
@@ -224,12 +236,12 @@ struct ByteWriter {
 // their dword with the neighbouring record.
 template <int K>
 struct SpanCopy {
-  const u32x4* W;
+  const __attribute__((address_space(1))) u32x4* W;
   uint32_t n, d, rel, nwin, h, tl, hb, tb;
   u32x4 w[K];
   __device__ __forceinline__ void load(const uint8_t* src, uint32_t n_, uint32_t d_) {
     const uint64_t a = (uint64_t)(uintptr_t)src;
-    W = reinterpret_cast<const u32x4*>(a & ~15ULL);
+    W = (const __attribute__((address_space(1))) u32x4*)(a & ~15ULL);
     n = n_;
     d = d_;
     rel = (uint32_t)(a & 15);
@@ -239,19 +251,22 @@ struct SpanCopy {
     h = min(n_, (4u - (d_ & 3u)) & 3u);
     tl = n_ > h ? (d_ + n_) & 3u : 0u;
     hb = tb = 0;
-    for (uint32_t k = 0; k < h; ++k) hb |= (uint32_t)src[k] << (8 * k);
-    for (uint32_t k = 0; k < tl; ++k) tb |= (uint32_t)src[n_ - tl + k] << (8 * k);
+    const gbl8_t* gs = (const gbl8_t*)src;
+    for (uint32_t k = 0; k < h; ++k) hb |= (uint32_t)gs[k] << (8 * k);
+    for (uint32_t k = 0; k < tl; ++k) tb |= (uint32_t)gs[n_ - tl + k] << (8 * k);
   }
-  __device__ __forceinline__ void emit(uint8_t* dst, int wi, const u32x4& cw, uint32_t next0, int t0, uint32_t sh,
+  template <class D>
+  __device__ __forceinline__ void emit(D* dst, int wi, const u32x4& cw, uint32_t next0, int t0, uint32_t sh,
                                        uint32_t da, int qa, int qb) const {
     const uint32_t c[5] = {cw.x, cw.y, cw.z, cw.w, next0};
 #pragma unroll
     for (int j = 0; j < 4; ++j) {
       const int q = 4 * wi + j - t0;
-      if (q >= qa && q <= qb) *reinterpret_cast<uint32_t*>(dst + da + 4 * q) = alignbyte(c[j + 1], c[j], sh);
+      if (q >= qa && q <= qb) st_u32(dst + da + 4 * q, alignbyte(c[j + 1], c[j], sh));
     }
   }
-  __device__ __forceinline__ void store(uint8_t* dst) const {
+  template <class D>
+  __device__ __forceinline__ void store(D* dst) const {
     for (uint32_t k = 0; k < h; ++k) dst[d + k] = (uint8_t)(hb >> (8 * k));
     for (uint32_t k = 0; k < tl; ++k) dst[d + n - tl + k] = (uint8_t)(tb >> (8 * k));
     const int qa = (d & 3) ? 1 : 0;
@@ -370,21 +385,21 @@ __device__ __forceinline__ ItemMeta cook_item(const RawItem& r, bool& bad) {
 
 __device__ __forceinline__ ItemMeta load_item(const EncodeParams& P, uint64_t i, bool& bad) {
   ItemMeta m;
-  m.ko = P.it.key_off[i];
-  const uint64_t kl = P.it.key_off[i + 1] - m.ko;
+  m.ko = gload(P.it.key_off, i);  // (gload: global loads, not flat ones)
+  const uint64_t kl = gload(P.it.key_off, i + 1) - m.ko;
   if (kl > 0xFFFF) bad = true;
   m.klen = (uint32_t)min(kl, (uint64_t)0xFFFF);
-  m.seq = P.it.seqno[i];
+  m.seq = gload(P.it.seqno, i);
   m.sh = 0;
   m.e = 0;
   if (is_index(P)) {
-    m.vo = P.it.handle_off[i];
-    m.vl = P.it.handle_size[i];
+    m.vo = gload(P.it.handle_off, i);
+    m.vl = gload(P.it.handle_size, i);
     m.vt = 0;
   } else {
-    m.vo = P.it.val_off[i];
-    const uint64_t vl = P.it.val_off[i + 1] - m.vo;
-    m.vt = P.it.vtype[i];
+    m.vo = gload(P.it.val_off, i);
+    const uint64_t vl = gload(P.it.val_off, i + 1) - m.vo;
+    m.vt = gload(P.it.vtype, i);
     if (!valid_vtype(m.vt)) bad = true;
     if (!is_tombstone(m.vt) && vl > 0xFFFFFFFFULL) bad = true;
     m.vl = (uint32_t)vl;
@@ -419,7 +434,8 @@ __device__ __forceinline__ uint64_t item_record_len(const EncodeParams& P, const
 }
 
 // Byte stores of a LEB128 (varint-rs write_*_varint) / single bytes.
-__device__ __forceinline__ uint32_t put_leb(uint8_t* dst, uint32_t pos, uint64_t v) {
+template <class D>
+__device__ __forceinline__ uint32_t put_leb(D* dst, uint32_t pos, uint64_t v) {
   while (v >= 0x80) {
     dst[pos++] = (uint8_t)(v | 0x80);
     v >>= 7;
@@ -444,7 +460,8 @@ struct RecordCopy {
     const uint32_t vpos = kpos + m.klen - kfrom + leb_len(m.vl);
     val.load(P.it.vals + (has_val ? m.vo : 0), has_val ? m.vl : 0, vpos);
   }
-  __device__ __forceinline__ void store(const EncodeParams& P, const ItemMeta& m, bool head, uint8_t* dst) const {
+  template <class D>
+  __device__ __forceinline__ void store(const EncodeParams& P, const ItemMeta& m, bool head, D* dst) const {
     uint32_t pos = dpos;
     if (is_index(P)) {
       dst[pos++] = 0;
@@ -468,7 +485,8 @@ struct RecordCopy {
   }
 };
 
-__device__ __forceinline__ void store_le(uint8_t* dst, uint32_t pos, uint64_t v, uint32_t n) {
+template <class D>
+__device__ __forceinline__ void store_le(D* dst, uint32_t pos, uint64_t v, uint32_t n) {
   for (uint32_t k = 0; k < n; ++k) dst[pos + k] = (uint8_t)(v >> (8 * k));
 }
 
@@ -2294,7 +2312,7 @@ __global__ __launch_bounds__(kE3Threads) void encode_large_kernel(EncodeParams P
       const uint32_t nbk = (plen - 1) / 1024;
       for (uint32_t n0 = 0; n0 < nbk; n0 += 64) {
         const uint32_t n1 = min(nbk, n0 + 64);
-        xxh3_kib_contribs(img, p0 + 1024 * n0, (n1 - n0) * 1024 + 1, &kLongSecret, contrib, wave, kE3Waves);
+        xxh3_kib_contribs<false>(img, p0 + 1024 * n0, (n1 - n0) * 1024 + 1, &kLongSecret, contrib, wave, kE3Waves);
         __syncthreads();
         if (wave == 0)
           for (uint32_t k = 0; k < n1 - n0; ++k) {
@@ -2481,12 +2499,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LSM_REC_WPE
   const uint64_t per = (units + gridDim.x - 1) / gridDim.x;
   const uint64_t u_begin = (uint64_t)blockIdx.x * per, u_end = min(units, u_begin + per);
   uint32_t i = u_begin < u_end ? last_le_u64(L.upre, n3, u_begin) : 0;
+#ifdef LSM_DIAG  // diagnostic per-phase s_memtime totals of wave 0 (reserved bit 0x40)
+  uint32_t ph_acc[8] = {}, ph_n = 0;
+  uint64_t t_last = __builtin_amdgcn_s_memtime();
+#define REC_PHASE(k)                                   \
+  if (P.diag & 0x40) {                                 \
+    const uint64_t t_ = __builtin_amdgcn_s_memtime();  \
+    ph_acc[k] += (uint32_t)(t_ - t_last);              \
+    t_last = t_;                                       \
+  }
+#else
+#define REC_PHASE(k)
+#endif
   for (uint64_t u = u_begin; u < u_end; ++u) {
-    while (i + 1 < n3 && L.upre[i + 1] <= u) ++i;
-    const EncHuge h = L.rec[i];
+    REC_PHASE(6);
+    while (i + 1 < n3 && gload(L.upre, i + 1) <= u) ++i;
+    const EncHuge h = gload_pod(L.rec, i);
     if (!h.accepted) continue;  // (uniform; rejected blocks own no units)
-    const uint32_t k = (uint32_t)(u - L.upre[i]);
-    const BlockPlan pl = P.plans[h.b];
+    const uint32_t k = (uint32_t)(u - gload(L.upre, i));
+    const BlockPlan pl = gload_pod(P.plans, h.b);
     const uint32_t step = pl.step_flags & 0xFF;
     const uint32_t ri = is_index(P) ? 1 : P.ri;
     const uint32_t plen = h.total - kHdrLen;
@@ -2494,6 +2525,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LSM_REC_WPE
     uint8_t* img = reinterpret_cast<uint8_t*>(dabs & ~15ULL);
     const uint32_t p0 = (uint32_t)(dabs & 15) + kHdrLen;
     const uint32_t bin_off = pl.recs + 1;
+    REC_PHASE(0);
     if (k < h.nru) {
       if (h.n <= kGItems) {  // one pass: record offsets from a workgroup scan
         const uint32_t j = tid;
@@ -2511,44 +2543,48 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LSM_REC_WPE
         if (j < h.n) {
           RecordCopy rc;
           rc.issue(P, m, head, p0 + roff);
-          rc.store(P, m, head, img);
-          if (head) store_le(img, p0 + bin_off + (j / ri) * step, roff, step);
+          rc.store(P, m, head, as_gbl(img));
+          if (head) store_le(as_gbl(img), p0 + bin_off + (j / ri) * step, roff, step);
         }
         __syncthreads();  // (psum is rewritten by the next unit)
       } else {
         // records [j0, j1) assembled in LDS (image bytes [a0, a0 + lend)), then copied
         // out in 16-B pieces; a unit larger than the image writes straight to HBM
         const uint32_t j0 = k * h.ipu, j1 = min(h.n, j0 + h.ipu);
-        const uint32_t rb = P.erec[h.s + j0], re = j1 < h.n ? P.erec[h.s + j1] : pl.recs;
+        const uint32_t rb = gload(P.erec, (uint64_t)h.s + j0), re = j1 < h.n ? gload(P.erec, (uint64_t)h.s + j1) : pl.recs;
         const uint32_t a0 = (p0 + rb) & ~15u, lend = p0 + re - a0;
         const bool staged = lend + 32 <= kEHugeImg;  // (uniform)
         uint8_t* limg = reinterpret_cast<uint8_t*>(lbuf) - a0;  // image offset x -> LDS limg + x
-        auto put = [&](uint8_t* dst) {  // (two call sites: LDS and global stores)
+        auto put = [&](auto* dst) {  // (two call sites: LDS and global stores)
           for (uint32_t j = j0 + tid; j < j1; j += 256) {
             const bool head = j % ri == 0;
             bool bad = false;
             // (after E1p the shared prefix is in hbucket: no key reads before the copy)
             ItemMeta m = P.hb_sh ? load_item(P, (uint64_t)h.s + j, bad) : load_item_lcp(P, h.s, j, ri, bad);
-            if (P.hb_sh && !head) m.sh = P.hbucket[(uint64_t)h.s + j];
-            const uint32_t roff = P.erec[h.s + j];
+            if (P.hb_sh && !head) m.sh = gload(P.hbucket, (uint64_t)h.s + j);
+            const uint32_t roff = gload(P.erec, (uint64_t)h.s + j);
             RecordCopy rc;
             rc.issue(P, m, head, p0 + roff);
             rc.store(P, m, head, dst);
-            if (head) store_le(img, p0 + bin_off + (j / ri) * step, roff, step);
+            if (head) store_le(as_gbl(img), p0 + bin_off + (j / ri) * step, roff, step);
           }
         };
-        if (staged) put(limg);
-        else put(img);
+        if (staged) put(as_lds(limg));
+        else put(as_gbl(img));
+        REC_PHASE(1);
         if (staged) {
           __syncthreads();
+          REC_PHASE(2);
           if (h.nbk) {  // the KiB blocks wholly inside these records: contributions from the image
             const uint32_t g0 = (rb + 1023) / 1024, g1 = min(h.nbk, re / 1024);
             if (g1 > g0) {
-              const uint64_t kg = L.kpre[i] + g0;
-              xxh3_kib_contribs(limg, p0 + 1024 * g0, (g1 - g0) * 1024 + 1, &kLongSecret, L.contrib + 8 * kg, wave, 4);
+              const uint64_t kg = gload(L.kpre, i) + g0;
+              xxh3_kib_contribs(reinterpret_cast<const uint8_t*>(lbuf), p0 + 1024 * g0 - a0, (g1 - g0) * 1024 + 1,
+                                &kLongSecret, L.contrib + 8 * kg, wave, 4);  // (lbuf-relative: ds_read, not flat)
               for (uint32_t g = tid; g < g1 - g0; g += 256) L.kdone[kg + g] = 1;
             }
           }
+          REC_PHASE(3);
           const uint32_t lo = (p0 + rb) - a0, c0 = (lo + 15) >> 4, c1 = lend >> 4;
           const u32x4* src = reinterpret_cast<const u32x4*>(lbuf);
           u32x4* dst = reinterpret_cast<u32x4*>(img + a0);
@@ -2561,8 +2597,12 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LSM_REC_WPE
           if (tid == kWave && c1 >= c0)
             for (uint32_t x = 16 * c1; x < lend; ++x) gb[x] = lb[x];
           __syncthreads();  // (the next unit rewrites the image)
+          REC_PHASE(4);
         }
       }
+#ifdef LSM_DIAG
+      ++ph_n;
+#endif
       continue;
     }
     // tail unit: hash-index votes (LDS passes), marker, trailer
@@ -2591,7 +2631,15 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LSM_REC_WPE
       if (lane == 0) img[p0 + pl.recs] = kTrailerMarker;
       write_trailer_bytes(img, p0 + plen - kTrailerLen, ri, step, pl.bin_len, bin_off, pl.hash_w, hash_off, h.n);
     }
+    REC_PHASE(5);
   }
+#ifdef LSM_DIAG
+  if ((P.diag & 0x40) && tid == 0) {
+    for (int k = 0; k < 7; ++k) atomicAdd(&P.phase[k], (unsigned long long)ph_acc[k]);
+    atomicAdd(&P.phase[15], (unsigned long long)ph_n);
+  }
+#endif
+#undef REC_PHASE
 }
 
 // The contributions the records kernel left (KiB blocks across two record
