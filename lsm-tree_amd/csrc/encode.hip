@@ -1564,17 +1564,26 @@ __device__ __forceinline__ uint64_t shfl_down64(uint64_t v, int o) {
          ((uint64_t)(uint32_t)__shfl_down((int)(uint32_t)(v >> 32), o) << 32);
 }
 
-// The block of item i from the workgroup's first item's block (one binary search
-// per workgroup, by thread 0): blocks of >= 4 Ki items on average leave at most
-// a step or two per thread.
+// The block of item i from the workgroup's first item's block, found by a
+// 256-way search of the starts (every thread one sample per round: one round
+// for batches of <= 256 blocks; a thread-0 binary search was eight dependent
+// loads before any item load of the workgroup); blocks of >= 4 Ki items on
+// average leave at most a step or two per thread.
 __device__ __forceinline__ uint32_t wg_block_of_item(const EncodeParams& P, uint32_t i, uint32_t* sh) {
   const uint32_t i_begin = clamped_start(P, 0), i_end = clamped_start(P, P.n_blocks);
-  if (threadIdx.x == 0) {
-    const uint32_t first = max(blockIdx.x * 256u, i_begin);
-    *sh = first < i_end ? block_of_item(P, first) : 0;
+  const uint32_t first = max(blockIdx.x * 256u, i_begin);
+  uint32_t lo = 0, hi = P.n_blocks;  // last b in [lo, hi) with start[b] <= first
+  if (first >= i_end) hi = 1;       // (no item of the batch here: block 0, unused)
+  while (hi - lo > 1) {             // (uniform)
+    const uint32_t st = (hi - lo + 255) / 256;
+    const uint32_t x = lo + threadIdx.x * st;
+    const uint32_t c = (uint32_t)__syncthreads_count(x < hi && clamped_start(P, x) <= first);
+    const uint32_t nlo = lo + (c ? c - 1 : 0) * st;  // (c = 0 only for a non-monotone array: rejected anyway)
+    hi = min(hi, nlo + st);
+    lo = nlo;
   }
-  __syncthreads();
-  uint32_t b = *sh;
+  (void)sh;
+  uint32_t b = lo;
   while (b + 1 < P.n_blocks && clamped_start(P, b + 1) <= i) ++b;
   return b;
 }

@@ -31,15 +31,31 @@ __device__ __forceinline__ uint64_t block_excl_scan_u64(uint64_t v, uint64_t* sh
   return wbase + incl - v;
 }
 
+// A thread's kScanPerThread inputs: one vector load when all are in range
+// (the inputs are 256-B aligned workspace arrays), else one at a time.
+template <class T>
+__device__ __forceinline__ void scan_load(const T* in, uint64_t base, uint64_t n, uint64_t (&v)[kScanPerThread]) {
+  typedef T vec_t __attribute__((ext_vector_type(kScanPerThread)));
+  if (base + kScanPerThread <= n) {
+    const vec_t x = *(const __attribute__((address_space(1))) vec_t*)(in + base);
+#pragma unroll
+    for (int i = 0; i < kScanPerThread; ++i) v[i] = x[i];
+  } else {
+#pragma unroll
+    for (int i = 0; i < kScanPerThread; ++i) v[i] = base + i < n ? in[base + i] : 0;
+  }
+}
+
 template <class T>
 __global__ __launch_bounds__(kScanThreads) void scan_tile_reduce(const T* __restrict__ in, uint64_t n,
                                                                  uint64_t* __restrict__ tile_sums) {
   __shared__ uint64_t sh[kScanThreads / 64];
   const uint64_t base = (uint64_t)blockIdx.x * kScanTile + (uint64_t)threadIdx.x * kScanPerThread;
+  uint64_t v[kScanPerThread];
+  scan_load(in, base, n, v);
   uint64_t s = 0;
 #pragma unroll
-  for (int i = 0; i < kScanPerThread; ++i)
-    if (base + i < n) s += in[base + i];
+  for (int i = 0; i < kScanPerThread; ++i) s += v[i];
   uint64_t total;
   block_excl_scan_u64(s, sh, total);
   if (threadIdx.x == 0) tile_sums[blockIdx.x] = total;
@@ -68,12 +84,10 @@ __global__ __launch_bounds__(kScanThreads) void scan_tile_apply(const T* in, uin
   __shared__ uint64_t sh[kScanThreads / 64];
   const uint64_t base = (uint64_t)blockIdx.x * kScanTile + (uint64_t)threadIdx.x * kScanPerThread;
   uint64_t v[kScanPerThread];
+  scan_load(in, base, n, v);
   uint64_t s = 0;
 #pragma unroll
-  for (int i = 0; i < kScanPerThread; ++i) {
-    v[i] = base + i < n ? in[base + i] : 0;
-    s += v[i];
-  }
+  for (int i = 0; i < kScanPerThread; ++i) s += v[i];
   uint64_t total;
   uint64_t ex = block_excl_scan_u64(s, sh, total) + tile_offsets[blockIdx.x];
 #pragma unroll
