@@ -827,8 +827,8 @@ __global__ __launch_bounds__(kBigWaves * kWave) void decode_deferred_staged_kern
 //          runs past the staged bytes) and computes the XXH3 contributions
 //          of the KiB blocks that start in the window, from LDS too
 //   chain  (decode_huge_chain_kernel): one wave per block, the eight
-//          accumulator chains on lanes 0..7 (xxh3_chain8)
-//   finish (decode_huge_finish_kernel): tail merge, checksum compare, status
+//          accumulator chains on lanes 0..7 (xxh3_chain8), then the tail
+//          merge, the checksum compare and the status
 // A block whose header fails, or that no longer fits the pool, goes to the
 // general path (defer2) as before: statuses and outputs are the same on both.
 #ifndef LSM_HUGE_WIN_KIB
@@ -1487,46 +1487,34 @@ __global__ __launch_bounds__(256) void decode_huge_kernel(DecodeParams P) {
 }
 
 // Chains of the huge blocks: a single-wave workgroup per block, its eight
-// accumulators on lanes 0..7 (xxh3_chain8).  The merge runs in
-// decode_huge_finish_kernel: the kernel boundary makes the eight results
-// visible (an agent-scope fence per chain would write back the XCD's whole L2).
+// accumulators on lanes 0..7 (xxh3_chain8), then on the same wave the tail
+// merge, the checksum compare and the status (oracle order: payload checksum,
+// then trailer, then parse).  The contributions cross a kernel boundary (an
+// agent-scope fence per unit would write back the XCD's whole L2); the chain
+// results stay in the wave, so the merge needs no second kernel.
 __global__ __launch_bounds__(64) void decode_huge_chain_kernel(DecodeParams P) {
   __shared__ __attribute__((aligned(16))) uint8_t ring[kChainRing * 1024];
-  const HugeHdr* hp = reinterpret_cast<const HugeHdr*>(P.huge_pool);
-  const uint32_t n = hp->n3;
-  if (!n || (P.flags & LSM_DECODE_PAYLOAD_VERIFIED)) return;
-  const HugeLayout L = huge_layout(P, n);
-  const uint32_t k = threadIdx.x & 7;
-  for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
-    HugeRec* r = L.rec + i;
-    if (!r->accepted || !r->nbk) continue;
-    uint64_t a0, a1;
-    xxh3_acc_init((int)(k >> 1), a0, a1);
-    const uint64_t x = xxh3_chain8<kChainRing>(L.contrib + 8 * gload(L.kpre, i), r->nbk, (k & 1) ? a1 : a0,
-                                               kLongSecret.acc[16 + k], ring);
-    if (threadIdx.x < 8) r->acc[k] = x;
-  }
-}
-
-// Wave per huge block: tail merge, checksum compare, status (oracle order:
-// payload checksum, then trailer, then parse).
-__global__ __launch_bounds__(256) void decode_huge_finish_kernel(DecodeParams P) {
   const HugeHdr* hp = reinterpret_cast<const HugeHdr*>(P.huge_pool);
   const uint32_t n = hp->n3;
   if (!n) return;
   const HugeLayout L = huge_layout(P, n);
   const bool hash = !(P.flags & LSM_DECODE_PAYLOAD_VERIFIED);
-  const int lane = threadIdx.x & 63, q = lane & 3;
-  for (uint32_t i = (blockIdx.x * blockDim.x + threadIdx.x) / 64; i < n; i += gridDim.x * blockDim.x / 64) {
+  const uint32_t lane = threadIdx.x & 63, k = lane & 7, q = lane & 3;
+  for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
     const HugeRec* r = L.rec + i;
     if (!r->accepted) continue;
     const BlockMeta m = r->m;
-    const int32_t tail_st = m.st != ST_OK ? m.st : r->parse_bad ? (int32_t)ST_PARSE : (int32_t)ST_OK;
-    int32_t st = tail_st;
+    int32_t st = m.st != ST_OK ? m.st : r->parse_bad ? (int32_t)ST_PARSE : (int32_t)ST_OK;
     if (hash) {
+      uint64_t a0, a1;
+      xxh3_acc_init((int)(k >> 1), a0, a1);
+      uint64_t x = (k & 1) ? a1 : a0;
+      if (r->nbk)
+        x = xxh3_chain8<kChainRing>(L.contrib + 8 * gload(L.kpre, i), r->nbk, x, kLongSecret.acc[16 + k], ring);
+      // lane quad position q takes accumulators 2q, 2q + 1 (lanes 2q, 2q + 1 hold them)
+      const uint64_t c0 = wave_shfl_u64(x, (int)(2 * q)), c1 = wave_shfl_u64(x, (int)(2 * q + 1));
       uint64_t lo, hi;
-      xxh3_wave_tail_merge(P.blocks + r->span0, m.p0, m.len - kHdrLen, &kLongSecret, r->acc[2 * q], r->acc[2 * q + 1],
-                           lo, hi);
+      xxh3_wave_tail_merge(P.blocks + r->span0, m.p0, m.len - kHdrLen, &kLongSecret, c0, c1, lo, hi);
       if (lo != m.ck_lo || hi != m.ck_hi) st = ST_CKSUM;
     }
     if (lane == 0) gstore(P.status, r->b, st);
@@ -1883,7 +1871,6 @@ hipError_t launch_decode(const DecodeParams& P0, void* ws, size_t ws_bytes, hipS
     hipLaunchKernelGGL(decode_huge_units_kernel, dim3(kHugeUnitsGrid), dim3(256), 0, st, P);
     if ((e = hipLaunchKernel(hk, dim3(kHugeGrid), dim3(256), args, kHugeLds, st)) != hipSuccess) return e;
     hipLaunchKernelGGL(decode_huge_chain_kernel, dim3(kHugeChainGrid), dim3(64), 0, st, P);
-    hipLaunchKernelGGL(decode_huge_finish_kernel, dim3(256), dim3(256), 0, st, P);
   }
   return hipGetLastError();
 }

@@ -2357,8 +2357,8 @@ __global__ __launch_bounds__(kE3Threads) void encode_large_kernel(EncodeParams P
 //            (the contributions of the KiB blocks wholly inside a unit's LDS
 //            image come from the image, flagged done)
 //   hash     XXH3 contributions of the other KiB blocks into the pool
-//   chain    one wave per block, the eight accumulator chains on lanes 0..7
-//   finish   wave per block: tail merge, header, status
+//   chain    one wave per block: the eight accumulator chains on lanes 0..7,
+//            then the tail merge, the header and the status
 constexpr uint32_t kEHugeItems = 1024;  // items per record unit, at most (four per thread)
 constexpr uint32_t kEHugeImg = 2 * 4 * kE3HashChunk;  // LDS image of a record unit (the tail unit's vote arrays)
 constexpr uint32_t kEHugeGrid = 2048;
@@ -2728,41 +2728,30 @@ __global__ __launch_bounds__(256) void encode_huge_contrib_kernel(EncodeParams P
 }
 
 // A single-wave workgroup per block, its eight accumulators on lanes 0..7
-// (xxh3_chain8).  The merge and the header run in encode_huge_finish_kernel:
-// the kernel boundary makes the eight results visible (an agent-scope fence
-// per chain would write back the XCD's whole L2).
+// (xxh3_chain8), then on the same wave the tail merge, the header
+// (Header::encode_into) and the status.  The contributions cross a kernel
+// boundary (an agent-scope fence per unit would write back the XCD's whole L2).
 constexpr uint32_t kEChainRing = 16;
 __global__ __launch_bounds__(64) void encode_huge_chain_kernel(EncodeParams P) {
   __shared__ __attribute__((aligned(16))) uint8_t ring[kEChainRing * 1024];
   const EncHugeLayout L = enc_huge_layout(P);
   const uint32_t n3 = L.hdr->n3;
   if (!n3) return;
-  const uint32_t k = threadIdx.x & 7;
+  const uint32_t lane = threadIdx.x & 63, k = lane & 7, q = lane & 3;
   for (uint32_t i = blockIdx.x; i < n3; i += gridDim.x) {
-    EncHuge* r = L.rec + i;
+    const EncHuge* r = L.rec + i;
     if (!r->accepted) continue;
     uint64_t a0, a1;
     xxh3_acc_init((int)(k >> 1), a0, a1);
-    const uint64_t x =
-        xxh3_chain8<kEChainRing>(L.contrib + 8 * L.kpre[i], r->nbk, (k & 1) ? a1 : a0, kLongSecret.acc[16 + k], ring);
-    if (threadIdx.x < 8) r->acc[k] = x;
-  }
-}
-
-// Wave per huge block: tail merge, header (Header::encode_into), status.
-__global__ __launch_bounds__(256) void encode_huge_finish_kernel(EncodeParams P) {
-  const EncHugeLayout L = enc_huge_layout(P);
-  const uint32_t n3 = L.hdr->n3;
-  if (!n3) return;
-  const int lane = threadIdx.x & 63, q = lane & 3;
-  for (uint32_t i = (blockIdx.x * blockDim.x + threadIdx.x) / 64; i < n3; i += gridDim.x * blockDim.x / 64) {
-    const EncHuge* r = L.rec + i;
-    if (!r->accepted) continue;
+    uint64_t x = (k & 1) ? a1 : a0;
+    if (r->nbk) x = xxh3_chain8<kEChainRing>(L.contrib + 8 * L.kpre[i], r->nbk, x, kLongSecret.acc[16 + k], ring);
+    // lane quad position q takes accumulators 2q, 2q + 1 (lanes 2q, 2q + 1 hold them)
+    const uint64_t c0 = wave_shfl_u64(x, (int)(2 * q)), c1 = wave_shfl_u64(x, (int)(2 * q + 1));
     const uint64_t dabs = (uint64_t)(uintptr_t)P.out + r->dst_off;
     uint8_t* img = reinterpret_cast<uint8_t*>(dabs & ~15ULL);
     const uint32_t pad = (uint32_t)(dabs & 15), plen = r->total - kHdrLen;
     uint64_t lo, hi;
-    xxh3_wave_tail_merge(img, pad + kHdrLen, plen, &kLongSecret, r->acc[2 * q], r->acc[2 * q + 1], lo, hi);
+    xxh3_wave_tail_merge(img, pad + kHdrLen, plen, &kLongSecret, c0, c1, lo, hi);
     write_header_bytes(img, pad, P.type, lo, hi, plen);
     if (lane == 0) P.status[r->b] = ST_OK;
   }
@@ -2964,7 +2953,6 @@ hipError_t launch_encode(const lsm_items& items, const uint32_t* starts, uint32_
     hipLaunchKernelGGL(encode_huge_contrib_kernel, dim3(kEHugeGrid), dim3(256), 0, st, P);
     // (an unused 40 KiB LDS request: one chain workgroup per SIMD)
     hipLaunchKernelGGL(encode_huge_chain_kernel, dim3(1024), dim3(64), 0, st, P);
-    hipLaunchKernelGGL(encode_huge_finish_kernel, dim3(256), dim3(256), 0, st, P);
   }
   hipLaunchKernelGGL(encode_large_kernel, dim3(512), dim3(kE3Threads), 0, st, P);
   return hipGetLastError();

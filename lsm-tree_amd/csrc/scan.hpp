@@ -1,6 +1,7 @@
 // scan.hpp — device-wide exclusive prefix sum over u64 counts (block item
 // counts -> item_start, encoded block sizes -> block offsets).
-// Three small launches: per-tile reduce, scan of tile sums, per-tile scan.
+// Three small launches: per-tile reduce, scan of tile sums, per-tile scan
+// (one, for a single tile).
 #pragma once
 
 #include <hip/hip_runtime.h>
@@ -77,6 +78,7 @@ static __global__ __launch_bounds__(kScanThreads) void scan_tile_sums(uint64_t* 
 
 // Out(i, prefix) is called for i in [0, n] with the exclusive prefix.  Each
 // thread reads its inputs before its first Out call, so Out may overwrite in[i].
+// tile_offsets == nullptr: a single tile (no tile sums to add).
 template <class T, class Out>
 __global__ __launch_bounds__(kScanThreads) void scan_tile_apply(const T* in, uint64_t n,
                                                                 const uint64_t* __restrict__ tile_offsets,
@@ -89,7 +91,7 @@ __global__ __launch_bounds__(kScanThreads) void scan_tile_apply(const T* in, uin
 #pragma unroll
   for (int i = 0; i < kScanPerThread; ++i) s += v[i];
   uint64_t total;
-  uint64_t ex = block_excl_scan_u64(s, sh, total) + tile_offsets[blockIdx.x];
+  uint64_t ex = block_excl_scan_u64(s, sh, total) + (tile_offsets ? tile_offsets[blockIdx.x] : 0);
 #pragma unroll
   for (int i = 0; i < kScanPerThread; ++i) {
     if (base + i < n) out(base + i, ex);
@@ -104,6 +106,11 @@ inline uint64_t scan_tiles(uint64_t n) { return (n + kScanTile - 1) / kScanTile;
 template <class T, class Out>
 inline hipError_t launch_excl_scan(const T* in, uint64_t n, uint64_t* tmp, Out out, hipStream_t st) {
   const uint64_t tiles = scan_tiles(n);
+  if (tiles == 1) {  // (a batch of <= 2048 blocks: one launch, not three of ~4.5 us each)
+    hipLaunchKernelGGL((scan_tile_apply<T, Out>), dim3(1), dim3(kScanThreads), 0, st, in, n, (const uint64_t*)nullptr,
+                       out);
+    return hipGetLastError();
+  }
   hipLaunchKernelGGL(scan_tile_reduce<T>, dim3((uint32_t)tiles), dim3(kScanThreads), 0, st, in, n, tmp);
   hipLaunchKernelGGL(scan_tile_sums, dim3(1), dim3(kScanThreads), 0, st, tmp, tiles);
   hipLaunchKernelGGL((scan_tile_apply<T, Out>), dim3((uint32_t)tiles), dim3(kScanThreads), 0, st, in, n,
