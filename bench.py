@@ -473,9 +473,11 @@ def bench_large_blocks(torch, lsmgpu, threads, steps=5):
         del items, enc, out, ref_buf
         torch.cuda.empty_cache()
     res["note"] = ("the workspace pool (lsm_*_workspace_size_ex) spreads each block over the GPU: encode = "
-                   "item-parallel plan (E1p), record units assembled in LDS + 16-B copy-out, KiB contribution "
-                   "units, eight XXH3 chains per block; decode = 32 KiB staged windows (phase A/B or interval "
-                   "walks, KiB contributions), eight chains per block, finish")
+                   "item-parallel plan (E1p), record units assembled in LDS (their KiB contributions from the "
+                   "image) + 16-B copy-out, the leftover KiB blocks, one wave per block for the eight XXH3 "
+                   "chains + header; decode = unit table, 32 KiB staged windows (phase A on one wave while three "
+                   "reduce KiB contributions; interval walks for odd shapes), one wave per block for the chains "
+                   "+ checksum + status")
     return res
 
 

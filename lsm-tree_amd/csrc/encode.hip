@@ -2359,7 +2359,10 @@ __global__ __launch_bounds__(kE3Threads) void encode_large_kernel(EncodeParams P
 //   hash     XXH3 contributions of the other KiB blocks into the pool
 //   chain    one wave per block: the eight accumulator chains on lanes 0..7,
 //            then the tail merge, the header and the status
-constexpr uint32_t kEHugeItems = 1024;  // items per record unit, at most (four per thread)
+#ifndef LSM_EHUGE_ITEMS
+#define LSM_EHUGE_ITEMS 1024
+#endif
+constexpr uint32_t kEHugeItems = LSM_EHUGE_ITEMS;  // items per record unit, at most (four per thread)
 constexpr uint32_t kEHugeImg = 2 * 4 * kE3HashChunk;  // LDS image of a record unit (the tail unit's vote arrays)
 constexpr uint32_t kEHugeGrid = 2048;
 
