@@ -575,7 +575,7 @@ struct Group {
 
 // offr / itr: lane l holds block_off / item_start of block b_begin + l.
 __device__ __forceinline__ Group form_group(const DecodeParams& P, uint32_t b, uint32_t b_begin, uint32_t b_end,
-                                            uint32_t gmax, uint64_t offr, uint32_t itr) {
+                                            uint32_t gmax, uint64_t offr, uint32_t itr, uint32_t& skip) {
   const int lane = threadIdx.x & (kWave - 1);
   Group G;
   G.b = b;
@@ -596,6 +596,9 @@ __device__ __forceinline__ Group form_group(const DecodeParams& P, uint32_t b, u
   const bool fits = in_run && !lone && G.end_j >= G.off_j && G.off_j >= off_b &&
                     ((G.end_j + 15) & ~15ULL) - G.span0 <= P.stage_bytes && G.it1_j - G.g_item0 <= P.tile_items;
   G.k = (uint32_t)__builtin_ctzll(~__ballot(fits));  // lanes >= gmax never fit
+  // (k = 0: the run of lone blocks from b, at least one, passed over at once:
+  // 64 huge blocks one form_group at a time took 17 us)
+  skip = max(1u, (uint32_t)__builtin_ctzll(~__ballot(in_run && lone)));
   G.span1 = G.k ? (wave_readlane_u64(G.end_j, G.k - 1) + 15) & ~15ULL : G.span0;
   G.n_items = G.k ? wave_readlane_u32(G.it1_j, G.k - 1) - G.g_item0 : 0;
   return G;
@@ -1580,36 +1583,18 @@ __global__ __launch_bounds__(kGroupWaves * kWave) __attribute__((amdgpu_waves_pe
     reinterpret_cast<uint64_t*>(ls)[tid] = reinterpret_cast<const uint64_t*>(&kLongSecret)[tid];
   uint32_t iter = 0;
   // Next stageable group at or after bb (larger blocks go to the general path).
-  // Lone blocks (larger than the stage, or more items than a tile) go to the
-  // general path, decode_deferred_staged_kernel (a 72 KiB stage, the block
-  // hashed by four waves): listed below by wave 0, one atomic per workgroup,
-  // and passed over here a run at a time (a run of 64 huge blocks took 17 us
-  // one form_group at a time).
-  uint64_t lone_mask;
-  {
-    const uint64_t nx = wave_shfl_u64(offr, min(lane + 1, kWave - 1));
-    const uint32_t ix = (uint32_t)__shfl((int)itr, min(lane + 1, kWave - 1));
-    const bool in = b_begin + lane < b_end;
-    lone_mask = __ballot(in && (((nx + 15) & ~15ULL) - (offr & ~15ULL) > lone_bytes(P) || ix - itr > P.tile_items));
-  }
   auto next_group = [&](uint32_t bb) -> Group {
     for (;;) {
-      if (bb < b_end) {
-        const uint64_t rest = lone_mask >> (bb - b_begin);
-        if (rest & 1) {
-          bb += (uint32_t)__builtin_ctzll(~rest);
-          continue;
-        }
-      }
       if (bb >= b_end) {
         Group z;
         z.b = bb;
         z.k = 0;
         return z;
       }
-      const Group g = form_group(P, bb, b_begin, b_end, gmax, offr, itr);
+      uint32_t skip;
+      const Group g = form_group(P, bb, b_begin, b_end, gmax, offr, itr, skip);
       if (g.k) return g;
-      bb += 1;
+      bb += skip;  // a run of lone blocks: listed for the general path before the loop
     }
   };
   // LDS-DMA of a group's span (wave w moves 1-KiB pieces w, w + 4, ...).
@@ -1621,7 +1606,16 @@ __global__ __launch_bounds__(kGroupWaves * kWave) __attribute__((amdgpu_waves_pe
         __builtin_amdgcn_global_load_lds((gbl_void_t*)(src + 1024 * i), (lds_void_t*)(dst + 1024 * i), 16, 0, 0);
     }
   };
-  if (wave == 0) defer_blocks_wave(P, (lone_mask >> lane) & 1, b_begin + lane);
+  // Lone blocks (larger than the stage, or more items than a tile) go to the
+  // general path, decode_deferred_staged_kernel (a 72 KiB stage, the block
+  // hashed by four waves): listed here, one atomic per workgroup.
+  if (wave == 0) {
+    const uint64_t nx = wave_shfl_u64(offr, min(lane + 1, kWave - 1));
+    const uint32_t ix = (uint32_t)__shfl((int)itr, min(lane + 1, kWave - 1));
+    const bool in = b_begin + lane < b_end;
+    const bool lone = in && (((nx + 15) & ~15ULL) - (offr & ~15ULL) > lone_bytes(P) || ix - itr > P.tile_items);
+    defer_blocks_wave(P, lone, b_begin + lane);
+  }
   Group G = next_group(b_begin);
   if (G.k) issue_dma(G, img);
   for (; G.k; ++iter) {
