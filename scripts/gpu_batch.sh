@@ -2,6 +2,7 @@
 # One GPU call for several checks (GPU slots are scarce).
 set -u
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}"
-V=lsm-tree_amd/.variants
 bash scripts/gpu_steps.sh \
-  "ab:300:for r in 1 2; do for L in lsm-tree_amd/liblsmgpu.so $V/libi256.so $V/libi512.so; do echo == \$L; LSMGPU_LIB=\$L python -u scripts/ab_large.py --which 256KiB,1MiB,4MiB || exit 1; done; done"
+  "all:400:python -u -m pytest tests -m gpu -x -q --timeout 120 --timeout-method thread" \
+  "ab:200:python -u scripts/ab_large.py --which 256KiB,1MiB,4MiB" \
+  "kt:200:bash scripts/prof_steps.sh large 'rocprofv3 --kernel-trace --stats -d gpurun_out/kt_large -o run --output-format csv -- python3 scripts/ab_large.py --which 1MiB,4MiB --steps 2'"
