@@ -1564,14 +1564,21 @@ __device__ __forceinline__ uint64_t shfl_down64(uint64_t v, int o) {
          ((uint64_t)(uint32_t)__shfl_down((int)(uint32_t)(v >> 32), o) << 32);
 }
 
-// The block of item i from the workgroup's first item's block, found by a
-// 256-way search of the starts (every thread one sample per round: one round
-// for batches of <= 256 blocks; a thread-0 binary search was eight dependent
-// loads before any item load of the workgroup); blocks of >= 4 Ki items on
-// average leave at most a step or two per thread.
-__device__ __forceinline__ uint32_t wg_block_of_item(const EncodeParams& P, uint32_t i, uint32_t* sh) {
-  const uint32_t i_begin = clamped_start(P, 0), i_end = clamped_start(P, P.n_blocks);
-  const uint32_t first = max(blockIdx.x * 256u, i_begin);
+// Items per thread in the item-parallel E1p kernels (strided by 256: each pass
+// of a workgroup is 256 consecutive items); the four items' loads are issued
+// together, and a workgroup's block search serves 1024 items.
+constexpr uint32_t kE1pPer = 4;
+#ifndef LSM_E1P_LEN_PER
+#define LSM_E1P_LEN_PER 1
+#endif
+constexpr uint32_t kE1pLenPer = LSM_E1P_LEN_PER;  // (the lengths kernel: 4 items took 136 VGPRs, 2 ran as 1)
+
+// The block holding item `first` (the workgroup's first item), by a 256-way
+// search of the starts (every thread one sample per round: one round for
+// batches of <= 256 blocks; a thread-0 binary search was eight dependent loads
+// before any item load of the workgroup).  Every thread calls it (a barrier).
+__device__ __forceinline__ uint32_t wg_first_block(const EncodeParams& P, uint32_t first) {
+  const uint32_t i_end = clamped_start(P, P.n_blocks);
   uint32_t lo = 0, hi = P.n_blocks;  // last b in [lo, hi) with start[b] <= first
   if (first >= i_end) hi = 1;       // (no item of the batch here: block 0, unused)
   while (hi - lo > 1) {             // (uniform)
@@ -1582,64 +1589,117 @@ __device__ __forceinline__ uint32_t wg_block_of_item(const EncodeParams& P, uint
     hi = min(hi, nlo + st);
     lo = nlo;
   }
-  (void)sh;
-  uint32_t b = lo;
-  while (b + 1 < P.n_blocks && clamped_start(P, b + 1) <= i) ++b;
-  return b;
+  return lo;
+}
+
+// This thread's kE1pPer items (base + 256 j + tid): each one's block and range,
+// walking forward from the workgroup's first block (blocks of >= 4 Ki items on
+// average: a step or two at most).
+template <uint32_t K>
+struct E1pItems {
+  uint32_t i[K], b[K], s[K], e[K];
+  bool in[K];
+};
+template <uint32_t K>
+__device__ __forceinline__ E1pItems<K> e1p_items(const EncodeParams& P) {
+  E1pItems<K> t;
+  const uint32_t i_begin = clamped_start(P, 0), i_end = clamped_start(P, P.n_blocks);
+  const uint32_t base = blockIdx.x * (256 * K);
+  uint32_t b = wg_first_block(P, max(base, i_begin));
+  uint32_t bs = clamped_start(P, b), be = clamped_start(P, b + 1);
+#pragma unroll
+  for (uint32_t j = 0; j < K; ++j) {
+    const uint32_t i = base + 256 * j + threadIdx.x;
+    const bool in = i >= i_begin && i < i_end && (uint64_t)i < P.it.n_items;
+    while (in && b + 1 < P.n_blocks && be <= i) {
+      ++b;
+      bs = be;
+      be = clamped_start(P, b + 1);
+    }
+    t.i[j] = i;
+    t.b[j] = b;
+    t.s[j] = bs;
+    t.e[j] = be;
+    t.in[j] = in;
+  }
+  return t;
 }
 
 __global__ __launch_bounds__(256) void encode_e1p_lengths_kernel(EncodeParams P) {
-  __shared__ uint32_t sb;
-  const uint32_t gid = blockIdx.x * 256 + threadIdx.x;
-  if (gid < P.n_blocks && clamped_start(P, gid + 1) < clamped_start(P, gid)) atomicOr(P.e1p_flag, 1u);
-  const uint32_t i = gid, i_begin = clamped_start(P, 0), i_end = clamped_start(P, P.n_blocks);
-  const bool in = i >= i_begin && i < i_end && (uint64_t)gid < P.it.n_items;
-  const uint32_t bw = wg_block_of_item(P, in ? i : 0, &sb);  // (every thread: it holds a barrier)
-  const uint32_t b = in ? bw : 0;
-  const uint32_t s = clamped_start(P, b), e = clamped_start(P, b + 1);
-  const bool live = in && s <= i && i < e;  // (not, for a non-monotone array: every block is rejected)
-  const uint32_t ri = P.ri, jj = i - s;
-  const bool head = jj % ri == 0;
-  uint64_t rec = 0;
-  bool bad = false;
-  if (live) {
-    RawItem r = load_raw<false>(P, i);
-    ItemMeta m = cook_item<false>(r, bad);
-    if (!head) {
-      const uint64_t h = (uint64_t)i - jj % ri;
-      const uint64_t hko = P.it.key_off[h];
-      const uint32_t n = min((uint32_t)min(P.it.key_off[h + 1] - hko, (uint64_t)0xFFFF), m.klen);
-      const Win16 wa = gwin16(P.it.keys + hko), wb = gwin16(P.it.keys + m.ko);
-      const uint64_t x0 = wa.lo ^ wb.lo, x1 = wa.hi ^ wb.hi;
-      uint32_t sh;
-      if (x0) sh = min(n, (uint32_t)(__builtin_ctzll(x0) >> 3));
-      else if (x1) sh = min(n, 8 + (uint32_t)(__builtin_ctzll(x1) >> 3));
-      else sh = n <= 16 ? n : lcp_tail(P.it.keys, hko, m.ko, n);
-      m.sh = sh;
-      P.hbucket[i] = (uint16_t)min(sh, 0xFFFFu);
+  for (uint64_t x = (uint64_t)blockIdx.x * 256 + threadIdx.x; x < P.n_blocks; x += (uint64_t)gridDim.x * 256)
+    if (clamped_start(P, (uint32_t)x + 1) < clamped_start(P, (uint32_t)x)) atomicOr(P.e1p_flag, 1u);
+  const E1pItems<kE1pLenPer> T = e1p_items<kE1pLenPer>(P);
+  const uint32_t ri = P.ri, lane = threadIdx.x & 63;
+  bool live[kE1pLenPer], head[kE1pLenPer];
+  RawItem r[kE1pLenPer];
+  uint64_t hko[kE1pLenPer], hko1[kE1pLenPer];
+#pragma unroll
+  for (uint32_t j = 0; j < kE1pLenPer; ++j) {  // every item's loads first
+    const uint32_t i = T.i[j];
+    live[j] = T.in[j] && T.s[j] <= i && i < T.e[j];  // (not, for a non-monotone array: every block is rejected)
+    head[j] = (i - T.s[j]) % ri == 0;
+    hko[j] = hko1[j] = 0;
+    if (live[j]) {
+      r[j] = load_raw<false>(P, i);
+      if (!head[j]) {
+        const uint64_t h = (uint64_t)i - (i - T.s[j]) % ri;
+        hko[j] = gload(P.it.key_off, h);
+        hko1[j] = gload(P.it.key_off, h + 1);
+      }
     }
-    rec = item_record_len(P, m, head);
   }
-  if ((uint64_t)gid < P.it.n_items) P.erec[i] = (uint32_t)min(rec, (uint64_t)0xFFFFFFFFu);
-  // per-block exact totals without same-address atomics (a 4-MiB block's ~800
-  // waves would serialise on one word): lanes of one block summed first (blocks
-  // are runs of lanes); a block inside this wave stores its total, one that began
-  // in an earlier wave its part as this wave's head, one that goes on past this
-  // wave its part as this wave's tail (encode_e1p_blocks_kernel adds them up)
-  const uint32_t lane = threadIdx.x & 63;
-  const uint32_t bb = live ? b : 0xFFFFFFFFu;
-  uint64_t sum = rec | (bad ? kE1pBad : 0);
-  for (int o = 1; o < 64; o <<= 1) {  // segmented wave reduction: run heads end with their run's total
-    const uint64_t v = shfl_down64(sum, o);
-    const uint32_t bo = (uint32_t)__shfl_down((int)bb, o);
-    if ((int)lane + o < 64 && bo == bb) sum = e1p_add(sum, v);
+  ItemMeta m[kE1pLenPer];
+  bool bad[kE1pLenPer];
+  Win16 wa[kE1pLenPer], wb[kE1pLenPer];
+#pragma unroll
+  for (uint32_t j = 0; j < kE1pLenPer; ++j) {  // then the key windows of the shared prefixes
+    bad[j] = false;
+    if (live[j]) {
+      m[j] = cook_item<false>(r[j], bad[j]);
+      if (!head[j]) {
+        wa[j] = gwin16(P.it.keys + hko[j]);
+        wb[j] = gwin16(P.it.keys + m[j].ko);
+      }
+    }
   }
-  const uint32_t bprev = (uint32_t)__shfl_up((int)bb, 1);
-  if (live && (lane == 0 || bprev != bb)) {
-    const uint32_t w0 = gid - lane;
-    if (s >= w0 && e - w0 <= 64) P.sizes[b] = sum;
-    else if (s < w0) P.wpart[2 * (uint64_t)(w0 / 64)] = sum;
-    else P.wpart[2 * (uint64_t)(w0 / 64) + 1] = sum;
+#pragma unroll
+  for (uint32_t j = 0; j < kE1pLenPer; ++j) {
+    const uint32_t i = T.i[j];
+    uint64_t rec = 0;
+    if (live[j]) {
+      if (!head[j]) {
+        const uint32_t n = min((uint32_t)min(hko1[j] - hko[j], (uint64_t)0xFFFF), m[j].klen);
+        const uint64_t x0 = wa[j].lo ^ wb[j].lo, x1 = wa[j].hi ^ wb[j].hi;
+        uint32_t sh;
+        if (x0) sh = min(n, (uint32_t)(__builtin_ctzll(x0) >> 3));
+        else if (x1) sh = min(n, 8 + (uint32_t)(__builtin_ctzll(x1) >> 3));
+        else sh = n <= 16 ? n : lcp_tail(P.it.keys, hko[j], m[j].ko, n);
+        m[j].sh = sh;
+        P.hbucket[i] = (uint16_t)min(sh, 0xFFFFu);
+      }
+      rec = item_record_len(P, m[j], head[j]);
+    }
+    if ((uint64_t)i < P.it.n_items) P.erec[i] = (uint32_t)min(rec, (uint64_t)0xFFFFFFFFu);
+    // per-block exact totals without same-address atomics (a 4-MiB block's ~800
+    // waves would serialise on one word): lanes of one block summed first (blocks
+    // are runs of lanes); a block inside this wave stores its total, one that began
+    // in an earlier wave its part as this wave's head, one that goes on past this
+    // wave its part as this wave's tail (encode_e1p_blocks_kernel adds them up)
+    const uint32_t b = T.b[j], s = T.s[j], e = T.e[j];
+    const uint32_t bb = live[j] ? b : 0xFFFFFFFFu;
+    uint64_t sum = rec | (bad[j] ? kE1pBad : 0);
+    for (int o = 1; o < 64; o <<= 1) {  // segmented wave reduction: run heads end with their run's total
+      const uint64_t v = shfl_down64(sum, o);
+      const uint32_t bo = (uint32_t)__shfl_down((int)bb, o);
+      if ((int)lane + o < 64 && bo == bb) sum = e1p_add(sum, v);
+    }
+    const uint32_t bprev = (uint32_t)__shfl_up((int)bb, 1);
+    if (live[j] && (lane == 0 || bprev != bb)) {
+      const uint32_t w0 = i - lane;
+      if (s >= w0 && e - w0 <= 64) P.sizes[b] = sum;
+      else if (s < w0) P.wpart[2 * (uint64_t)(w0 / 64)] = sum;
+      else P.wpart[2 * (uint64_t)(w0 / 64) + 1] = sum;
+    }
   }
 }
 
@@ -1713,18 +1773,28 @@ __global__ __launch_bounds__(256) void encode_e1p_blocks_kernel(EncodeParams P) 
 }
 
 __global__ __launch_bounds__(256) void encode_e1p_offsets_kernel(EncodeParams P) {
-  __shared__ uint32_t sb;
-  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-  const uint32_t i_begin = clamped_start(P, 0), i_end = clamped_start(P, P.n_blocks);
-  const bool in = i >= i_begin && i < i_end;
-  const uint32_t b = wg_block_of_item(P, in ? i : 0, &sb);  // (every thread: it holds a barrier)
-  if ((uint64_t)i >= P.it.n_items || P.e1p_flag[0] || !in) return;
-  if ((P.plans[b].step_flags >> 8) & kPlanBad) return;
-  const uint32_t s = clamped_start(P, b), n = clamped_start(P, b + 1) - s;
-  const uint32_t roff = P.erec[i] - P.pfirst[b], jj = i - s;
-  const bool head = jj % P.ri == 0;
-  const uint32_t x = head ? jj / P.ri : P.hbucket[i];
-  P.erec[i] = n > kGItems ? roff : min(roff, 0x7FFFu) | (head ? kErecHead : 0u) | (min(x, 0xFFFFu) << 16);
+  const E1pItems<kE1pPer> T = e1p_items<kE1pPer>(P);
+  if (P.e1p_flag[0]) return;
+  const uint32_t ri = P.ri;
+  uint32_t fl[kE1pPer], er[kE1pPer], pf[kE1pPer], hb[kE1pPer];
+#pragma unroll
+  for (uint32_t j = 0; j < kE1pPer; ++j) {  // every item's loads first
+    fl[j] = er[j] = pf[j] = hb[j] = 0;
+    if (T.in[j]) {
+      fl[j] = gload_pod(P.plans, T.b[j]).step_flags;
+      er[j] = gload(P.erec, T.i[j]);
+      pf[j] = gload(P.pfirst, T.b[j]);
+      hb[j] = gload(P.hbucket, T.i[j]);
+    }
+  }
+#pragma unroll
+  for (uint32_t j = 0; j < kE1pPer; ++j) {
+    if (!T.in[j] || ((fl[j] >> 8) & kPlanBad)) continue;
+    const uint32_t n = T.e[j] - T.s[j], roff = er[j] - pf[j], jj = T.i[j] - T.s[j];
+    const bool head = jj % ri == 0;
+    const uint32_t x = head ? jj / ri : hb[j];
+    P.erec[T.i[j]] = n > kGItems ? roff : min(roff, 0x7FFFu) | (head ? kErecHead : 0u) | (min(x, 0xFFFFu) << 16);
+  }
 }
 
 // The buckets of the keys E1 left (more than 16 bytes): a wave per block,
@@ -2897,8 +2967,9 @@ hipError_t launch_encode(const lsm_items& items, const uint32_t* starts, uint32_
   if (e1p) {  // batches of huge blocks: the plan item-parallel
     P.hb_sh = 1;
     if ((e = hipMemsetAsync(P.e1p_flag, 0, 4, st)) != hipSuccess) return e;
-    const dim3 igrid((uint32_t)((std::max<uint64_t>(items.n_items, n_blocks) + 255) / 256));
-    hipLaunchKernelGGL(encode_e1p_lengths_kernel, igrid, dim3(256), 0, st, P);
+    const dim3 igrid((uint32_t)((items.n_items + 256 * kE1pPer - 1) / (256 * kE1pPer)));
+    const dim3 lgrid((uint32_t)((items.n_items + 256 * kE1pLenPer - 1) / (256 * kE1pLenPer)));
+    hipLaunchKernelGGL(encode_e1p_lengths_kernel, lgrid, dim3(256), 0, st, P);
     if ((e = launch_excl_scan(P.erec, items.n_items, tiles, E1pOut{P.erec, P.pfirst + n_blocks, items.n_items},
                               st)) != hipSuccess)
       return e;
