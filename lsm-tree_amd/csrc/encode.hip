@@ -2954,6 +2954,8 @@ hipError_t launch_encode(const lsm_items& items, const uint32_t* starts, uint32_
     P.huge_pool_bytes = pool ? ws_bytes - base : 0;
     P.huge_cap = pool ? (uint32_t)cap : 0;
     if (pool && (e = hipMemsetAsync(P.huge_pool, 0, 256, st)) != hipSuccess) return e;
+    // (with a pool the E1p flag sits in the cleared pool header: one memset launch, not two)
+    if (pool) P.e1p_flag = reinterpret_cast<uint32_t*>(P.huge_pool + 128);
   }
   P.plan_bpw = plan_blocks_per_wg(items.n_items, n_blocks);
   P.hb_valid = 0;
@@ -2966,7 +2968,7 @@ hipError_t launch_encode(const lsm_items& items, const uint32_t* starts, uint32_
 #endif
   if (e1p) {  // batches of huge blocks: the plan item-parallel
     P.hb_sh = 1;
-    if ((e = hipMemsetAsync(P.e1p_flag, 0, 4, st)) != hipSuccess) return e;
+    if (!P.huge_pool && (e = hipMemsetAsync(P.e1p_flag, 0, 4, st)) != hipSuccess) return e;
     const dim3 igrid((uint32_t)((items.n_items + 256 * kE1pPer - 1) / (256 * kE1pPer)));
     const dim3 lgrid((uint32_t)((items.n_items + 256 * kE1pLenPer - 1) / (256 * kE1pLenPer)));
     hipLaunchKernelGGL(encode_e1p_lengths_kernel, lgrid, dim3(256), 0, st, P);
