@@ -123,6 +123,31 @@ def test_huge_blocks_bad_binary_index(gpu, pool):
     compare_decode(g, parsed, item_start, status)
 
 
+@pytest.mark.parametrize("pool", [True, False])
+def test_huge_blocks_long_chains(gpu, pool):
+    """A batch of ~3.7 MiB blocks (4096-step XXH3 chains) with a flipped payload
+    bit (CKSUM) deep in a block, a broken record re-sealed (PARSE) and a trailer
+    whose item count is one too many: statuses and fields as the oracle's."""
+    items = counter_items(3 * 52429, seed=13)
+    starts = np.array([0, 52429, 2 * 52429, 3 * 52429], np.uint32)
+    buf, off = pyoracle.encode_blocks(items, starts)
+    blocks = [bytes(buf[int(off[i]):int(off[i + 1])]) for i in range(3)]
+    assert min(len(b) for b in blocks) > 3_500_000
+    bad_ck = bytearray(blocks[0]); bad_ck[33 + 3_000_000] ^= 0x10
+    rec = bytearray(blocks[1][33:])
+    step, bin_off = rec[-30], int.from_bytes(rec[-25:-21], "little")
+    st = int.from_bytes(rec[bin_off + step * 2000:bin_off + step * 2001], "little")
+    rec[st] = 9  # a restart head's value type
+    late = bytearray(blocks[2][33:]); late[-4] += 1
+    tests = [blocks[0], bytes(bad_ck), pyoracle.block_write(bytes(rec), 0), pyoracle.block_write(bytes(late), 0),
+             blocks[2]]
+    buf2, off2 = pack(tests)
+    g = gpu_decode(gpu, buf2, off2, pool=pool)
+    parsed, item_start, status = pyoracle.decode_blocks(buf2, off2)
+    assert status[0] == 0 and status[1] == 4 and (status[2:4] != 0).all() and status[4] == 0, status
+    compare_decode(g, parsed, item_start, status)
+
+
 def _mixed_batch(seed=5):
     """48 blocks of 80-400 KiB between 4 KiB blocks, and corrupted copies of
     some: header checksum (HDR_CKSUM), payload bit (CKSUM), broken record
