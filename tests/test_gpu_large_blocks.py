@@ -192,6 +192,22 @@ def test_huge_blocks_mixed_batch(gpu, pool):
         compare_decode(g, parsed, item_start, status)
 
 
+@pytest.mark.parametrize("pool", [True, False])
+@pytest.mark.parametrize("ratio", [0.0, 1.33])
+def test_e1p_batch_with_small_blocks(gpu, ratio, pool):
+    """A batch planned item-parallel (E1p: >= 4 Ki items per block on average)
+    that also holds blocks of 1..300 items (the group kernel's packed record
+    words, hash indexes) and blocks crossing many 64-item waves at odd
+    offsets: bytes and offsets bit-exact against the oracle."""
+    sizes = [50, 200, 20000, 7, 1, 30000, 300, 13, 9000, 64, 65, 129]
+    items = counter_items(int(sum(sizes)), seed=21, tomb_frac=0.05)
+    starts = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint32)
+    assert sum(sizes) / len(sizes) >= 4096
+    ref_buf, ref_off = pyoracle.encode_blocks(items, starts, restart_interval=16, hash_ratio=ratio)
+    buf, off, st = _gpu_encode(gpu, items, starts, 16, ratio, pool)
+    assert (st == 0).all() and (off == ref_off).all() and buf.tobytes() == ref_buf.tobytes()
+
+
 def test_huge_blocks_pool_sizes(gpu):
     """A pool too small for every huge block of the batch: the blocks whose
     contributions do not fit take the one-workgroup path; results unchanged."""
