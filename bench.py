@@ -1144,7 +1144,10 @@ def main():
     # rank on cuda:0, the two timing reductions over gloo on the host); never
     # set by the driver, whose N > 1 runs use one GPU per rank and RCCL
     rehearse = world > 1 and os.environ.get("LSM_BENCH_REHEARSE") == "1"
-    if world > 1:
+    # LSM_BENCH_DIST=1 under torchrun --nproc-per-node 1: a one-rank RCCL group,
+    # so the N > 1 code path (RCCL init, device barriers, the two device
+    # all_reduces) runs on a one-GPU box; the result equals the N = 1 run
+    if world > 1 or os.environ.get("LSM_BENCH_DIST") == "1":
         import torch.distributed as dist
         if rehearse:
             torch.cuda.set_device(0)
@@ -1334,6 +1337,8 @@ def main():
             line["rehearsal"] = True
             line["physical_gpus"] = 1
             line["data"] += f"; REHEARSAL: {world} ranks shared one GPU, not a multi-GPU measurement"
+        if dist is not None:
+            line["process_group"] = {"backend": dist.get_backend(), "world_size": dist.get_world_size()}
         print(json.dumps(line), flush=True)
     if dist is not None:
         dist.barrier()
