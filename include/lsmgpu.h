@@ -197,7 +197,11 @@ int lsm_set_device(int device);
  * (blocks_bytes >= the bytes the batch spans), blocks larger than 72 KiB (the
  * writer's up-to-4-MiB data blocks, writer/mod.rs:193-198; full block indexes)
  * are cut into work units across the whole GPU instead of one workgroup each.
- * Same outputs and statuses either way. */
+ * Same outputs and statuses either way.  The pool is taken whenever
+ * workspace_bytes >= round_up(lsm_decode_workspace_size(n_blocks), 256) + 8704
+ * (a pool of 8 KiB past its 512-byte header), whatever buffer it came from: a
+ * caller reusing a larger arena for a batch that should stay on the
+ * one-workgroup path passes exactly lsm_decode_workspace_size(n_blocks). */
 size_t lsm_decode_workspace_size(uint32_t n_blocks);
 size_t lsm_decode_workspace_size_ex(uint32_t n_blocks, uint64_t blocks_bytes);
 int lsm_decode_blocks(const uint8_t* d_blocks, const uint64_t* d_block_off, uint32_t n_blocks,
@@ -220,7 +224,11 @@ int lsm_decode_blocks16(const uint8_t* d_blocks, const uint64_t* d_block_off, ui
 /* ---- encode ---------------------------------------------------------------
  * Encodes n_blocks blocks; block b holds items [d_block_item_start[b],
  * d_block_item_start[b+1]) (n_blocks+1 device u32; every block non-empty,
- * mod.rs:530).  Output blocks (header || payload) are packed back to back
+ * mod.rs:530).  A d_block_item_start that is not strictly increasing is a
+ * caller error: it gets LSM_BAD_ARG for some or all blocks of the batch (the
+ * blocks planned together with the offending ones; every block when the batch
+ * is planned item-parallel, >= 4 Ki items per block on average), so a caller
+ * treats any LSM_BAD_ARG block as failing the whole batch.  Output blocks (header || payload) are packed back to back
  * into d_out; d_block_off (n_blocks+1 device u64) receives their offsets.
  * d_out needs lsm_encode_bound(...) bytes (status LSM_OVERFLOW otherwise).
  * d_workspace: lsm_encode_workspace_size(n_items, n_blocks) bytes, or

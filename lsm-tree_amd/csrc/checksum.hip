@@ -275,21 +275,26 @@ __device__ __forceinline__ bool batch_state_ok(const Xxh3Stream* st, const uint6
 // workspace (total_len below the real byte count) is rejected whole.
 __global__ __launch_bounds__(1024) void xxh3_batch_plan_kernel(const Xxh3Stream* __restrict__ states, uint32_t n,
                                                                const uint64_t* __restrict__ off, uint64_t cap_blocks,
-                                                               uint64_t* __restrict__ bpre, int32_t* __restrict__ status) {
+                                                               uint64_t total_len, uint64_t* __restrict__ bpre,
+                                                               int32_t* __restrict__ status) {
   __shared__ uint64_t wsum[16];
   __shared__ uint64_t carry_s;
+  __shared__ unsigned long long bytes_s;
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  if (tid == 0) carry_s = 0;
+  if (tid == 0) carry_s = 0, bytes_s = 0;
   __syncthreads();
   for (uint32_t c = 0; c < n; c += 1024) {
     const uint32_t i = c + tid;
-    uint64_t nb = 0;
+    uint64_t nb = 0, len = 0;
     if (i < n) {
       const bool ok = batch_state_ok(states + i, off, i);
-      nb = ok ? stream_blocks(states[i].pending, off[i + 1] - off[i]) : 0;
+      len = ok ? off[i + 1] - off[i] : 0;
+      nb = ok ? stream_blocks(states[i].pending, len) : 0;
       status[i] = ok ? (int32_t)LSM_OK : (int32_t)LSM_BAD_ARG;
     }
     const uint64_t incl = wave_incl_scan_u64(nb);
+    const uint64_t lsum = wave_incl_scan_u64(len);
+    if (lane == 63) atomicAdd(&bytes_s, (unsigned long long)lsum);
     if (lane == 63) wsum[wave] = incl;
     __syncthreads();
     uint64_t base = carry_s, tot = 0;
@@ -303,7 +308,9 @@ __global__ __launch_bounds__(1024) void xxh3_batch_plan_kernel(const Xxh3Stream*
     __syncthreads();
   }
   if (tid == 0) bpre[n] = carry_s;
-  if (carry_s > cap_blocks) {  // (uniform) a caller error: nothing is updated
+  // (uniform) a caller error: the ranges hold more bytes than total_len (or
+  // more KiB blocks than the workspace was sized for): nothing is updated
+  if (bytes_s > total_len || carry_s > cap_blocks) {
     for (uint32_t i = tid; i < n; i += 1024) status[i] = LSM_BAD_ARG;
     if (tid == 0) bpre[n] = 0;
   }
@@ -390,7 +397,8 @@ hipError_t launch_xxh3_stream_update_batch(Xxh3Stream* states, uint32_t n, const
   uint64_t* bpre = (uint64_t*)ws;
   uint64_t* contrib = (uint64_t*)((uint8_t*)ws + ((8 * ((size_t)n + 1) + 255) & ~(size_t)255));
   const uint64_t cap = batch_cap_blocks(n, total_len);
-  hipLaunchKernelGGL(xxh3_batch_plan_kernel, dim3(1), dim3(1024), 0, s, states, n, off, cap, bpre, status);
+  hipLaunchKernelGGL(xxh3_batch_plan_kernel, dim3(1), dim3(1024), 0, s, states, n, off, cap, total_len, bpre,
+                     status);
   const uint64_t wgs = (cap + kBatchWgBlocks - 1) / kBatchWgBlocks;
   if (wgs > 0x7FFFFFFFull) return hipErrorInvalidValue;
   hipLaunchKernelGGL(xxh3_batch_contrib_kernel, dim3((uint32_t)wgs), dim3(256), 0, s, states, n, data, off, bpre,

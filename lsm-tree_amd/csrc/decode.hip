@@ -886,7 +886,7 @@ struct HugeLayout {
   uint64_t rest;  // pool bytes after the fixed part
   bool ok;
 };
-__host__ __device__ __forceinline__ uint64_t huge_fixed_bytes(uint64_t n) {
+__host__ __device__ constexpr uint64_t huge_fixed_bytes(uint64_t n) {
   return (256 + 24 * (n + 1) + sizeof(HugeRec) * n + 255) & ~255ULL;
 }
 __device__ __forceinline__ HugeLayout huge_layout(const DecodeParams& P, uint32_t n) {
@@ -1801,6 +1801,7 @@ hipError_t launch_decode(const DecodeParams& P0, void* ws, size_t ws_bytes, hipS
   P.defer3_list = (uint32_t*)(dws + 256 + 2 * defer_bytes(P.n_blocks));
   const size_t base = decode_workspace_size(P.n_blocks);
   const size_t pool0 = (base + 255) & ~(size_t)255;
+  static_assert(huge_fixed_bytes(1) + 64 * 128 == 8704, "the threshold lsmgpu.h documents");
   P.huge_pool = ws_bytes >= pool0 + huge_fixed_bytes(1) + 64 * 128 ? (uint8_t*)ws + pool0 : nullptr;
   P.huge_pool_bytes = P.huge_pool ? ws_bytes - pool0 : 0;
   hipError_t e = hipMemsetAsync(dws, 0, 16, st);

@@ -286,13 +286,16 @@ class Decoder:
 
     def workspace(self, n_blocks, blocks_bytes=0):
         """Workspace for n_blocks; with blocks_bytes (the batch buffer's size) it
-        includes the pool that spreads blocks > 72 KiB over the whole GPU."""
+        includes the pool that spreads blocks > 72 KiB over the whole GPU.  The
+        cached buffer is returned viewed at exactly the size this call needs:
+        the library turns the pool on from the size it is handed (lsmgpu.h), so
+        bytes grown by an earlier pool call must not reach a pool=False call."""
         torch = _torch()
         need = (lib().lsm_decode_workspace_size_ex(n_blocks, blocks_bytes) if blocks_bytes
                 else lib().lsm_decode_workspace_size(n_blocks))
         if self.ws is None or self.ws.numel() < need:
             self.ws = torch.empty(max(need, 256), dtype=torch.uint8, device=self.device)
-        return self.ws
+        return self.ws[:need]
 
     def alloc_outputs(self, item_cap, n_blocks, fields=None, compact=False):
         torch = _torch()

@@ -167,3 +167,17 @@ def test_stream_batch_bad_states(gpu):
     assert list(st) == [10, 10, 10, 10]
     got2 = ws.checksums()
     assert got2[0] == got[0] and got2[2] == got[2] and got2[3] == got[3]
+    # ranges only a few bytes over total_len (within the workspace's KiB-block
+    # slack): still the whole call is rejected, as lsmgpu.h states
+    for total in (19997, 19999):
+        st = ws.write(d, off2, total).cpu().numpy()
+        assert list(st) == [10, 10, 10, 10], total
+        assert ws.checksums() == got2
+    # one state, total_len 0, a 2000-byte range (the advisor's example)
+    one = gpu.ChecksummedWriterSet(1)
+    off1 = torch.tensor([0, 2000], dtype=torch.int64, device="cuda")
+    assert list(one.write(d, off1, 0).cpu().numpy()) == [10]
+    assert (lambda c: (c[1] << 64) | c[0])(one.checksums()[0]) == pyoracle.xxh3_128(b"")
+    # exactly total_len bytes: accepted
+    st = ws.write(d, off2, 20000).cpu().numpy()
+    assert list(st) == [0, 10, 0, 0]

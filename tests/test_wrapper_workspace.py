@@ -1,0 +1,79 @@
+"""Host-side checks of the ctypes mirror's workspace handling (no GPU: the
+library is replaced by a recorder; the size functions are the real ones).
+
+lsm_decode_blocks takes the huge-block pool whenever the workspace it is
+handed is large enough (include/lsmgpu.h), so a Decoder reused across calls
+must hand a pool=False call exactly lsm_decode_workspace_size(n), however
+large an earlier pool=True call grew its cached buffer."""
+import ctypes as C
+
+import pytest
+import torch
+
+import lsmgpu
+
+
+class _Recorder:
+    def __init__(self, real):
+        self.real = real
+        self.calls = []
+
+    def __getattr__(self, name):
+        if name.startswith("lsm_decode_workspace_size") or name.startswith("lsm_encode_workspace_size") \
+                or name == "lsm_encode_bound":
+            return getattr(self.real, name)
+
+        def rec(*args):
+            self.calls.append((name, args))
+            return 0
+        return rec
+
+
+@pytest.fixture
+def fake(monkeypatch):
+    real = lsmgpu.lib()
+    r = _Recorder(real)
+    monkeypatch.setattr(lsmgpu, "lib", lambda: r)
+    monkeypatch.setattr(lsmgpu, "_torch", lambda: torch)
+    monkeypatch.setattr(lsmgpu, "_stream", lambda s: C.c_void_p(0))
+    return r
+
+
+def _ws_arg(call):
+    name, args = call
+    assert name == "lsm_decode_blocks"
+    return args[9], args[8]  # workspace_bytes, workspace pointer
+
+
+def test_decoder_pool_then_no_pool(fake):
+    n = 100
+    blocks = torch.zeros(n * 300 * 1024, dtype=torch.uint8)  # 300 KiB mean: the pool would pay
+    off = torch.zeros(n + 1, dtype=torch.int64)
+    d = lsmgpu.Decoder("cpu")
+    out = d.alloc_outputs(16, n)
+    d.decode(blocks, off, n, out, 16, pool=True)
+    d.decode(blocks, off, n, out, 16, pool=False)
+    d.decode(blocks, off, n, out, 16)  # default: the mean block size picks the pool
+    base = fake.real.lsm_decode_workspace_size(n)
+    full = fake.real.lsm_decode_workspace_size_ex(n, blocks.numel())
+    got = [_ws_arg(c)[0] for c in fake.calls]
+    assert got == [full, base, full]
+    threshold = ((base + 255) & ~255) + 8704  # lsmgpu.h: the pool threshold
+    assert base < threshold <= full
+    # the cached buffer is reused (one allocation), only its view changes
+    assert len({_ws_arg(c)[1].value for c in fake.calls}) == 1
+
+
+def test_encoder_passes_exact_workspace(fake):
+    n_items, n_blocks = 64, 4
+    items = {"keys": torch.zeros(64 * 16 + 64, dtype=torch.uint8),
+             "key_off": torch.arange(n_items + 1, dtype=torch.int64) * 16,
+             "vals": torch.zeros(64 * 64 + 64, dtype=torch.uint8),
+             "val_off": torch.arange(n_items + 1, dtype=torch.int64) * 64,
+             "seqno": torch.zeros(n_items, dtype=torch.int64), "vtype": torch.zeros(n_items, dtype=torch.uint8)}
+    starts = torch.arange(0, n_items + 1, 16, dtype=torch.int32)
+    e = lsmgpu.Encoder("cpu")
+    e.encode(items, starts, n_blocks, pool=True)
+    e.encode(items, starts, n_blocks, pool=False)
+    ws = [args[9] for name, args in fake.calls if name == "lsm_encode_blocks"]
+    assert ws[1] == fake.real.lsm_encode_workspace_size(n_items, n_blocks) < ws[0]
