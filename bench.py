@@ -56,6 +56,8 @@ PARSED_BYTES_PER_ITEM = 8 + 4 + 4 + 4 + 2 + 2 + 1  # seqno key_off val_off val_l
 PER_BLOCK_OUT = 8  # item_start u32 + status i32
 # encode input per item as the ABI reads it: key + value bytes, seqno u64, vtype u8, key_off / val_off u64
 ENC_IN_PER_ITEM = 8 + 1 + 8 + 8
+# the same as SURVEY §8(d) counts it: 4-byte key / value offsets
+ENC_IN_PER_ITEM_SURVEY = 8 + 1 + 4 + 4
 DATA_FIELDS = ["seqno", "key_off", "val_off", "val_len", "key_len", "prefix_len", "vtype"]
 FIELD_NP = {"seqno": "uint64", "key_off": "uint32", "val_off": "uint32", "val_len": "uint32", "key_len": "uint16",
             "prefix_len": "uint16", "vtype": "uint8", "handle_off": "uint64"}
@@ -1118,6 +1120,110 @@ def roofline_entry(name, alg_bytes, ms, ceil, traffic_kernel, nb):
             "practical_peak": ceil, "frac_of_copy_ceiling": round(achieved / ceil["copy_GBps"], 4) if ceil else None}
 
 
+def load_trace_ms(kernels, n_blocks):
+    """Mean duration (ms) of one launch of each (kernel, workgroups) pair, summed,
+    from the newest committed rocprofv3 kernel-trace summary
+    (profiles/*_bench_kernels_by_grid.csv, scripts/trace_by_grid.py) of a bench
+    run over the same batch size; None when no profile has every pair."""
+    import csv
+    best, src = None, None
+    for p in sorted((ROOT / "profiles").glob("*_bench_kernels_by_grid.csv"), key=lambda q: q.stat().st_mtime):
+        try:
+            rows = list(csv.DictReader(p.open()))
+        except Exception:
+            continue
+        by = {(r["kernel"], int(r["workgroups"])): r for r in rows}
+        if not all(k in by for k in kernels):
+            continue
+        unit = 1e-3 if "avg_us" in rows[0] else 1e-6
+        col = "avg_us" if "avg_us" in rows[0] else "avg_ns"
+        best, src = sum(float(by[k][col]) * unit for k in kernels), p.name
+    return (round(best, 4), src) if best is not None else (None, None)
+
+
+def encode_roofline(name, enc_ms, key_val, n_items, nb, total_bytes, ceil, trace_kernels=None):
+    """Encode roofline: `frac` on the ABI's input bytes (u64 key / value offsets:
+    25 B of SoA per item beside the key and value bytes), `frac_survey` on SURVEY
+    §8(d)'s (4-byte offsets: 17 B per item).  kernel_ms is the whole
+    lsm_encode_blocks call timed with HIP events on its launch stream (plan +
+    scan + write kernels); kernel_ms_trace the same kernels' mean launch
+    durations from the committed rocprofv3 trace of a bench run, when one
+    exists."""
+    enc_alg = key_val + n_items * ENC_IN_PER_ITEM + 4 * (nb + 1) + total_bytes + 8 * (nb + 1) + 4 * nb
+    enc_alg_survey = key_val + n_items * ENC_IN_PER_ITEM_SURVEY + total_bytes
+    r = roofline_entry(name, enc_alg, enc_ms, ceil, "lsm_encode_blocks", nb)
+    r["kernel_ms_source"] = "HIP events around the whole lsm_encode_blocks call on its launch stream"
+    r["alg_bytes_survey"] = enc_alg_survey
+    r["frac_survey"] = round(enc_alg_survey / (enc_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
+    if trace_kernels:
+        tms, tsrc = load_trace_ms(trace_kernels, nb)
+        if tms:
+            r["kernel_ms_trace"] = tms
+            r["kernel_ms_trace_source"] = tsrc
+            r["frac_trace"] = round(enc_alg / (tms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
+            r["frac_survey_trace"] = round(enc_alg_survey / (tms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
+    return r
+
+
+def bench_random_keys(torch, lsmgpu, steps, rank, threads, ceil, nb=1 << 20):
+    """SURVEY §8(d) config 2 variant G2: the headline shape with random 16 B
+    keys (sorted), 64 B values, 1 M x 4 KiB blocks (~4466 B each: 0-4 key
+    bytes shared with the restart head).  Encode and decode timed alone, each
+    with its roofline; every block checked against the oracle."""
+    check_cut_rule(lsmgpu, 52, 16, 64)
+    items, starts, n = make_workload(torch, lsmgpu, nb, seed=0x5EED0012 + rank, kind="random")
+    enc_ctx = lsmgpu.Encoder()
+    enc = enc_ctx.encode(items, starts, nb)
+    torch.cuda.synchronize()
+    total = int(enc["block_off"][nb].item())
+    e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
+    enc_ctx.encode(items, starts, nb, out=enc)
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(steps):
+        enc_ctx.encode(items, starts, nb, out=enc)
+    e1.record()
+    torch.cuda.synchronize()
+    enc_ms = e0.elapsed_time(e1) / steps
+    dec_ms, out = time_decode(torch, lsmgpu, enc["buf"], enc["block_off"], nb, n, steps)
+    dec = lsmgpu.Decoder(enc["buf"].device)
+    out2 = dec.alloc_outputs(n, nb)
+    kdec = lambda: dec.decode(enc["buf"], enc["block_off"], nb, out2, n,  # noqa: E731
+                              tuning=(0, 0, 0, lsmgpu.DECODE_ITEM_START_VALID))
+    out2["item_start"].copy_(out["item_start"])
+    kdec()
+    torch.cuda.synchronize()
+    e0.record()
+    for _ in range(steps):
+        kdec()
+    e1.record()
+    torch.cuda.synchronize()
+    kdec_ms = e0.elapsed_time(e1) / steps
+    ref_buf, ref_off = check_encode_all(torch, items, starts, enc, nb, n, threads)
+    check_decode_all(out, ref_buf, ref_off, nb, threads)
+    check_decode_all(out2, ref_buf, ref_off, nb, threads)
+    key_val = int(items["key_off"][n].item()) + int(items["val_off"][n].item())
+    dec_alg = total + n * PARSED_BYTES_PER_ITEM + nb * PER_BLOCK_OUT
+    r_dec = roofline_entry("decode_blocks_kernel (item_start precomputed)", dec_alg, kdec_ms, ceil,
+                           "decode_blocks_kernel", nb)
+    r_dec["traffic"] = r_dec["traffic_source"] = None  # (the committed PMC summaries are of the G1 batch)
+    r_dec["read_only_frac"] = round(total / (kdec_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
+    r_enc = encode_roofline("lsm_encode_blocks (encode_plan_wave_kernel + scan + encode_group_kernel)", enc_ms,
+                            key_val, n, nb, total, ceil)
+    r_enc["traffic"] = r_enc["traffic_source"] = None
+    res = {"workload": "SURVEY §8(d) config 2 variant G2: 1 M x 4 KiB blocks, random sorted 16 B keys, 64 B values, "
+                       "seqno 63, restart interval 16",
+           "blocks": nb, "items": n, "bytes": total,
+           "encode_ms": round(enc_ms, 4), "encode_GiB_per_s": round(total / (enc_ms * 1e-3) / 2 ** 30, 3),
+           "decode_ms": round(dec_ms, 4), "decode_kernel_ms": round(kdec_ms, 4),
+           "decode_GiB_per_s": round(total / (dec_ms * 1e-3) / 2 ** 30, 3),
+           "round_trip_GiB_per_s": round(total / ((enc_ms + dec_ms) * 1e-3) / 2 ** 30, 3),
+           "roofline_decode": r_dec, "roofline_encode": r_enc, "oracle_checked_blocks": nb}
+    del items, enc, out, out2, ref_buf
+    torch.cuda.empty_cache()
+    return res
+
+
 # --------------------------------------------------------------------- main
 def main():
     ap = argparse.ArgumentParser()
@@ -1252,12 +1358,19 @@ def main():
     dec_alg = total_bytes + n_items * PARSED_BYTES_PER_ITEM + nb * PER_BLOCK_OUT
     dec16_alg = total_bytes + n_items * 19 + nb * PER_BLOCK_OUT
     key_val = int(items["key_off"][n_items].item()) + int(items["val_off"][n_items].item())
-    enc_alg = key_val + n_items * ENC_IN_PER_ITEM + 4 * (nb + 1) + total_bytes + 8 * (nb + 1) + 4 * nb
     r_dec = roofline_entry("decode_blocks_kernel (item_start precomputed)", dec_alg, kdec_ms, ceil,
                            "decode_blocks_kernel", nb)
+    r_dec["kernel_ms_source"] = "HIP events around lsm_decode_blocks with item_start precomputed (the decode kernel alone)"
     r_dec["read_only_frac"] = round(total_bytes / (kdec_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
-    r_enc = roofline_entry("lsm_encode_blocks (encode_plan_wave_kernel + scan + encode_group_kernel)", enc_alg, enc_ms,
-                           ceil, "lsm_encode_blocks", nb)
+    tms, tsrc = load_trace_ms([("decode_blocks_kernel<true, false>", (nb + 53) // 54)], nb) if nb == 1 << 20 \
+        else (None, None)
+    if tms:
+        r_dec["kernel_ms_trace"], r_dec["kernel_ms_trace_source"] = tms, tsrc
+        r_dec["read_only_frac_trace"] = round(total_bytes / (tms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
+    r_enc = encode_roofline("lsm_encode_blocks (encode_plan_wave_kernel + scan + encode_group_kernel)", enc_ms,
+                            key_val, n_items, nb, total_bytes, ceil,
+                            [("encode_plan_wave_kernel<false>", (nb + 127) // 128),
+                             ("encode_group_kernel<false, false, false>", (nb + 31) // 32)] if nb == 1 << 20 else None)
     dominant = r_enc if enc_ms >= kdec_ms else r_dec
 
     extra = {}
@@ -1288,6 +1401,7 @@ def main():
         if world == 1:
             extra["large_blocks"] = bench_large_blocks(torch, lsmgpu, threads)
             extra["hash_index"] = bench_hash_index(torch, lsmgpu, max(3, args.steps // 4), threads)
+            extra["random_keys"] = bench_random_keys(torch, lsmgpu, max(3, args.steps // 4), rank, threads, ceil)
 
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu and ref_buf is not None:
