@@ -107,7 +107,70 @@ __global__ __launch_bounds__(256) void soa_kernel(uint8_t* __restrict__ out, uin
   }
 }
 
+// FETCH_SIZE / WRITE_SIZE calibration for the encode kernels' narrow access
+// shapes (the guide calibrates only 16 B/lane streams): each mode touches a
+// known number of distinct bytes of `buf` once, in one access shape.
+//   0  u64 per lane, lane-contiguous                  (E2 item fields)
+//   1  u64, lane t reads elements 2t, 2t+1, 2t+2      (E1 key / value offsets)
+//   2  u64, lane t reads elements 2t, 2t+1            (E1 seqnos)
+//   3  u8, lane t reads bytes 2t, 2t+1                (E1 value types)
+//   4  u8 per lane, lane-contiguous                   (E2 value types)
+//   5  u32 per lane, lane-contiguous                  (E2 erec)
+//   6  16 B per lane, lane-contiguous                 (the guide's calibrated shape)
+//   7  u32 stores, lane t writes elements 2t, 2t+1    (E1 erec)
+//   8  u32 stores per lane, lane-contiguous
+// n = elements of the mode's type; the sum goes to sink[0] (reads kept live).
+__global__ __launch_bounds__(256) void fetch_calib_kernel(const uint8_t* __restrict__ buf, uint8_t* __restrict__ wbuf,
+                                                          uint64_t n, int mode, uint32_t* __restrict__ sink) {
+  const uint64_t t = (uint64_t)blockIdx.x * 256 + threadIdx.x;
+  uint64_t acc = 0;
+  const uint64_t* b64 = reinterpret_cast<const uint64_t*>(buf);
+  switch (mode) {
+    case 0:
+      if (t < n) acc = b64[t];
+      break;
+    case 1:
+      if (2 * t < n) acc = b64[2 * t] + b64[min(2 * t + 1, n - 1)] + b64[min(2 * t + 2, n - 1)];
+      break;
+    case 2:
+      if (2 * t < n) acc = b64[2 * t] + b64[min(2 * t + 1, n - 1)];
+      break;
+    case 3:
+      if (2 * t < n) acc = buf[2 * t] + buf[min(2 * t + 1, n - 1)];
+      break;
+    case 4:
+      if (t < n) acc = buf[t];
+      break;
+    case 5:
+      if (t < n) acc = reinterpret_cast<const uint32_t*>(buf)[t];
+      break;
+    case 6:
+      if (t < n) {
+        const u32x4 v = reinterpret_cast<const u32x4*>(buf)[t];
+        acc = v.x ^ v.y ^ v.z ^ v.w;
+      }
+      break;
+    case 7:
+      if (2 * t < n) {
+        reinterpret_cast<uint32_t*>(wbuf)[2 * t] = (uint32_t)t;
+        if (2 * t + 1 < n) reinterpret_cast<uint32_t*>(wbuf)[2 * t + 1] = (uint32_t)t + 1;
+      }
+      break;
+    case 8:
+      if (t < n) reinterpret_cast<uint32_t*>(wbuf)[t] = (uint32_t)t;
+      break;
+  }
+  if (acc == 0x9E3779B97F4A7C15ULL) sink[0] = (uint32_t)acc;  // keeps the reads live
+}
+
 }  // namespace
+
+extern "C" int lsm_ceiling_fetch_calib(const void* buf, void* wbuf, uint64_t n, int mode, uint32_t* sink, void* stream) {
+  const uint64_t threads = (mode == 1 || mode == 2 || mode == 3 || mode == 7) ? (n + 1) / 2 : n;
+  hipLaunchKernelGGL(fetch_calib_kernel, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, (hipStream_t)stream,
+                     (const uint8_t*)buf, (uint8_t*)wbuf, n, mode, sink);
+  return hipGetLastError() == hipSuccess ? 0 : 11;
+}
 
 extern "C" int lsm_ceiling_soa(void* out, uint64_t n_items, int mode, void* stream) {
   if (((uintptr_t)out & 15) || (n_items & 15)) return 10;
