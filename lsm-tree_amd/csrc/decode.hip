@@ -36,10 +36,7 @@ namespace lsmgpu {
 // (16 blocks x 80 B of block metadata: the LDS this frees lets the stage hold
 // two 17 KB blocks of the 16 KiB random-key class, or nine 4 KiB blocks,
 // inside the 40 KiB that keeps four workgroups per CU)
-#ifndef LSM_DEC_MAX_GROUP
-#define LSM_DEC_MAX_GROUP 16
-#endif
-constexpr uint32_t kMaxGroup = LSM_DEC_MAX_GROUP;  // blocks per staged group
+constexpr uint32_t kMaxGroup = 16;  // blocks per staged group
 // Internal status: the block needs the general path (index block, a record
 // shape the straight-line parsers do not take, a block larger than the
 // stage).  The group kernel lists it for decode_big_kernel, which hands on
@@ -558,10 +555,7 @@ typedef const __attribute__((address_space(1))) void gbl_void_t;
 // than the stage.  (Half the stage measured slower: the 17 KB blocks of the
 // 16 KiB random-key class run at 0.82 TB/s through the big-block kernel, one
 // block per iteration, and at 1.42 TB/s here, one block per group.)
-#ifndef LSM_LONE_DIV
-#define LSM_LONE_DIV 1
-#endif
-__device__ __forceinline__ uint32_t lone_bytes(const DecodeParams& P) { return P.stage_bytes / LSM_LONE_DIV; }
+__device__ __forceinline__ uint32_t lone_bytes(const DecodeParams& P) { return P.stage_bytes; }
 
 // A group: the longest run of consecutive blocks from b that fits the stage
 // (k == 0: block b alone is too large and takes the direct path).  Lane j of
@@ -834,17 +828,11 @@ __global__ __launch_bounds__(kBigWaves * kWave) void decode_deferred_staged_kern
 //          merge, the checksum compare and the status
 // A block whose header fails, or that no longer fits the pool, goes to the
 // general path (defer2) as before: statuses and outputs are the same on both.
-#ifndef LSM_HUGE_WIN_KIB
-#define LSM_HUGE_WIN_KIB 32
-#endif
-constexpr uint32_t kHugeWin = LSM_HUGE_WIN_KIB * 1024;  // span bytes per unit
-#ifndef LSM_HUGE_OVL
-#define LSM_HUGE_OVL (8 * 1024 - 256)
-#endif
-constexpr uint32_t kHugeOverlap = LSM_HUGE_OVL;  // staged past the window (intervals that straddle it)
+constexpr uint32_t kHugeWin = 32 * 1024;  // span bytes per unit
+constexpr uint32_t kHugeOverlap = ((8 * 1024 - 256));  // staged past the window (intervals that straddle it)
 constexpr uint32_t kHugeStage = kHugeWin + kHugeOverlap;
 constexpr uint32_t kHugeMaxIv = 512;                   // intervals per window for phase A / B (else thread walks)
-constexpr uint32_t kHugeTile = 32 * LSM_HUGE_WIN_KIB;  // items per window for phase A / B
+constexpr uint32_t kHugeTile = 32 * 32;  // items per window for phase A / B
 constexpr uint32_t kHugeBix = kHugeStage + kStagePad;  // LDS: the window's binary-index entries
 constexpr uint32_t kHugeMeta = kHugeBix + 4 * (kHugeMaxIv + 4);
 constexpr uint32_t kHugeOwner = kHugeMeta + 80;
@@ -1019,10 +1007,7 @@ __global__ __launch_bounds__(1024) void decode_huge_plan_kernel(DecodeParams P) 
 //               it is the block's critical path)
 // Blocks larger than the stage, with more items than kBigGTile, index blocks
 // and rare record shapes go on to the general path (defer2 list).
-#ifndef LSM_BIG_WAVES
-#define LSM_BIG_WAVES 8
-#endif
-constexpr uint32_t kBigGWaves = LSM_BIG_WAVES;
+constexpr uint32_t kBigGWaves = 8;
 constexpr uint32_t kBigGStage = 69376;  // 67.75 KiB: a 64 KiB-target block of 69.2 KB plus alignment
 constexpr uint32_t kBigGSlot = kBigGStage + kStagePad;
 constexpr uint32_t kBigGTile = 832;
@@ -1425,10 +1410,7 @@ __global__ __launch_bounds__(256) void decode_huge_kernel(DecodeParams P) {
       HUGE_PHASE(2);
       // phase A (serial LDS walks: latency) on wave 0, the contributions (VALU) on the
       // other waves meanwhile; without phase A on all four
-#ifndef LSM_HUGE_SPLIT
-#define LSM_HUGE_SPLIT 1
-#endif
-      const bool split = LSM_HUGE_SPLIT && fast;
+      const bool split = fast;
       if (fast && (split ? wave == 0 : true))
         phase_a<true>(stage, wmeta, owner, rec, split ? 0 : wave * kWave, split ? kWave : 4 * kWave, niv, kHugeTile);
       HUGE_PHASE(3);
@@ -1534,26 +1516,12 @@ __global__ __launch_bounds__(64) void decode_huge_chain_kernel(DecodeParams P) {
 // pa rotates with the group index so the serial walk lands on each SIMD in
 // turn.  Phase A needs only the trailer, not the checksum, so it runs
 // concurrently with the hash; statuses merge in oracle order at the end.
-#ifndef LSM_DEC_WAVES
-#define LSM_DEC_WAVES 4
-#endif
-#ifndef LSM_DEC_WPE
-#define LSM_DEC_WPE 3
-#endif
-constexpr uint32_t kGroupWaves = LSM_DEC_WAVES;
-#ifndef LSM_PRIO_A
-#define LSM_PRIO_A 0
-#endif
-#ifndef LSM_PRIO_H
-#define LSM_PRIO_H 0
-#endif
-constexpr int kPrioA = LSM_PRIO_A;  // s_setprio of the phase-A wave
-constexpr int kPrioH = LSM_PRIO_H;  // s_setprio of a wave hashing one whole block
+constexpr uint32_t kGroupWaves = 4;
 // 17-bit record descriptors for stages of 64 KiB and more (two 8-wave workgroups per CU)
 constexpr bool kDecWide = kDefaultStageBytes >= 65536;
 
 template <bool kAllFields, bool kCompact>
-__global__ __launch_bounds__(kGroupWaves * kWave) __attribute__((amdgpu_waves_per_eu(LSM_DEC_WPE))) void decode_blocks_kernel(DecodeParams P) {
+__global__ __launch_bounds__(kGroupWaves * kWave) __attribute__((amdgpu_waves_per_eu(3))) void decode_blocks_kernel(DecodeParams P) {
   // LDS: [meta: G x 80 B][rec: u64 per item + 1 scratch][owner: u8 per item][staged bytes + pad][secret]
 #if defined(LSM_DIAG) && !defined(LSM_DIAG_NOTIME)
   uint64_t t_last = __builtin_amdgcn_s_memtime(), ph[16] = {};
@@ -1660,9 +1628,7 @@ __global__ __launch_bounds__(kGroupWaves * kWave) __attribute__((amdgpu_waves_pe
       // payload checksums (not when verified upstream: the LZ4 path checks the stored bytes)
       const bool hash = !(kDiagBuild && (P.flags & kDiagSkipHash)) && !(P.flags & LSM_DECODE_PAYLOAD_VERIFIED);
       if (role < nA) {
-        if (kPrioA) __builtin_amdgcn_s_setprio(kPrioA);  // the serial walk is the group's critical path
         phase_a<kDecWide>(stage, meta, owner, rec, role * kWave, nA * kWave, total, P.tile_items);
-        if (kPrioA) __builtin_amdgcn_s_setprio(0);
         DEC_ROLE(8);
       } else if (hash && k <= kGroupWaves - nA) {
         // few (large) blocks: one wave per block, the 64-lane XXH3 (1 KiB per step)
@@ -1670,9 +1636,7 @@ __global__ __launch_bounds__(kGroupWaves * kWave) __attribute__((amdgpu_waves_pe
         if (jb < k && meta[jb].hdr_st == ST_OK) {
           const uint32_t hb = meta[jb].hb, plen = meta[jb].len - kHdrLen;
           uint64_t lo, hi;
-          if (kPrioH) __builtin_amdgcn_s_setprio(kPrioH);
           xxh3_128_wave(stage, hb + kHdrLen, plen, ls, lo, hi);
-          if (kPrioH) __builtin_amdgcn_s_setprio(0);
           const bool hck = header_cksum_ok(stage, hb);
           if (lane == 0) {
             meta[jb].ck_bad = lo != meta[jb].ck_lo || hi != meta[jb].ck_hi;

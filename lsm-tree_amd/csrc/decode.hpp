@@ -14,16 +14,9 @@ namespace lsmgpu {
 // of LDS per workgroup, four workgroups per CU.  Measured against 48 / 32 KiB
 // / 448: configs[1] equal within 1 %, configs[4]'s 16 KiB random class 0.99 ->
 // 0.65 ms (profiles/r02s5_decode_stage_ab.txt).
-#ifndef LSM_DEC_STAGE
-#define LSM_DEC_STAGE 34560
-#define LSM_DEC_TILE 480
-#endif
-#ifndef LSM_DEC_BPW
-#define LSM_DEC_BPW 54
-#endif
-constexpr uint32_t kDefaultBlocksPerWave = LSM_DEC_BPW;
-constexpr uint32_t kDefaultStageBytes = LSM_DEC_STAGE;
-constexpr uint32_t kDefaultTileItems = LSM_DEC_TILE;
+constexpr uint32_t kDefaultBlocksPerWave = 54;
+constexpr uint32_t kDefaultStageBytes = 34560;
+constexpr uint32_t kDefaultTileItems = 480;
 
 struct DecodeParams {
   const uint8_t* blocks;

@@ -609,12 +609,9 @@ __device__ __forceinline__ void xxh3_kib_contribs_b(const uint8_t* base, uint32_
   }
 }
 
-#ifndef LSM_KIB_BATCH
-#define LSM_KIB_BATCH 4  // KiB blocks per reduce-scatter (1: a quad_group_sum64 pair per block)
-#endif
 // XXH3-128 long path split across the waves of a workgroup.  The per-KiB
 // contributions of the accumulate loop do not depend on the accumulators, so
-// wave w of nw reduces runs of LSM_KIB_BATCH KiB blocks (starting at B w,
+// wave w of nw reduces runs of B = 4 consecutive KiB blocks (starting at B w,
 // B (w + nw), ...) into contrib[8 n ..]; after a workgroup barrier one wave
 // runs the serial scramble chain over them and the tail
 // (xxh3_128_wave_finish).  len > 240; kLds: base is LDS.  With `ready`, KiB block n's
@@ -628,8 +625,7 @@ __device__ __forceinline__ void xxh3_kib_contribs(const uint8_t* base, uint32_t 
   const int q = lane & 3, s = lane >> 2;
   const uint64_t k0 = ls->acc[s + 2 * q], k1 = ls->acc[s + 2 * q + 1];
   const uint32_t nb_blocks = (len - 1) / 1024;
-#if LSM_KIB_BATCH > 1
-  constexpr uint32_t B = LSM_KIB_BATCH;
+  constexpr uint32_t B = 4;
   for (uint32_t n0 = B * w; n0 < nb_blocks; n0 += B * nw) {
     const uint32_t cnt = min(B, nb_blocks - n0);
     xxh3_kib_contribs_b<B, kLds>(base, pos, n0, cnt, k0, k1, contrib);
@@ -638,36 +634,6 @@ __device__ __forceinline__ void xxh3_kib_contribs(const uint8_t* base, uint32_t 
       if ((uint32_t)lane < cnt) __hip_atomic_store(&ready[n0 + lane], tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
     }
   }
-#else
-  // two KiB blocks per step (both windows read before either is reduced)
-  for (uint32_t n = w; n < nb_blocks; n += 2 * nw) {
-    const bool two = n + nw < nb_blocks;
-    const Win16 wa = read_win16(base, pos + n * 1024 + 16 * lane);
-    const Win16 wb = read_win16(base, pos + (two ? n + nw : n) * 1024 + 16 * lane);  // (no branch: no wait between)
-    uint64_t c0 = 0, c1 = 0, d0 = 0, d1 = 0;
-    stripe_part(wa, k0, k1, c0, c1);
-    stripe_part(wb, k0, k1, d0, d1);
-    c0 = quad_group_sum64(c0);
-    c1 = quad_group_sum64(c1);
-    d0 = quad_group_sum64(d0);
-    d1 = quad_group_sum64(d1);
-    if (lane < 4) {
-      contrib[8 * n + 2 * q] = c0;
-      contrib[8 * n + 2 * q + 1] = c1;
-      if (two) {
-        contrib[8 * (n + nw) + 2 * q] = d0;
-        contrib[8 * (n + nw) + 2 * q + 1] = d1;
-      }
-    }
-    if (ready) {
-      __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
-      if (lane == 0) {
-        __hip_atomic_store(&ready[n], tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-        if (two) __hip_atomic_store(&ready[n + nw], tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-      }
-    }
-  }
-#endif
 }
 
 // With `ready`, the chain consumes the contributions as xxh3_kib_contribs

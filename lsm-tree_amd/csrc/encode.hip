@@ -42,10 +42,7 @@ constexpr uint32_t kPlanHuge = 1, kPlanBad = 2, kPlanMedium = 4, kPlanBig = 8;
 constexpr uint32_t kPlanHugeGpu = 16;  // a huge block the whole-GPU E3 path took over (not the one-workgroup E3)
 constexpr uint32_t kImgMedium = 20 * 1024;
 constexpr uint32_t kImgBig = 96 * 1024;
-#ifndef LSM_LIST_BW
-#define LSM_LIST_BW 8
-#endif
-constexpr uint32_t kListBigWaves = LSM_LIST_BW;  // waves per listed big block
+constexpr uint32_t kListBigWaves = 8;  // waves per listed big block
 constexpr uint32_t kE3HashChunk = 4096;    // buckets per LDS pass in E3
 constexpr uint64_t kListedOne = 1ULL << 40, kOffMask = kListedOne - 1;
 
@@ -792,32 +789,15 @@ __device__ __forceinline__ void write_block_lds_mw(const EncodeParams& P, uint32
 constexpr uint32_t kErecHead = 0x8000u;
 
 // Group write kernel (E2) budget, see encode_group_kernel.
-#ifndef LSM_G_WAVES
-#define LSM_G_WAVES 4
-#endif
-constexpr uint32_t kGWaves = LSM_G_WAVES, kGThreads = kGWaves * kWave;
-#ifndef LSM_G_RUN
-#define LSM_G_RUN 32
-#endif
-constexpr uint32_t kGRun = LSM_G_RUN;          // blocks per workgroup (<= 63: one lane each)
-#ifndef LSM_G_BLOCKS
-#define LSM_G_BLOCKS 16
-#endif
-constexpr uint32_t kGBlocks = LSM_G_BLOCKS;    // blocks per group
+constexpr uint32_t kGWaves = 4, kGThreads = kGWaves * kWave;
+constexpr uint32_t kGRun = 32;          // blocks per workgroup (<= 63: one lane each)
+constexpr uint32_t kGBlocks = 16;    // blocks per group
 constexpr uint32_t kGItems = kGThreads;        // items per group (one thread each)
 constexpr uint32_t kGSlack = 48;               // readable bytes past each staged span
-#ifndef LSM_G_KEYS  // group LDS budget (four configs[1] blocks by default)
-#define LSM_G_KEYS 4096
-#define LSM_G_VALS 14400
-#define LSM_G_IMG 15872
-#define LSM_G_UNION 4096
-#endif
-#ifndef LSM_G_WPE
-#define LSM_G_WPE 4
-#endif
-constexpr uint32_t kGKeys = LSM_G_KEYS, kGVals = LSM_G_VALS, kGImg = LSM_G_IMG;
+// group LDS budget (four configs[1] blocks by default)
+constexpr uint32_t kGKeys = 4096, kGVals = 14400, kGImg = 15872;
 constexpr uint32_t kGUnits = kGImg / 1024 + kGBlocks + 1;  // hash units per group
-constexpr uint32_t kGUnion = LSM_G_UNION;      // hash votes | hash contributions
+constexpr uint32_t kGUnion = 4096;      // hash votes | hash contributions
 constexpr uint32_t kGHash = kGUnion / 8;       // vote pairs
 static_assert(kGUnits * 64 <= kGUnion, "hash contributions");
 static_assert((kGUnits + 4) * 64 <= kGUnion, "the chain's batched reads stay inside L.uni");
@@ -843,16 +823,10 @@ __device__ __host__ __forceinline__ bool group_fits(uint64_t n, uint64_t kspan, 
 //      in its block, kept for E2 in erec.
 // Per block: size, binary-index step, hash-index size, size class, and the
 // key / value span starts E2 stages.
-#ifndef LSM_PLAN_BLOCKS
-#define LSM_PLAN_BLOCKS 128
-#endif
 // blocks per workgroup: longer-lived workgroups (16 -> 128: 0.80 -> 0.68 ms per 1 M blocks)
-constexpr uint32_t kPlanBlocks = LSM_PLAN_BLOCKS;
+constexpr uint32_t kPlanBlocks = 128;
 static_assert(kPlanBlocks <= 255, "thread nb loads the run's end: nb < 256 threads");
-#ifndef LSM_PLAN_PER
-#define LSM_PLAN_PER 2
-#endif
-constexpr uint32_t kPlanPer = LSM_PLAN_PER;          // consecutive items per thread
+constexpr uint32_t kPlanPer = 2;          // consecutive items per thread
 constexpr uint32_t kPlanChunk = 256 * kPlanPer;      // items per chunk
 
 // 16 bytes at p (global, any alignment): two aligned 16-B loads and a funnel
@@ -902,11 +876,7 @@ __device__ __forceinline__ Win16 gwin16a(const uint8_t* p) {
 
 // Shared prefix past an equal first 16 bytes: 16 bytes per step (rare: long
 // common key prefixes; kept narrow so the common path's registers stay low).
-#ifdef LSM_LCP_INLINE
-__device__ __forceinline__
-#else
 __device__ __noinline__
-#endif
 uint32_t lcp_tail(const uint8_t* keys, uint64_t a, uint64_t b, uint32_t n) {
   for (uint32_t k = 16; k < n; k += 16) {
     const Win16 wa = gwin16(keys + a + k), wb = gwin16(keys + b + k);
@@ -918,10 +888,7 @@ uint32_t lcp_tail(const uint8_t* keys, uint64_t a, uint64_t b, uint32_t n) {
 }
 
 template <bool kIndex>
-#ifndef LSM_PLAN_WPE
-#define LSM_PLAN_WPE 1
-#endif
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LSM_PLAN_WPE))) void encode_plan_kernel(EncodeParams P) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void encode_plan_kernel(EncodeParams P) {
   __shared__ uint32_t bst[kPlanBlocks + 1];
   __shared__ unsigned long long bfirst[kPlanBlocks], bend[kPlanBlocks], lhead[kPlanBlocks];
   __shared__ unsigned long long psum[4];
@@ -1111,16 +1078,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LSM_PLAN_WP
 // offset from the step's LDS copy, or for a head before the step from the
 // carried last head; and the next step's item fields are loaded while this
 // step's key windows are in flight.
-#ifndef LSM_PW_PER
-#define LSM_PW_PER 2
-#endif
-constexpr uint32_t kPW = LSM_PW_PER;  // consecutive items per lane
+constexpr uint32_t kPW = 2;  // consecutive items per lane
 constexpr uint32_t kPWStep = kPW * kWave;
-#ifndef LSM_PW_WPE
-#define LSM_PW_WPE 4
-#endif
 template <bool kBkt>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LSM_PW_WPE))) void encode_plan_wave_kernel(EncodeParams P) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void encode_plan_wave_kernel(EncodeParams P) {
   __shared__ uint32_t bst[kPlanBlocks + 1];
   __shared__ unsigned long long bfirst[kPlanBlocks], bend[kPlanBlocks], lhead[kPlanBlocks];
   __shared__ unsigned long long kos[4][kPWStep];
@@ -1437,10 +1398,7 @@ __device__ __forceinline__ void lds_copy(uint8_t* dst, uint32_t d, const uint8_t
   // 32 start points: a ds_read_b32 wave access is two groups of 32 lanes, so
   // lanes with a 64-B source stride (16 dwords: two per bank) all differ.
   uint32_t q = ((rot & 31u) * body) >> 5;  // 0 <= q < body
-#ifndef LSM_COPY_UNROLL
-#define LSM_COPY_UNROLL 4
-#endif
-  constexpr uint32_t U = LSM_COPY_UNROLL;  // dwords per step (all reads before the writes)
+  constexpr uint32_t U = 4;  // dwords per step (all reads before the writes)
   // Each source dword is read once: destination dword p is
   // alignbyte(src[p + 1], src[p]) and src[p] is the previous step's src[p + 1],
   // except after the wrap to p = 0, which takes w0 = src[0].
@@ -1521,9 +1479,6 @@ __device__ __forceinline__ void group_barrier_lds() {
 // has hash indexes (hash ratio > 0).  Both are batch-wide, so the paths a
 // batch never takes are compiled out (their registers would spill the
 // common path: every scratch reload waits for all outstanding loads).
-#ifndef LSM_NOVOTE
-#define LSM_NOVOTE 0
-#endif
 // ---------------------------------------- E1p: the plan of huge-block batches
 // Blocks of ~4 Ki items and more on average (the writer's 1-4 MiB data blocks,
 // writer/mod.rs:193-198) leave encode_plan_kernel one workgroup per one to four
@@ -1568,10 +1523,7 @@ __device__ __forceinline__ uint64_t shfl_down64(uint64_t v, int o) {
 // of a workgroup is 256 consecutive items); the four items' loads are issued
 // together, and a workgroup's block search serves 1024 items.
 constexpr uint32_t kE1pPer = 4;
-#ifndef LSM_E1P_LEN_PER
-#define LSM_E1P_LEN_PER 1
-#endif
-constexpr uint32_t kE1pLenPer = LSM_E1P_LEN_PER;  // (the lengths kernel: 4 items took 136 VGPRs, 2 ran as 1)
+constexpr uint32_t kE1pLenPer = 1;  // (the lengths kernel: 4 items took 136 VGPRs, 2 ran as 1)
 
 // The block holding item `first` (the workgroup's first item), by a 256-way
 // search of the starts (every thread one sample per round: one round for
@@ -1823,7 +1775,7 @@ __global__ __launch_bounds__(256) void encode_bucket_fixup_kernel(EncodeParams P
 }
 
 template <bool kIndex, bool kHash, bool kPlanBkt = false>
-__global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(LSM_G_WPE))) void encode_group_kernel(EncodeParams P) {
+__global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(4))) void encode_group_kernel(EncodeParams P) {
   __shared__ GroupLds L;
   typedef __attribute__((address_space(3))) void lds_void_t;
   typedef const __attribute__((address_space(1))) void gbl_void_t;
@@ -1957,9 +1909,7 @@ __global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(LSM_G
     // the next group's item fields: in flight under this whole group
     const Grp Gn = next_group(G.b + k);
     ItemMeta m = cook(raw);
-#ifndef LSM_NO_PREFETCH
     if (Gn.k) load_items(Gn, raw);
-#endif
     ENC_PHASE(9);
     // ---- wave 0: the group's block table (lane j = group block j; shuffles with every lane active)
     if (wave == 0) {
@@ -2043,7 +1993,7 @@ __global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(LSM_G
         const uint32_t bp = p0 + B.recs + 1 + (m.e >> 16) * B.step;
         for (uint32_t q = 0; q < B.step; ++q) L.img[bp + q] = (uint8_t)(roff >> (8 * q));
       }
-      if (kHash && B.hash_w && !LSM_NOVOTE) {
+      if (kHash && B.hash_w) {
         const uint32_t ridx = (tid - B.it0) / ri;
         const uint32_t hb =
             kPlanBkt ? m.hb
@@ -2093,7 +2043,7 @@ __global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(LSM_G
         const uint32_t bp = p0 + B.recs + 1 + (m.e >> 16) * B.step;
         for (uint32_t q = 0; q < B.step; ++q) L.img[bp + q] = (uint8_t)(roff >> (8 * q));
       }
-      if (kHash && B.hash_w && part == 0 && !LSM_NOVOTE) {
+      if (kHash && B.hash_w && part == 0) {
         const uint32_t ridx = (item - B.it0) / ri;
         const uint32_t hb =
             kPlanBkt ? m.hb
@@ -2429,10 +2379,7 @@ __global__ __launch_bounds__(kE3Threads) void encode_large_kernel(EncodeParams P
 //   hash     XXH3 contributions of the other KiB blocks into the pool
 //   chain    one wave per block: the eight accumulator chains on lanes 0..7,
 //            then the tail merge, the header and the status
-#ifndef LSM_EHUGE_ITEMS
-#define LSM_EHUGE_ITEMS 1024
-#endif
-constexpr uint32_t kEHugeItems = LSM_EHUGE_ITEMS;  // items per record unit, at most (four per thread)
+constexpr uint32_t kEHugeItems = 1024;  // items per record unit, at most (four per thread)
 constexpr uint32_t kEHugeImg = 2 * 4 * kE3HashChunk;  // LDS image of a record unit (the tail unit's vote arrays)
 constexpr uint32_t kEHugeGrid = 2048;
 
@@ -2564,10 +2511,7 @@ __global__ __launch_bounds__(1024) void encode_huge_plan_kernel(EncodeParams P) 
 }
 
 // Record units (u < nru of a block) and the tail unit (u == nru).
-#ifndef LSM_REC_WPE
-#define LSM_REC_WPE 4
-#endif
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(LSM_REC_WPE))) void encode_huge_records_kernel(EncodeParams P) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void encode_huge_records_kernel(EncodeParams P) {
   __shared__ __attribute__((aligned(16))) uint32_t lbuf[2 * kE3HashChunk];  // record image | vote arrays
   uint32_t* hlo = lbuf;
   uint32_t* hhi = lbuf + kE3HashChunk;
@@ -2961,11 +2905,7 @@ hipError_t launch_encode(const lsm_items& items, const uint32_t* starts, uint32_
   P.hb_valid = 0;
   P.hb_sh = 0;
   const dim3 pgrid((n_blocks + P.plan_bpw - 1) / P.plan_bpw);
-#ifndef LSM_NO_E1P
   const bool e1p = P.type != 1 && P.plan_bpw <= kE1pMaxBpw && items.n_items > 0 && items.n_items < 0xFFFFFFFFull;
-#else
-  const bool e1p = false;
-#endif
   if (e1p) {  // batches of huge blocks: the plan item-parallel
     P.hb_sh = 1;
     if (!P.huge_pool && (e = hipMemsetAsync(P.e1p_flag, 0, 4, st)) != hipSuccess) return e;
@@ -2979,7 +2919,6 @@ hipError_t launch_encode(const lsm_items& items, const uint32_t* starts, uint32_
     hipLaunchKernelGGL(encode_e1p_offsets_kernel, igrid, dim3(256), 0, st, P);
   } else if (P.type == 1)
     hipLaunchKernelGGL(encode_plan_kernel<true>, pgrid, dim3(256), 0, st, P);
-#ifndef LSM_PLAN_V1
   // (the wave kernel gives each wave whole blocks: with a few blocks of many items
   // per workgroup most waves would idle, so those batches keep the workgroup walk)
   else if (P.plan_bpw >= 16 && P.ratio > 0.0f) {  // (only this plan kernel fills hbucket)
@@ -2989,7 +2928,6 @@ hipError_t launch_encode(const lsm_items& items, const uint32_t* starts, uint32_
     hipLaunchKernelGGL(encode_bucket_fixup_kernel, dim3(1024), dim3(256), 0, st, P);
   } else if (P.plan_bpw >= 16)
     hipLaunchKernelGGL(encode_plan_wave_kernel<false>, pgrid, dim3(256), 0, st, P);
-#endif
   else
     hipLaunchKernelGGL(encode_plan_kernel<false>, pgrid, dim3(256), 0, st, P);
   EncodeOffOut oo{block_off, P.sizes, P.lists, P.list_count, n_blocks, P.plans, nullptr, nullptr, 0};
@@ -3010,10 +2948,6 @@ hipError_t launch_encode(const lsm_items& items, const uint32_t* starts, uint32_
     hipLaunchKernelGGL((encode_group_kernel<false, true>), ggrid, gblock, 0, st, P);
   else
     hipLaunchKernelGGL((encode_group_kernel<false, false>), ggrid, gblock, 0, st, P);
-#ifdef LSM_LIST_1WAVE
-  hipLaunchKernelGGL(encode_write_list_kernel, dim3(2048), dim3(kWave), kImgMedium, st, P, kPlanMedium);
-  hipLaunchKernelGGL(encode_write_list_kernel, dim3(512), dim3(kWave), kImgBig, st, P, kPlanBig);
-#else
   static uint64_t attr_mw = 0;
   if ((e = set_lds_attr((const void*)encode_write_list_mw_kernel<kListBigWaves>, kImgBig, &attr_mw)) != hipSuccess)
     return e;
@@ -3022,7 +2956,6 @@ hipError_t launch_encode(const lsm_items& items, const uint32_t* starts, uint32_
   hipLaunchKernelGGL(encode_write_list_kernel, dim3(2048), dim3(kWave), kImgMedium, st, P, kPlanMedium);
   hipLaunchKernelGGL(encode_write_list_mw_kernel<kListBigWaves>, dim3(512), dim3(kListBigWaves * kWave), kImgBig, st,
                      P, kPlanBig);
-#endif
   if (P.huge_pool) {  // huge blocks across the GPU (the ones it does not take stay flagged for E3 below)
     hipLaunchKernelGGL(encode_huge_plan_kernel, dim3(1), dim3(1024), 0, st, P);
     hipLaunchKernelGGL(encode_huge_records_kernel, dim3(kEHugeGrid), dim3(256), 0, st, P);

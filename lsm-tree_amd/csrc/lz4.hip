@@ -178,15 +178,8 @@ __device__ __forceinline__ int32_t lz4_stage_and_decode(const Lz4Block& b, uint3
   const uint32_t* src = reinterpret_cast<const uint32_t*>(b.base + a0);
   for (uint32_t w = lane; w < words; w += 64) lin[w] = src[w];
   __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
-#ifdef LSM_LZ4_DIAG_SKIP_DECODE  // ablation build only: checks + checksum + staging, no decode
-  if (lane == 0) b.dst[0] = (uint8_t)lin[0];
-  return ST_OK;
-#endif
   const int64_t got = lz4_wave_decode(lin, sh, b.data_len, lout, kOut, lane);
   if (got != (int64_t)b.raw_len) return LSM_DECOMPRESS;
-#ifdef LSM_LZ4_BYTE_STORE
-  for (uint32_t j = lane; j < b.raw_len; j += 64) b.dst[j] = lout[j];
-#else
   // dword stores to HBM: head bytes up to the first aligned dword, then dwords
   // built from two aligned LDS dwords (alignbyte), then the tail bytes
   const uint32_t len = b.raw_len;
@@ -201,7 +194,6 @@ __device__ __forceinline__ int32_t lz4_stage_and_decode(const Lz4Block& b, uint3
     d32[w] = s ? alignbyte(l32[a + 1], l32[a], s) : l32[a];
   }
   for (uint32_t j = head + 4 * body + lane; j < len; j += 64) b.dst[j] = lout[j];
-#endif
   return ST_OK;
 }
 

@@ -12,10 +12,7 @@
 namespace lsmgpu {
 
 constexpr int kScanThreads = 256;
-#ifndef LSM_SCAN_PER
-#define LSM_SCAN_PER 8
-#endif
-constexpr int kScanPerThread = LSM_SCAN_PER;
+constexpr int kScanPerThread = 8;
 constexpr int kScanTile = kScanThreads * kScanPerThread;  // 2048
 
 __device__ __forceinline__ uint64_t block_excl_scan_u64(uint64_t v, uint64_t* sh /*[kScanThreads/64]*/,
