@@ -288,7 +288,7 @@ __global__ __launch_bounds__(1024) void xxh3_batch_plan_kernel(const Xxh3Stream*
     uint64_t nb = 0, len = 0;
     if (i < n) {
       const bool ok = batch_state_ok(states + i, off, i);
-      len = ok ? off[i + 1] - off[i] : 0;
+      len = off[i + 1] >= off[i] ? off[i + 1] - off[i] : 0;  // (every range counts against total_len)
       nb = ok ? stream_blocks(states[i].pending, len) : 0;
       status[i] = ok ? (int32_t)LSM_OK : (int32_t)LSM_BAD_ARG;
     }

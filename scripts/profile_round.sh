@@ -23,7 +23,10 @@ line=$(grep "^variants:" $OUT/fetch.log)
 BYTES=$(echo "$line" | sed 's/.* bytes \([0-9]*\) items.*/\1/')
 ITEMS=$(echo "$line" | sed 's/.* items \([0-9]*\).*/\1/')
 EALG=$(grep "alg_bytes" $OUT/efetch.log | sed 's/.*alg_bytes \([0-9]*\).*/\1/')
-python3 scripts/traffic_summary.py $OUT/fetch $OUT/write $NB $BYTES $ITEMS $OUT/efetch $OUT/ewrite $EALG > $OUT/traffic.json
+EITEMS=$(grep "alg_bytes" $OUT/efetch.log | sed 's/.*blocks \([0-9]*\) items.*/\1/')
+# (the counter workload: 16 B keys, 64 B values)
+python3 scripts/traffic_summary.py $OUT/fetch $OUT/write $NB $BYTES $ITEMS $OUT/efetch $OUT/ewrite $EALG \
+  $EITEMS $((16 * EITEMS)) $((64 * EITEMS)) > $OUT/traffic.json
 cat $OUT/traffic.json
 find $OUT/kt -name "*kernel_stats.csv" -exec cp {} $OUT/kernel_stats.csv \;
 head -20 $OUT/kernel_stats.csv

@@ -3,11 +3,14 @@
 one entry per hot-path kernel group, in the format bench.load_traffic reads.
 
 gfx950 correction (MI355X_MICROARCH.md, HBM section): FETCH_SIZE reports half
-the bytes of wide streaming reads -> doubled.  WRITE_SIZE is exact for 16-B
-stores; narrower stores (the decode SoA's 1-8 B lanes, the encode plan's u32
-words) are uncalibrated and reported raw.
+the bytes of wide streaming reads -> doubled.  Calibrated for every read shape
+these kernels use (scripts/fetch_calib.py, profiles/r05_fetch_calib.json: u64,
+u32 and u8 per lane, the plan's overlapping u64 windows, 16 B per lane and the
+LDS-DMA all report exactly half).  WRITE_SIZE is exact for 16-B stores, u32
+stores (r05_fetch_calib.json) and the decode SoA's 1-8 B stores
+(scripts/write_calib.py, round 2).
 Usage: traffic_summary.py DEC_FETCH DEC_WRITE DEC_BLOCKS DEC_BYTES DEC_ITEMS
-                          ENC_FETCH ENC_WRITE ENC_ALG_BYTES > profiles/traffic_rNN.json
+                          ENC_FETCH ENC_WRITE ENC_ALG_BYTES ITEMS KEY_BYTES VAL_BYTES > profiles/traffic_rNN.json
 """
 import csv
 import json
@@ -54,15 +57,30 @@ def main():
     f, n = per_dispatch(a[0], "FETCH_SIZE", ["decode_blocks_kernel"], True)
     w, _ = per_dispatch(a[1], "WRITE_SIZE", ["decode_blocks_kernel"], True)
     out = {"decode_blocks_kernel": entry("decode_blocks_kernel", f, w, n, dblocks, dbytes + ditems * 25 + dblocks * 8,
-                                         "FETCH_SIZE x2 (gfx950 wide-read correction); WRITE_SIZE raw (1-8 B/lane "
-                                         "SoA stores, uncalibrated)")}
+                                         "FETCH_SIZE x2 (gfx950 correction, calibrated for LDS-DMA reads); WRITE_SIZE "
+                                         "raw (1-8 B/lane SoA stores: exact, scripts/write_calib.py)")}
     if len(a) >= 8:
         names = ["encode_plan", "scan_tile", "encode_group_kernel", "encode_write_list", "encode_large"]
         f, n = per_dispatch(a[5], "FETCH_SIZE", names, True)
         w, _ = per_dispatch(a[6], "WRITE_SIZE", names, True)
         out["lsm_encode_blocks"] = entry("lsm_encode_blocks", f, w, n, dblocks, int(a[7]),
-                                         "plan + scan + group kernels summed per launch; FETCH_SIZE x2; WRITE_SIZE "
-                                         "raw (16 B/lane copy-out exact, plan words uncalibrated)")
+                                         "plan + scan + group kernels summed per launch; FETCH_SIZE x2 and WRITE_SIZE "
+                                         "raw, both calibrated (profiles/r05_fetch_calib.json)")
+        # per kernel: what each pass of the two-pass design must move (bytes per launch):
+        #   plan  reads the item SoA (8 + 8 + 8 + 1 B) and each key's first 16 bytes,
+        #         writes erec (4 B per item) and per block size, plan, key / value span starts (40 B)
+        #   group reads keys, values, the item SoA again, erec, the block plans (40 B) and offsets,
+        #         writes the blocks and their statuses
+        items, key_bytes, val_bytes = int(a[8]), int(a[9]), int(a[10])
+        out_bytes = int(a[7]) - (key_bytes + val_bytes + items * 25 + 16 * dblocks + 4)
+        plan_alg = items * (25 + 16 + 4) + dblocks * 40
+        group_alg = key_bytes + val_bytes + items * (25 + 4) + dblocks * 48 + out_bytes
+        for k, alg in (("encode_plan_wave_kernel", plan_alg), ("encode_group_kernel", group_alg)):
+            f1, n1 = per_dispatch(a[5], "FETCH_SIZE", [k], True)
+            w1, _ = per_dispatch(a[6], "WRITE_SIZE", [k], True)
+            e = entry(k, f1, w1, n1, dblocks, alg, "this kernel's share of the two-pass encode; alg = the bytes its "
+                                                   "pass must move (see traffic_summary.py)")
+            out[k] = e
     print(json.dumps(out, indent=1))
 
 
