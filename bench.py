@@ -1127,10 +1127,12 @@ def load_trace_ms(kernels, n_blocks):
     run over the same batch size; None when no profile has every pair."""
     import csv
     best, src = None, None
-    for p in sorted((ROOT / "profiles").glob("*_bench_kernels_by_grid.csv"), key=lambda q: q.stat().st_mtime):
+    for p in sorted((ROOT / "profiles").glob("*_bench_kernels_by_grid.csv")):  # (round names sort in order)
         try:
             rows = list(csv.DictReader(p.open()))
         except Exception:
+            continue
+        if not rows or not {"kernel", "workgroups"} <= set(rows[0]) or not ({"avg_us", "avg_ns"} & set(rows[0])):
             continue
         by = {(r["kernel"], int(r["workgroups"])): r for r in rows}
         if not all(k in by for k in kernels):
