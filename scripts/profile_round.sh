@@ -9,7 +9,7 @@ R=${1:-r01}
 OUT=gpurun_out/prof_$R
 mkdir -p $OUT
 timeout -k 10 400 rocprofv3 --kernel-trace --stats -d $OUT/kt -o bench --output-format csv -- \
-  python3 bench.py --steps 10 --warmup 2 --no-cpu > $OUT/bench_kt.log 2>&1
+  python3 bench.py --steps 10 --warmup 2 --no-cpu --no-extra --no-host > $OUT/bench_kt.log 2>&1
 NB=1048576
 timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE --output-format csv -d $OUT/fetch -o pmc -- \
   python3 scripts/prof_decode.py --variants full --reps 4 --blocks $NB > $OUT/fetch.log 2>&1
@@ -29,4 +29,5 @@ python3 scripts/traffic_summary.py $OUT/fetch $OUT/write $NB $BYTES $ITEMS $OUT/
   $EITEMS $((16 * EITEMS)) $((64 * EITEMS)) > $OUT/traffic.json
 cat $OUT/traffic.json
 find $OUT/kt -name "*kernel_stats.csv" -exec cp {} $OUT/kernel_stats.csv \;
+python3 scripts/trace_by_grid.py $(find $OUT/kt -name "*kernel_trace.csv" | head -1) > $OUT/kernels_by_grid.csv
 head -20 $OUT/kernel_stats.csv

@@ -14,8 +14,8 @@ with open(sys.argv[1]) as fh:
         if "lsmgpu::" not in name:
             continue
         grid = int(r["Grid_Size_X"]) // max(1, int(r["Workgroup_Size_X"]))
-        rows[(name.split("(")[0].replace("void ", ""), grid)].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
+        rows[(name.split("(")[0].replace("void ", "").replace("lsmgpu::", ""), grid)].append(int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
 w = csv.writer(sys.stdout)
-w.writerow(["kernel", "workgroups", "calls", "avg_ns", "min_ns", "max_ns"])
+w.writerow(["kernel", "workgroups", "calls", "avg_us", "min_us", "max_us"])
 for (k, g), d in sorted(rows.items(), key=lambda kv: -sum(kv[1])):
-    w.writerow([k, g, len(d), round(sum(d) / len(d)), min(d), max(d)])
+    w.writerow([k, g, len(d), round(sum(d) / len(d) / 1e3, 1), round(min(d) / 1e3, 1), round(max(d) / 1e3, 1)])
