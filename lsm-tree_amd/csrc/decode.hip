@@ -1644,6 +1644,22 @@ __global__ __launch_bounds__(kGroupWaves * kWave) __attribute__((amdgpu_waves_pe
           }
         }
         DEC_ROLE(10);
+      } else if (hash && k <= (kGroupWaves - nA) * 4 && (role - nA) * 4 + 1 == k) {
+        // this wave's share of the rows is one block (k = 4 h + 1, e.g. nine
+        // 4 KiB blocks on three hash waves): the whole wave hashes it, 1 KiB
+        // per step, instead of one row with three rows idle
+        const uint32_t jb = k - 1;
+        if (meta[jb].hdr_st == ST_OK) {
+          const uint32_t hb = meta[jb].hb, plen = meta[jb].len - kHdrLen;
+          uint64_t lo, hi;
+          xxh3_128_wave(stage, hb + kHdrLen, plen, ls, lo, hi);
+          const bool hck = header_cksum_ok(stage, hb);
+          if (lane == 0) {
+            meta[jb].ck_bad = lo != meta[jb].ck_lo || hi != meta[jb].ck_hi;
+            meta[jb].hck_bad = !hck;
+          }
+        }
+        DEC_ROLE(10);
       } else if (hash) {
         const uint32_t rows = (kGroupWaves - nA) * 4;
         for (uint32_t jb = (role - nA) * 4 + (lane >> 4); jb < k; jb += rows) {

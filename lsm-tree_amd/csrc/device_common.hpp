@@ -440,11 +440,13 @@ __device__ __forceinline__ void stripe_part(const Win16& w, uint64_t k0, uint64_
 // Sum of v over the 16 lanes that share (lane & 3): two DPP row rotates
 // (within each 16-lane row) + gfx950 v_permlane16_swap / v_permlane32_swap
 // (across rows) — all VALU, no LDS round trips.
+// (row rotates and quad perms read an in-range lane for every lane, so the
+// bound-control form needs no zeroed "old" operand: one VALU per move, not two)
 __device__ __forceinline__ uint32_t dpp_ror4(uint32_t x) {
-  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x124, 0xF, 0xF, false);
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x124, 0xF, 0xF, true);
 }
 __device__ __forceinline__ uint32_t dpp_ror8(uint32_t x) {
-  return (uint32_t)__builtin_amdgcn_update_dpp(0, (int)x, 0x128, 0xF, 0xF, false);
+  return (uint32_t)__builtin_amdgcn_mov_dpp((int)x, 0x128, 0xF, 0xF, true);
 }
 __device__ __forceinline__ uint64_t quad_group_sum64(uint64_t v) {
   uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
@@ -897,11 +899,11 @@ __device__ __forceinline__ uint64_t row_quad_sum64(uint64_t v) {
 // sum over the 4 lanes of each quad (DPP quad_perm [1,0,3,2] then [2,3,0,1])
 __device__ __forceinline__ uint64_t quad_sum64(uint64_t v) {
   uint32_t lo = (uint32_t)v, hi = (uint32_t)(v >> 32);
-  v += (uint64_t)(uint32_t)__builtin_amdgcn_update_dpp(0, (int)lo, 0xB1, 0xF, 0xF, false) |
-       ((uint64_t)(uint32_t)__builtin_amdgcn_update_dpp(0, (int)hi, 0xB1, 0xF, 0xF, false) << 32);
+  v += (uint64_t)(uint32_t)__builtin_amdgcn_mov_dpp((int)lo, 0xB1, 0xF, 0xF, true) |
+       ((uint64_t)(uint32_t)__builtin_amdgcn_mov_dpp((int)hi, 0xB1, 0xF, 0xF, true) << 32);
   lo = (uint32_t)v; hi = (uint32_t)(v >> 32);
-  v += (uint64_t)(uint32_t)__builtin_amdgcn_update_dpp(0, (int)lo, 0x4E, 0xF, 0xF, false) |
-       ((uint64_t)(uint32_t)__builtin_amdgcn_update_dpp(0, (int)hi, 0x4E, 0xF, 0xF, false) << 32);
+  v += (uint64_t)(uint32_t)__builtin_amdgcn_mov_dpp((int)lo, 0x4E, 0xF, 0xF, true) |
+       ((uint64_t)(uint32_t)__builtin_amdgcn_mov_dpp((int)hi, 0x4E, 0xF, 0xF, true) << 32);
   return v;
 }
 
