@@ -1630,26 +1630,13 @@ __global__ __launch_bounds__(kGroupWaves * kWave) __attribute__((amdgpu_waves_pe
       if (role < nA) {
         phase_a<kDecWide>(stage, meta, owner, rec, role * kWave, nA * kWave, total, P.tile_items);
         DEC_ROLE(8);
-      } else if (hash && k <= kGroupWaves - nA) {
-        // few (large) blocks: one wave per block, the 64-lane XXH3 (1 KiB per step)
-        const uint32_t jb = role - nA;
+      } else if (hash && (k <= kGroupWaves - nA || (k <= (kGroupWaves - nA) * 4 && (role - nA) * 4 + 1 == k))) {
+        // few (large) blocks: one wave per block, the 64-lane XXH3 (1 KiB per
+        // step); also a wave whose share of the rows below is one block
+        // (k = 4 h + 1, e.g. nine 4 KiB blocks on three hash waves): the whole
+        // wave hashes it instead of one row with three rows idle
+        const uint32_t jb = k <= kGroupWaves - nA ? role - nA : k - 1;
         if (jb < k && meta[jb].hdr_st == ST_OK) {
-          const uint32_t hb = meta[jb].hb, plen = meta[jb].len - kHdrLen;
-          uint64_t lo, hi;
-          xxh3_128_wave(stage, hb + kHdrLen, plen, ls, lo, hi);
-          const bool hck = header_cksum_ok(stage, hb);
-          if (lane == 0) {
-            meta[jb].ck_bad = lo != meta[jb].ck_lo || hi != meta[jb].ck_hi;
-            meta[jb].hck_bad = !hck;
-          }
-        }
-        DEC_ROLE(10);
-      } else if (hash && k <= (kGroupWaves - nA) * 4 && (role - nA) * 4 + 1 == k) {
-        // this wave's share of the rows is one block (k = 4 h + 1, e.g. nine
-        // 4 KiB blocks on three hash waves): the whole wave hashes it, 1 KiB
-        // per step, instead of one row with three rows idle
-        const uint32_t jb = k - 1;
-        if (meta[jb].hdr_st == ST_OK) {
           const uint32_t hb = meta[jb].hb, plen = meta[jb].len - kHdrLen;
           uint64_t lo, hi;
           xxh3_128_wave(stage, hb + kHdrLen, plen, ls, lo, hi);

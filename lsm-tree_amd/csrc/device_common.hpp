@@ -167,6 +167,15 @@ __device__ __forceinline__ Win16 read_win16(const uint8_t* base, uint32_t pos) {
            e3 = alignbyte(d4, d3, s);
   return {(uint64_t)e0 | ((uint64_t)e1 << 32), (uint64_t)e2 | ((uint64_t)e3 << 32)};
 }
+// read_win16 with the dword-aligned offset a and the shift s split out, for
+// loops that step a window by whole dwords: a + constant folds into the
+// ds_read offsets, and the alignment is computed once per loop, not per window.
+__device__ __forceinline__ Win16 read_win16_split(const uint8_t* base, uint32_t a, uint32_t s) {
+  const uint32_t d0 = ld32(base, a), d1 = ld32(base, a + 4), d2 = ld32(base, a + 8), d3 = ld32(base, a + 12),
+                 d4 = ld32(base, a + 16);
+  return {(uint64_t)alignbyte(d1, d0, s) | ((uint64_t)alignbyte(d2, d1, s) << 32),
+          (uint64_t)alignbyte(d3, d2, s) | ((uint64_t)alignbyte(d4, d3, s) << 32)};
+}
 // The same from an LDS pointer (explicit address space: ds_read even where
 // the compiler cannot tell that a generic pointer is LDS).
 __device__ __forceinline__ Win16 read_win16_lds(const uint8_t* base_generic, uint32_t pos) {
@@ -485,9 +494,10 @@ __device__ __forceinline__ void xxh3_128_wave_long(const uint8_t* base, uint32_t
   // The per-KiB contributions do not depend on the accumulators, so two
   // KiB blocks are loaded and reduced together; only the scramble is serial.
   uint32_t n = 0;
+  const uint32_t la = (pos + 16 * lane) & ~3u, lsh = (pos + 16 * lane) & 3u;  // (one shift for every window)
   for (; n + 2 <= nb_blocks; n += 2) {
-    const Win16 wa = read_win16(base, pos + n * 1024 + 16 * lane);
-    const Win16 wb = read_win16(base, pos + (n + 1) * 1024 + 16 * lane);
+    const Win16 wa = read_win16_split(base, la + n * 1024, lsh);
+    const Win16 wb = read_win16_split(base, la + n * 1024 + 1024, lsh);
     uint64_t c0 = 0, c1 = 0, d0 = 0, d1 = 0;
     stripe_part(wa, k0, k1, c0, c1);
     stripe_part(wb, k0, k1, d0, d1);
@@ -501,7 +511,7 @@ __device__ __forceinline__ void xxh3_128_wave_long(const uint8_t* base, uint32_t
     a1 = xxh3_scr(a1, d1, scr1);
   }
   if (n < nb_blocks) {
-    const Win16 w = read_win16(base, pos + n * 1024 + 16 * lane);
+    const Win16 w = read_win16_split(base, la + n * 1024, lsh);
     uint64_t c0 = 0, c1 = 0;
     stripe_part(w, k0, k1, c0, c1);
     c0 = quad_group_sum64(c0);
@@ -972,11 +982,12 @@ __device__ __forceinline__ void xxh3_128_row_long_lean(const uint8_t* base, uint
   uint64_t a1 = q == 0 ? P64_1 : q == 1 ? P64_3 : q == 2 ? (uint64_t)P32_2 : (uint64_t)P32_1;
   const uint32_t nb_blocks = (len - 1) / 1024;
   const uint64_t* acc = ls->acc + s + 2 * q;
+  const uint32_t wa = (pos + 16 * r) & ~3u, wsh = (pos + 16 * r) & 3u;  // (every window of the lane shares the shift)
   for (uint32_t n = 0; n < nb_blocks; ++n) {
     uint64_t c0 = 0, c1 = 0;
 #pragma unroll 2
     for (int t = 0; t < 4; ++t) {
-      const Win16 w = read_win16(base, pos + n * 1024 + 256 * t + 16 * r);
+      const Win16 w = read_win16_split(base, wa + n * 1024 + 256 * t, wsh);
       stripe_part(w, acc[4 * t], acc[4 * t + 1], c0, c1);
     }
     c0 = row_quad_sum64(c0);
@@ -991,7 +1002,7 @@ __device__ __forceinline__ void xxh3_128_row_long_lean(const uint8_t* base, uint
 #pragma unroll 1
     for (int t = 0; t < 4; ++t) {
       if ((uint32_t)(4 * t + s) < nb_stripes) {
-        const Win16 w = read_win16(base, pos + tail0 + 256 * t + 16 * r);
+        const Win16 w = read_win16_split(base, wa + tail0 + 256 * t, wsh);
         stripe_part(w, acc[4 * t], acc[4 * t + 1], c0, c1);
       }
     }
