@@ -823,9 +823,10 @@ __global__ __launch_bounds__(kBigWaves * kWave) void decode_deferred_staged_kern
 //          oracle check, the LEB cursor for rare shapes; from HBM when one
 //          runs past the staged bytes) and computes the XXH3 contributions
 //          of the KiB blocks that start in the window, from LDS too
-//   chain  (decode_huge_chain_kernel): one wave per block, the eight
-//          accumulator chains on lanes 0..7 (xxh3_chain8), then the tail
-//          merge, the checksum compare and the status
+//   chain  (inside decode_huge_kernel: its first workgroups): one wave per
+//          block, the eight accumulator chains on lanes 0..7 (xxh3_chain8)
+//          over the KiB contributions as the units publish them (unit-done
+//          flags), then the tail merge, the checksum compare and the status
 // A block whose header fails, or that no longer fits the pool, goes to the
 // general path (defer2) as before: statuses and outputs are the same on both.
 constexpr uint32_t kHugeWin = 32 * 1024;  // span bytes per unit
@@ -839,8 +840,12 @@ constexpr uint32_t kHugeOwner = kHugeMeta + 80;
 constexpr uint32_t kHugeRec = kHugeOwner + kHugeMaxIv;
 constexpr uint32_t kHugeLds = 64 + kHugeRec + 8 * (kHugeTile + 1);
 constexpr uint32_t kHugeGrid = 2048;
-constexpr uint32_t kChainRing = 16;     // xxh3_chain8: KiB of contribution rows in flight per chain wave
-constexpr uint32_t kHugeChainGrid = 1024;  // chain workgroups (one block each, grid-stride)
+constexpr uint32_t kStreamRing = 12;    // the same for the chain waves inside decode_huge_kernel (4 per workgroup)
+constexpr uint32_t kStreamPolls = 1u << 18;  // flag polls before a chain wave gives a block up (hang guard)
+constexpr uint32_t kStreamChainWgs = 16;     // chain workgroups: 64 chain waves (a 1 KiB step of 20 ns each)
+constexpr uint32_t kStreamMinUnits = 64;     // stream the chains for batches holding a block of >= 2 MiB
+constexpr uint32_t kChainRing = 16;          // the chain kernel's ring (KiB of contribution rows in flight per wave)
+constexpr uint32_t kHugeChainGrid = 1024;    // chain kernel workgroups (one block each, grid-stride)
 constexpr uint32_t kHugeUnitsGrid = 1024;  // unit-table workgroups (thread per restart interval, grid-stride)
 
 struct HugeRec {
@@ -855,14 +860,18 @@ struct HugeRec {
 static_assert(sizeof(HugeRec) % 16 == 0, "HugeRec layout");
 
 struct HugeHdr {
-  uint64_t total_kib;  // contributions over every accepted block
+  uint64_t total_kib;  // contribution rows over every listed block (each block's padded to 16)
   uint32_t n3;         // listed huge blocks (HugeRec entries)
   uint32_t total_pu;   // work units (kHugeWin windows)
   uint64_t total_iv;   // restart intervals + 1 per parsed block (units kernel threads)
+  uint32_t max_npu;    // most units of one accepted block
+  uint32_t stream;     // chains inside decode_huge_kernel, streaming behind the units (blocks of >= 2 MiB)
 };
 
 // Pool: [HugeHdr | 256][kpre, ppre, ipre: u64 x (n + 1) each][HugeRec x n][contributions, 64 B per KiB
-// from the front] .. [unit table, 8 B per unit, from the back: entry u at uend[-1 - u]].
+// from the front, each block's rows padded to a multiple of 16 (one 1-KiB chain chunk holds no
+// other block's rows)] .. [unit table, 16 B per unit, from the back: entry u at uend[-1 - u]:
+// first interval, its payload offset, the unit-done flag].
 struct HugeLayout {
   HugeHdr* hdr;
   uint64_t* kpre;
@@ -870,7 +879,7 @@ struct HugeLayout {
   uint64_t* ipre;
   HugeRec* rec;
   uint64_t* contrib;
-  uint2* uend;    // unit u: {first restart interval starting in it, that interval's payload offset}
+  uint4* uend;    // unit u: {first restart interval starting in it, that interval's payload offset, done flag}
   uint64_t rest;  // pool bytes after the fixed part
   bool ok;
 };
@@ -888,8 +897,8 @@ __device__ __forceinline__ HugeLayout huge_layout(const DecodeParams& P, uint32_
   const uint64_t fixed = huge_fixed_bytes(n);
   L.contrib = reinterpret_cast<uint64_t*>(b + fixed);
   L.ok = b != nullptr && fixed <= P.huge_pool_bytes;
-  L.rest = L.ok ? (P.huge_pool_bytes - fixed) & ~7ULL : 0;
-  L.uend = reinterpret_cast<uint2*>(b + fixed + L.rest);
+  L.rest = L.ok ? (P.huge_pool_bytes - fixed) & ~15ULL : 0;
+  L.uend = reinterpret_cast<uint4*>(b + fixed + L.rest);
   return L;
 }
 
@@ -911,11 +920,13 @@ __device__ void huge_plan(const DecodeParams& P, uint64_t* sh, uint32_t nthr) {
       L.hdr->total_pu = 0;
       L.hdr->total_kib = 0;
       L.hdr->total_iv = 0;
+      L.hdr->max_npu = 0;
+      L.hdr->stream = 0;
     }
     return;
   }
   const bool hash = !(P.flags & LSM_DECODE_PAYLOAD_VERIFIED);
-  if (tid == 0) sh[48] = 0, sh[49] = 0, sh[50] = 0;
+  if (tid == 0) sh[48] = 0, sh[49] = 0, sh[50] = 0, sh[51] = 0;
   __syncthreads();
   for (uint32_t c = 0; c < n; c += nthr) {
     const uint32_t i = c + tid;
@@ -942,7 +953,8 @@ __device__ void huge_plan(const DecodeParams& P, uint64_t* sh, uint32_t nthr) {
         niv = m.st == ST_OK ? trailer_of(m).bin_len + 1 : 0;  // (+1: the units kernel's end-of-block thread)
       }
     }
-    const uint64_t ik = wave_incl_scan_u64(nbk), ip = wave_incl_scan_u64(npu), ii = wave_incl_scan_u64(niv);
+    const uint64_t nbk16 = (nbk + 15) & ~15ULL;  // (rows padded to whole 1-KiB chain chunks)
+    const uint64_t ik = wave_incl_scan_u64(nbk16), ip = wave_incl_scan_u64(npu), ii = wave_incl_scan_u64(niv);
     if (lane == 63) sh[wave] = ik, sh[16 + wave] = ip, sh[32 + wave] = ii;
     __syncthreads();
     uint64_t bk = sh[48], bp = sh[49], bi = sh[50], tk = 0, tp = 0, ti = 0;
@@ -954,10 +966,10 @@ __device__ void huge_plan(const DecodeParams& P, uint64_t* sh, uint32_t nthr) {
       tp += sh[16 + w];
       ti += sh[32 + w];
     }
-    const uint64_t kp = bk + ik - nbk, pp = bp + ip - npu, ivp = bi + ii - niv;
+    const uint64_t kp = bk + ik - nbk16, pp = bp + ip - npu, ivp = bi + ii - niv;
     if (i < n) {
       // (the pool holds the contributions, front, and unit entries, back, of a prefix of the list)
-      acc = acc && 64 * (kp + nbk) + 8 * (pp + npu) <= L.rest;
+      acc = acc && 64 * (kp + nbk16) + 16 * (pp + npu) <= L.rest;
       HugeRec* r = L.rec + i;
       r->m = m;
       r->span0 = span0;
@@ -974,6 +986,10 @@ __device__ void huge_plan(const DecodeParams& P, uint64_t* sh, uint32_t nthr) {
       gstore(L.ipre, i, ivp);
       if (!acc) defer2_block(P, b);
     }
+    {  // the most units of an accepted block: one LDS atomic per wave
+      const uint32_t mx = wave_max_u32(i < n && acc ? (uint32_t)npu : 0u);
+      if (lane == 0 && mx) atomicMax(reinterpret_cast<unsigned int*>(&sh[51]), mx);
+    }
     __syncthreads();
     if (tid == 0) sh[48] += tk, sh[49] += tp, sh[50] += ti;
     __syncthreads();
@@ -985,6 +1001,8 @@ __device__ void huge_plan(const DecodeParams& P, uint64_t* sh, uint32_t nthr) {
     L.hdr->total_kib = sh[48];
     L.hdr->total_pu = (uint32_t)sh[49];
     L.hdr->total_iv = sh[50];
+    L.hdr->max_npu = (uint32_t)sh[51];
+    L.hdr->stream = (uint32_t)sh[51] >= kStreamMinUnits;
     L.hdr->n3 = n;
   }
 }
@@ -1235,6 +1253,10 @@ __global__ __launch_bounds__(256) void decode_huge_units_kernel(DecodeParams P) 
   const uint32_t n = hp->n3;
   if (!n) return;
   const HugeLayout L = huge_layout(P, n);
+  if (hp->stream)  // this call's unit-done flags start clear (entries inside the pool only)
+    for (uint64_t u = (uint64_t)blockIdx.x * 256 + threadIdx.x; u < hp->total_pu && 16 * (u + 1) <= L.rest;
+         u += (uint64_t)gridDim.x * 256)
+      L.uend[-1 - (int64_t)u].z = 0;
   const uint64_t tiv = hp->total_iv;
   for (uint64_t t0 = (uint64_t)blockIdx.x * 256; t0 < tiv; t0 += (uint64_t)gridDim.x * 256) {
     if (threadIdx.x == 0) sb = last_le(L.ipre, n, t0);
@@ -1257,7 +1279,7 @@ __global__ __launch_bounds__(256) void decode_huge_units_kernel(DecodeParams P) 
     if (x > 0 && x < nint && sv < sp) __hip_atomic_store(&r->nonmono, 1u, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     const int64_t ulo = x > 0 ? (int64_t)((m.p0 + (uint64_t)sp) / kHugeWin) + 1 : 0;
     const int64_t uhi = x < nint ? min((int64_t)((m.p0 + (uint64_t)sv) / kHugeWin), npu - 1) : npu - 1;
-    for (int64_t u = ulo; u <= uhi; ++u) L.uend[-1 - (int64_t)(ub + u)] = make_uint2(x, sv);
+    for (int64_t u = ulo; u <= uhi; ++u) *reinterpret_cast<uint2*>(&L.uend[-1 - (int64_t)(ub + u)]) = make_uint2(x, sv);
   }
 }
 
@@ -1267,8 +1289,76 @@ __global__ __launch_bounds__(256) void decode_huge_units_kernel(DecodeParams P) 
 // fields) on a window view of the block (meta offsets relative to the stage,
 // interval numbers absolute, the binary-index entries copied next to the
 // stage); others walk their intervals thread by thread.
+// Unit-done flags: unit u's entry .z = the call's tag once its records and
+// contributions are written.  The contributions are agent-scope stores
+// (through the writer XCD's L2), waited for (vmcnt) before the flag store;
+// a chain wave reads a 1-KiB chunk of rows (LDS-DMA) only after the flags of
+// every unit that writes into it: no L2 of this launch holds a line of the
+// chunk before that, and every block's rows are padded to whole chunks.
+// ready_upto: units [0, ready_upto) of the block are known done; polls 64
+// flags per load.  Returns false after kStreamPolls polls (hang guard).
+__device__ __forceinline__ bool huge_wait_units(const HugeLayout& L, uint64_t ub, uint32_t need, uint32_t tag,
+                                                uint32_t npu, uint32_t& ready_upto) {
+  const uint32_t lane = threadIdx.x & 63;
+  need = min(need, npu);
+  for (uint32_t polls = 0; ready_upto < need; ++polls) {
+    if (polls >= kStreamPolls) return false;
+    const uint32_t c = ready_upto + lane;
+    const uint32_t f = c < npu ? __hip_atomic_load(&L.uend[-1 - (int64_t)(ub + c)].z, __ATOMIC_RELAXED,
+                                                    __HIP_MEMORY_SCOPE_AGENT)
+                               : tag;
+    const uint64_t done = __ballot(f == tag);
+    const uint32_t adv = (uint32_t)__builtin_ctzll(~done);  // (done == ~0: 64)
+    ready_upto = min(npu, ready_upto + (done == ~0ULL ? 64u : adv));
+    if (ready_upto < need && adv == 0) __builtin_amdgcn_s_sleep(2);
+  }
+  return true;
+}
+
+// One block's chain on this wave, its rows consumed as the units publish
+// them, then the tail merge, the checksum compare and the status (oracle
+// order: payload checksum, then trailer, then parse) once every unit is done.
+__device__ void huge_chain_streamed(const DecodeParams& P, const HugeLayout& L, uint32_t i, uint8_t* ring) {
+  const HugeRec* r = L.rec + i;
+  const uint32_t lane = threadIdx.x & 63, k = lane & 7, q = lane & 3;
+  const bool hash = !(P.flags & LSM_DECODE_PAYLOAD_VERIFIED);
+  const BlockMeta m = r->m;
+  const uint64_t ub = gload(L.ppre, i);
+  const uint32_t npu = (uint32_t)(gload(L.ppre, i + 1) - ub);
+  const uint32_t tag = P.huge_tag;
+  uint32_t ready_upto = 0;
+  bool ok = true;
+  int32_t st = ST_OK;
+  if (hash) {
+    uint64_t a0, a1;
+    xxh3_acc_init((int)(k >> 1), a0, a1);
+    uint64_t x = (k & 1) ? a1 : a0;
+    const uint32_t nbk = r->nbk;
+    if (nbk) {
+      // chunk c of 16 rows needs the units holding the starts of KiB blocks 16c .. 16c + 15
+      auto wait = [&](uint64_t c) {
+        const uint64_t last = min((uint64_t)nbk - 1, 16 * c + 15);
+        const uint32_t need = (uint32_t)((m.p0 + 1024 * last) / kHugeWin) + 1;
+        ok = ok && huge_wait_units(L, ub, need, tag, npu, ready_upto);
+      };
+      x = xxh3_chain8<kStreamRing>(L.contrib + 8 * gload(L.kpre, i), nbk, x, kLongSecret.acc[16 + k], ring, wait);
+    }
+    const uint64_t c0 = wave_shfl_u64(x, (int)(2 * q)), c1 = wave_shfl_u64(x, (int)(2 * q + 1));
+    uint64_t lo, hi;
+    xxh3_wave_tail_merge(P.blocks + r->span0, m.p0, m.len - kHdrLen, &kLongSecret, c0, c1, lo, hi);
+    if (lo != m.ck_lo || hi != m.ck_hi) st = ST_CKSUM;
+  }
+  ok = ok && huge_wait_units(L, ub, npu, tag, npu, ready_upto);  // every unit's parse result
+  if (st == ST_OK) {
+    const uint32_t bad = __hip_atomic_load(&r->parse_bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    st = m.st != ST_OK ? m.st : bad ? (int32_t)ST_PARSE : (int32_t)ST_OK;
+  }
+  if (!ok) st = ST_CKSUM;  // (not reached: a unit that never finished)
+  if (lane == 0) gstore(P.status, r->b, st);
+}
+
 template <bool kAllFields>
-__global__ __launch_bounds__(256) void decode_huge_kernel(DecodeParams P) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void decode_huge_kernel(DecodeParams P, uint32_t chain_wgs) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   uint8_t* stage = smem + 64;
   uint32_t* cnt = reinterpret_cast<uint32_t*>(smem);  // [0, 1]: search counts; [2..]: per-wave partials
@@ -1276,16 +1366,31 @@ __global__ __launch_bounds__(256) void decode_huge_kernel(DecodeParams P) {
   const uint32_t n = hp->n3;
   if (!n) return;
   const HugeLayout L = huge_layout(P, n);
-  const uint32_t units = hp->total_pu;
   const uint32_t tid = threadIdx.x, lane = tid & 63;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(tid / kWave);
   const bool hash = !(P.flags & LSM_DECODE_PAYLOAD_VERIFIED);
-  // a run of consecutive units per workgroup: one block search per run, and a
-  // window's first interval is the previous window's end (the same bound)
-  const uint32_t per = (units + gridDim.x - 1) / gridDim.x;
-  const uint32_t u_begin = blockIdx.x * per, u_end = min(units, u_begin + per);
-  uint32_t i = u_begin < u_end ? last_le(L.ppre, n, u_begin) : 0;
-  uint32_t carry_u = 0xFFFFFFFFu, carry_r = 0;  // unit whose r1 search answer is carry_r (block i)
+  const bool stream = hp->stream != 0;
+  if (blockIdx.x < chain_wgs) {
+    if (!stream) return;  // (decode_huge_chain_kernel runs the chains after this kernel)
+    // chain workgroups (dispatched first): wave q = 4 g + w takes blocks q, q + 4 chain_wgs, ...
+    uint8_t* ring = smem + 64 + wave * kStreamRing * 1024;
+    for (uint32_t i = 4 * blockIdx.x + wave; i < n; i += 4 * chain_wgs)
+      if (L.rec[i].accepted) huge_chain_streamed(P, L, i, ring);
+    return;
+  }
+  // Unit order: batches of B = 4 chain_wgs blocks (one per chain wave), window-major
+  // inside a batch: virtual unit v = (batch, window c, block in batch), so the blocks
+  // of a batch progress together, each chain streams behind its own, and a chain
+  // wave's next block (the next batch) is produced while it finishes this one.
+  // Without streaming: a run of consecutive units per workgroup (one block search
+  // per run, and a window's first interval is the previous window's end).
+  const uint32_t pgrid = gridDim.x - chain_wgs, pb = blockIdx.x - chain_wgs;
+  const uint32_t B = 4 * chain_wgs, mx = hp->max_npu;
+  const uint64_t vtot = stream ? (uint64_t)((n + B - 1) / B) * B * mx : hp->total_pu;
+  const uint64_t per = (vtot + pgrid - 1) / pgrid;
+  const uint64_t v_begin = (uint64_t)pb * per, v_end = min(vtot, v_begin + per);
+  uint32_t iseq = !stream && v_begin < v_end ? last_le(L.ppre, n, v_begin) : 0;
+  uint32_t carry_u = 0xFFFFFFFFu, carry_r = 0;  // unit whose r1 search answer is carry_r (block iseq)
 #if defined(LSM_DIAG) && !defined(LSM_DIAG_NOTIME)
   // diagnostic builds: per-phase s_memtime totals of wave 0 (g_dec_phase[8..13], units in [14])
   uint64_t t_last = __builtin_amdgcn_s_memtime(), ph[8] = {};
@@ -1294,16 +1399,33 @@ __global__ __launch_bounds__(256) void decode_huge_kernel(DecodeParams P) {
 #else
 #define HUGE_PHASE(k)
 #endif
-  for (uint32_t u = u_begin; u < u_end; ++u) {
+  uint32_t pending = ~0u;  // a processed unit whose done flag is not yet published
+  for (uint64_t v = v_begin; v < v_end; ++v) {
     HUGE_PHASE(6);
-    while (i + 1 < n && gload(L.ppre, i + 1) <= u) ++i, carry_u = 0xFFFFFFFFu;
+    uint32_t i, wc;
+    uint64_t ub;
+    if (stream) {
+      const uint64_t bw = (uint64_t)B * mx, rem = v % bw;
+      i = (uint32_t)(v / bw) * B + (uint32_t)(rem % B);
+      wc = (uint32_t)(rem / B);
+      if (i >= n) continue;
+      if (!L.rec[i].accepted) continue;  // (uniform)
+      ub = gload(L.ppre, i);
+      if (wc >= gload(L.ppre, i + 1) - ub) continue;  // the block has fewer windows
+    } else {
+      while (iseq + 1 < n && gload(L.ppre, iseq + 1) <= v) ++iseq, carry_u = 0xFFFFFFFFu;
+      i = iseq;
+      if (!L.rec[i].accepted) continue;
+      ub = gload(L.ppre, i);
+      wc = (uint32_t)(v - ub);
+    }
     const HugeRec* r = L.rec + i;
-    if (!r->accepted) continue;  // (uniform)
+    const uint32_t u = (uint32_t)(ub + wc);
     const BlockMeta m = r->m;
     const TrailerInfo t = trailer_of(m);
     const uint32_t span = r->span;
     const uint8_t* gbase = P.blocks + r->span0;
-    const uint32_t cs = (uint32_t)(u - gload(L.ppre, i)) * kHugeWin;
+    const uint32_t cs = wc * kHugeWin;
     const uint32_t ce = min(cs + kHugeWin, span), ss = min(ce + kHugeOverlap, span);
     {  // stage [cs, ss): wave w moves 1-KiB pieces w, w + 4, ...
       const uint32_t chunks = (ss - cs + 15) >> 4;
@@ -1318,9 +1440,9 @@ __global__ __launch_bounds__(256) void decode_huge_kernel(DecodeParams P) {
     const bool table = !r->nonmono;
     uint32_t r0 = 0, r1 = 0, stop1 = 0;  // stop1: payload offset where the window's last interval ends
     if (parse && table) {
-      const uint2 e0 = L.uend[-1 - (int64_t)u];
+      const uint4 e0 = L.uend[-1 - (int64_t)u];
       const bool last = ce == span;
-      const uint2 e1 = last ? make_uint2(t.bin_len, t.rec_end) : L.uend[-2 - (int64_t)u];
+      const uint2 e1 = last ? make_uint2(t.bin_len, t.rec_end) : make_uint2(L.uend[-2 - (int64_t)u].x, L.uend[-2 - (int64_t)u].y);
       r0 = cs == 0 ? 0 : e0.x;
       r1 = last ? t.bin_len : e1.x;
       stop1 = e1.y;
@@ -1357,7 +1479,7 @@ __global__ __launch_bounds__(256) void decode_huge_kernel(DecodeParams P) {
       // at least once even when the binary index is not monotone (its walk then fails)
       r0 = cs == 0 ? 0 : lo0;
       r1 = ce == span ? nint : lo1;
-      carry_u = u;
+      carry_u = stream ? 0xFFFFFFFFu : u;  // (streaming: the next unit is another block's)
       carry_r = lo1;
     }
     const uint8_t* sbase = reinterpret_cast<const uint8_t*>(reinterpret_cast<uintptr_t>(stage) - cs);  // span-relative
@@ -1407,6 +1529,8 @@ __global__ __launch_bounds__(256) void decode_huge_kernel(DecodeParams P) {
       HUGE_PHASE(1);
       vm_wait<0>();
       lds_barrier();
+      if (tid == 0 && pending != ~0u)  // (streaming) the previous unit: its stores have completed (vmcnt(0) above)
+        __hip_atomic_store(&L.uend[-1 - (int64_t)pending].z, P.huge_tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       HUGE_PHASE(2);
       // phase A (serial LDS walks: latency) on wave 0, the contributions (VALU) on the
       // other waves meanwhile; without phase A on all four
@@ -1418,9 +1542,14 @@ __global__ __launch_bounds__(256) void decode_huge_kernel(DecodeParams P) {
         const uint32_t nbk = r->nbk;
         const uint32_t n0 = min(nbk, cs > p0 ? (cs - p0 + 1023) / 1024 : 0u);
         const uint32_t n1 = min(nbk, ce > p0 ? (ce - p0 + 1023) / 1024 : 0u);
-        if (n1 > n0)
-          xxh3_kib_contribs(stage, p0 + 1024 * n0 - cs, (n1 - n0) * 1024 + 1, &kLongSecret,
-                            L.contrib + 8 * (gload(L.kpre, i) + n0), split ? wave - 1 : wave, split ? 3 : 4);
+        if (n1 > n0) {  // (streaming: agent-scope stores, read by a chain wave of this launch)
+          if (stream)
+            xxh3_kib_contribs<true, true>(stage, p0 + 1024 * n0 - cs, (n1 - n0) * 1024 + 1, &kLongSecret,
+                                          L.contrib + 8 * (gload(L.kpre, i) + n0), split ? wave - 1 : wave, split ? 3 : 4);
+          else
+            xxh3_kib_contribs(stage, p0 + 1024 * n0 - cs, (n1 - n0) * 1024 + 1, &kLongSecret,
+                              L.contrib + 8 * (gload(L.kpre, i) + n0), split ? wave - 1 : wave, split ? 3 : 4);
+        }
       }
       HUGE_PHASE(4);
       bool walk = !fast;
@@ -1449,18 +1578,33 @@ __global__ __launch_bounds__(256) void decode_huge_kernel(DecodeParams P) {
     } else if (hash && r->nbk) {
       vm_wait<0>();
       lds_barrier();
+      if (tid == 0 && pending != ~0u)  // (streaming) the previous unit: its stores have completed (vmcnt(0) above)
+        __hip_atomic_store(&L.uend[-1 - (int64_t)pending].z, P.huge_tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
       const uint32_t p0 = m.p0, nbk = r->nbk;
       const uint32_t n0 = min(nbk, cs > p0 ? (cs - p0 + 1023) / 1024 : 0u);
       const uint32_t n1 = min(nbk, ce > p0 ? (ce - p0 + 1023) / 1024 : 0u);
-      if (n1 > n0)
-        xxh3_kib_contribs(stage, p0 + 1024 * n0 - cs, (n1 - n0) * 1024 + 1, &kLongSecret,
-                          L.contrib + 8 * (gload(L.kpre, i) + n0), wave, 4);
+      if (n1 > n0) {
+        if (stream)
+          xxh3_kib_contribs<true, true>(stage, p0 + 1024 * n0 - cs, (n1 - n0) * 1024 + 1, &kLongSecret,
+                                        L.contrib + 8 * (gload(L.kpre, i) + n0), wave, 4);
+        else
+          xxh3_kib_contribs(stage, p0 + 1024 * n0 - cs, (n1 - n0) * 1024 + 1, &kLongSecret,
+                            L.contrib + 8 * (gload(L.kpre, i) + n0), wave, 4);
+      }
     }
     HUGE_PHASE(5);
     lds_barrier();  // (the next unit rewrites the stage)
+    // published after the next unit's DMA wait (vmcnt(0): this unit's contribution
+    // stores and parse_bad update have completed by then), or after the loop
+    if (stream) pending = u;
 #if defined(LSM_DIAG) && !defined(LSM_DIAG_NOTIME)
     ++nunits;
 #endif
+  }
+  if (pending != ~0u) {
+    vm_wait<0>();
+    lds_barrier();
+    if (tid == 0) __hip_atomic_store(&L.uend[-1 - (int64_t)pending].z, P.huge_tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
 #if defined(LSM_DIAG) && !defined(LSM_DIAG_NOTIME)
   if (threadIdx.x == 0) {
@@ -1471,17 +1615,17 @@ __global__ __launch_bounds__(256) void decode_huge_kernel(DecodeParams P) {
 #undef HUGE_PHASE
 }
 
-// Chains of the huge blocks: a single-wave workgroup per block, its eight
-// accumulators on lanes 0..7 (xxh3_chain8), then on the same wave the tail
-// merge, the checksum compare and the status (oracle order: payload checksum,
-// then trailer, then parse).  The contributions cross a kernel boundary (an
-// agent-scope fence per unit would write back the XCD's whole L2); the chain
-// results stay in the wave, so the merge needs no second kernel.
+// Chains of the huge blocks when they do not stream (decode_huge_kernel's
+// chain workgroups took them otherwise): a single-wave workgroup per block,
+// its eight accumulators on lanes 0..7 (xxh3_chain8), then on the same wave
+// the tail merge, the checksum compare and the status (oracle order: payload
+// checksum, then trailer, then parse).  The contributions cross a kernel
+// boundary here; the chain results stay in the wave.
 __global__ __launch_bounds__(64) void decode_huge_chain_kernel(DecodeParams P) {
   __shared__ __attribute__((aligned(16))) uint8_t ring[kChainRing * 1024];
   const HugeHdr* hp = reinterpret_cast<const HugeHdr*>(P.huge_pool);
   const uint32_t n = hp->n3;
-  if (!n) return;
+  if (!n || hp->stream) return;
   const HugeLayout L = huge_layout(P, n);
   const bool hash = !(P.flags & LSM_DECODE_PAYLOAD_VERIFIED);
   const uint32_t lane = threadIdx.x & 63, k = lane & 7, q = lane & 3;
@@ -1745,8 +1889,8 @@ size_t decode_workspace_size(uint32_t n_blocks) {
 size_t decode_workspace_size_ex(uint32_t n_blocks, uint64_t blocks_bytes) {
   const uint64_t most = blocks_bytes / kBigStage + 1;
   const uint64_t n3 = most < n_blocks ? most : n_blocks;
-  return decode_workspace_size(n_blocks) + huge_fixed_bytes(n3) + 64 * (blocks_bytes / 1024 + 1) +
-         8 * (blocks_bytes / kHugeWin + n3 + 1) + 256;
+  return decode_workspace_size(n_blocks) + huge_fixed_bytes(n3) + 64 * (blocks_bytes / 1024 + 1 + 16 * n3) +
+         16 * (blocks_bytes / kHugeWin + n3 + 1) + 256;
 }
 
 uint32_t decode_lds_bytes(uint32_t stage_bytes, uint32_t tile_items, uint32_t blocks_per_wave) {
@@ -1827,12 +1971,16 @@ hipError_t launch_decode(const DecodeParams& P0, void* ws, size_t ws_bytes, hipS
     hipLaunchKernelGGL(decode_deferred_staged_kernel, dim3(dgrid), dim3(kBigWaves * kWave), big, st, P2);
   }
   if (P.huge_pool && bgrid) {
+    P.huge_tag = 1;  // (the units kernel clears the flags first)
     const void* hk = all ? (const void*)decode_huge_kernel<true> : (const void*)decode_huge_kernel<false>;
     static uint64_t done_hk[2] = {};
     if ((e = set_lds_attr(hk, kHugeLds, &done_hk[all ? 1 : 0])) != hipSuccess) return e;
     hipLaunchKernelGGL(decode_huge_units_kernel, dim3(kHugeUnitsGrid), dim3(256), 0, st, P);
-    if ((e = hipLaunchKernel(hk, dim3(kHugeGrid), dim3(256), args, kHugeLds, st)) != hipSuccess) return e;
-    hipLaunchKernelGGL(decode_huge_chain_kernel, dim3(kHugeChainGrid), dim3(64), 0, st, P);
+    // chain workgroups first (four blocks each, at most one per CU), then the units
+    uint32_t chain_wgs = min((P.n_blocks + 3) / 4, kStreamChainWgs);
+    void* hargs[] = {&P, &chain_wgs};
+    if ((e = hipLaunchKernel(hk, dim3(chain_wgs + kHugeGrid), dim3(256), hargs, kHugeLds, st)) != hipSuccess) return e;
+    hipLaunchKernelGGL(decode_huge_chain_kernel, dim3(kHugeChainGrid), dim3(64), 0, st, P);  // (returns at once when streamed)
   }
   return hipGetLastError();
 }

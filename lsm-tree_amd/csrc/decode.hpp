@@ -42,6 +42,7 @@ struct DecodeParams {
   uint64_t huge_pool_bytes;
   uint64_t seqno_add;     // added to every decoded seqno (Scanner's global_seqno, scanner.rs:84)
   uint32_t compact;       // lsm_decode_blocks16: out.key_off / val_off / val_len are uint16_t arrays
+  uint32_t huge_tag;      // this call's tag for the huge path's unit-done flags (never 0)
 };
 
 // Diagnostic builds (-DLSM_DIAG, `make variant`) honour ablation bits in

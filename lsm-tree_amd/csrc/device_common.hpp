@@ -569,7 +569,7 @@ __device__ __forceinline__ uint64_t pair_swap_sum64(uint64_t a, uint64_t b) {
 // permlane16 swaps (each halves the values a lane holds), then DPP row
 // rotates (kB = 8: bit 3 a scatter, bit 2 a sum; kB = 4: both sums): about
 // 10 VALU per KiB block against 32 for a quad_group_sum64 pair.
-template <int kB, bool kLds>
+template <int kB, bool kLds, bool kAgent = false>
 __device__ __forceinline__ void xxh3_kib_contribs_b(const uint8_t* base, uint32_t pos, uint32_t n0, uint32_t cnt,
                                                     uint64_t k0, uint64_t k1, uint64_t* contrib) {
   static_assert(kB == 4 || kB == 8, "batch");
@@ -616,8 +616,13 @@ __device__ __forceinline__ void xxh3_kib_contribs_b(const uint8_t* base, uint32_
   x1 += u64_of(dpp_ror4((uint32_t)x1), dpp_ror4((uint32_t)(x1 >> 32)));
   const bool st = kB == 8 ? (lane & 4) != 0 : (lane & 12) == 4;
   if (st && n < cnt) {
-    contrib[8 * (uint64_t)(n0 + n) + 2 * q] = x0;
-    contrib[8 * (uint64_t)(n0 + n) + 2 * q + 1] = x1;
+    if (kAgent) {  // agent-scope stores (written through the XCD's L2): read by another XCD in this launch
+      __hip_atomic_store(&contrib[8 * (uint64_t)(n0 + n) + 2 * q], x0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+      __hip_atomic_store(&contrib[8 * (uint64_t)(n0 + n) + 2 * q + 1], x1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    } else {
+      contrib[8 * (uint64_t)(n0 + n) + 2 * q] = x0;
+      contrib[8 * (uint64_t)(n0 + n) + 2 * q + 1] = x1;
+    }
   }
 }
 
@@ -629,7 +634,7 @@ __device__ __forceinline__ void xxh3_kib_contribs_b(const uint8_t* base, uint32_
 // (xxh3_128_wave_finish).  len > 240; kLds: base is LDS.  With `ready`, KiB block n's
 // contribution is published to a concurrent xxh3_128_wave_finish by
 // ready[n] = tag (LDS, workgroup release).
-template <bool kLds = true>
+template <bool kLds = true, bool kAgent = false>
 __device__ __forceinline__ void xxh3_kib_contribs(const uint8_t* base, uint32_t pos, uint32_t len,
                                                   const LongSecret* __restrict__ ls, uint64_t* contrib, uint32_t w,
                                                   uint32_t nw, uint32_t* ready = nullptr, uint32_t tag = 0) {
@@ -640,7 +645,7 @@ __device__ __forceinline__ void xxh3_kib_contribs(const uint8_t* base, uint32_t 
   constexpr uint32_t B = 4;
   for (uint32_t n0 = B * w; n0 < nb_blocks; n0 += B * nw) {
     const uint32_t cnt = min(B, nb_blocks - n0);
-    xxh3_kib_contribs_b<B, kLds>(base, pos, n0, cnt, k0, k1, contrib);
+    xxh3_kib_contribs_b<B, kLds, kAgent>(base, pos, n0, cnt, k0, k1, contrib);
     if (ready) {
       __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
       if ((uint32_t)lane < cnt) __hip_atomic_store(&ready[n0 + lane], tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -750,9 +755,14 @@ __device__ __forceinline__ uint64_t xxh3_chain_wave(const uint64_t* __restrict__
 // LDS), 16 rows per wave instruction, kRing instructions in flight (counted
 // vmcnt, lds_dma.hpp), and each lane reads its accumulator's word with one
 // ds_read_b64 per step, a chunk ahead of its steps.
-template <uint32_t kRing = 16>
+struct ChainNoWait {
+  __device__ __forceinline__ void operator()(uint64_t) const {}
+};
+// wait(q): called (wave-uniform) before chunk q's rows are fetched; a caller
+// whose rows are produced in the same launch waits there until they are.
+template <uint32_t kRing = 16, class Wait = ChainNoWait>
 __device__ __forceinline__ uint64_t xxh3_chain8(const uint64_t* __restrict__ c, uint64_t n_in, uint64_t acc, uint64_t s,
-                                                uint8_t* ring) {
+                                                uint8_t* ring, Wait wait = Wait{}) {
   static_assert(kRing >= 2 && kRing <= 32, "chunks in flight");
   const uint32_t lane = threadIdx.x & 63, k = lane & 7;
   const uint32_t s_lo = (uint32_t)s, s_hi = (uint32_t)(s >> 32);
@@ -766,6 +776,7 @@ __device__ __forceinline__ uint64_t xxh3_chain8(const uint64_t* __restrict__ c, 
   const uint32_t rbase = (uint32_t)(uintptr_t)(__attribute__((address_space(3))) uint8_t*)ring;
   auto dma = [&](uint64_t q, uint32_t slot) {  // (past the last chunk: the last one again, so the count stays)
     const uint64_t qq = q < nc ? q : nc - 1;
+    if (q < nc) wait(qq);
     if (16 * qq + lane / 4 < n) dma16<false>(src + 1024 * qq + 16 * lane, rbase + 1024 * slot);
   };
   const __attribute__((address_space(3))) uint64_t* rw =
