@@ -148,6 +148,38 @@ def test_huge_blocks_long_chains(gpu, pool):
     compare_decode(g, parsed, item_start, status)
 
 
+def test_streamed_chains_pool_reuse(gpu):
+    """Batches holding blocks of >= 2 MiB stream their XXH3 chains behind the
+    parse units (unit-done flags in the pool).  One Decoder, so one pool, reused
+    across calls with different blocks, statuses and expected types: a flag left
+    by an earlier call must never pass for this call's (blocks whose trailer
+    fails, or whose type differs, are hashed but not parsed)."""
+    import torch
+    items = counter_items(2 * 52429 + 3300, seed=17, tomb_frac=0.02)
+    starts = np.array([0, 52429, 55729, 2 * 52429 + 3300], np.uint32)  # ~3.7 MiB, ~230 KiB, ~3.5 MiB
+    buf, off = pyoracle.encode_blocks(items, starts)
+    blocks = [bytes(buf[int(off[i]):int(off[i + 1])]) for i in range(3)]
+    assert len(blocks[0]) > 2 * 1024 * 1024 and len(blocks[2]) > 2 * 1024 * 1024
+    bad_ck = bytearray(blocks[2]); bad_ck[33 + 1_000_000] ^= 0x04
+    late = bytearray(blocks[0][33:]); late[-4] += 1
+    batches = [pack(blocks), pack([blocks[0], blocks[1], bytes(bad_ck)]),
+               pack([pyoracle.block_write(bytes(late), 0), blocks[1], blocks[2]]), pack(blocks)]
+    dec = gpu.Decoder()
+    for buf2, off2 in batches:
+        for et in (-1, 1, -1):
+            n = len(off2) - 1
+            d_blocks = gpu.to_device_bytes(buf2)
+            d_off = torch.from_numpy(off2.astype(np.int64)).cuda()
+            cap = len(buf2) // 3 + 1
+            out = dec.alloc_outputs(cap, n)
+            res = dec.decode(d_blocks, d_off, n, out, cap, et, pool=True)
+            torch.cuda.synchronize()
+            g = {k: v.cpu().numpy() for k, v in res.items()}
+            g["status"] = g["status"][:n]
+            parsed, item_start, status = pyoracle.decode_blocks(buf2, off2, expect_type=et)
+            compare_decode(g, parsed, item_start, status)
+
+
 def _mixed_batch(seed=5):
     """48 blocks of 80-400 KiB between 4 KiB blocks, and corrupted copies of
     some: header checksum (HDR_CKSUM), payload bit (CKSUM), broken record
