@@ -24,6 +24,7 @@
 
 #include "block_format.hpp"
 #include "decode.hpp"
+#include "fill.hpp"
 #include "lds_dma.hpp"
 #include "scan.hpp"
 
@@ -1915,7 +1916,7 @@ hipError_t launch_decode(const DecodeParams& P0, void* ws, size_t ws_bytes, hipS
   static_assert(huge_fixed_bytes(1) + 64 * 128 == 8704, "the threshold lsmgpu.h documents");
   P.huge_pool = ws_bytes >= pool0 + huge_fixed_bytes(1) + 64 * 128 ? (uint8_t*)ws + pool0 : nullptr;
   P.huge_pool_bytes = P.huge_pool ? ws_bytes - pool0 : 0;
-  hipError_t e = hipMemsetAsync(dws, 0, 16, st);
+  hipError_t e = fill_words_async(dws, 4, 0, st);
   if (e != hipSuccess) return e;
   if (!(P.flags & LSM_DECODE_ITEM_START_VALID)) {
     hipLaunchKernelGGL(trailer_counts_kernel, dim3((P.n_blocks + 255) / 256), dim3(256), 0, st, P.blocks,

@@ -31,6 +31,7 @@
 #include "decode.hpp"
 #include "encode.hpp"
 #include "scan.hpp"
+#include "fill.hpp"
 
 namespace lsmgpu {
 
@@ -2376,9 +2377,10 @@ __global__ __launch_bounds__(kE3Threads) void encode_large_kernel(EncodeParams P
 //            trailer)
 //            (the contributions of the KiB blocks wholly inside a unit's LDS
 //            image come from the image, flagged done)
-//   hash     XXH3 contributions of the other KiB blocks into the pool
-//   chain    one wave per block: the eight accumulator chains on lanes 0..7,
-//            then the tail merge, the header and the status
+//   chain    a workgroup per block: three waves hash the KiB blocks the
+//            records kernel left into the pool while the fourth runs the eight
+//            accumulator chains on lanes 0..7 behind them, then the tail merge,
+//            the header and the status
 constexpr uint32_t kEHugeItems = 1024;  // items per record unit, at most (four per thread)
 constexpr uint32_t kEHugeImg = 2 * 4 * kE3HashChunk;  // LDS image of a record unit (the tail unit's vote arrays)
 constexpr uint32_t kEHugeGrid = 2048;
@@ -2668,100 +2670,86 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
 #undef REC_PHASE
 }
 
-// The contributions the records kernel left (KiB blocks across two record
-// units or into the index / trailer, units over the LDS image, one-pass
-// blocks): a workgroup per range of kECRange KiB blocks reads their done
-// flags, lists the others in LDS and hashes them from the written payloads,
-// four per wave at a time (block lookup in an LDS copy of kpre).
-constexpr uint32_t kECRange = 256;
-constexpr uint32_t kECKpre = 2048;  // kpre entries staged in LDS (more blocks: the lookup reads HBM)
-__global__ __launch_bounds__(256) void encode_huge_contrib_kernel(EncodeParams P) {
-  __shared__ uint64_t kp[kECKpre + 1];
-  __shared__ uint32_t todo[kECRange];
-  __shared__ uint32_t ntodo;
-  const EncHugeLayout L = enc_huge_layout(P);
-  const uint32_t n3 = L.hdr->n3;
-  if (!n3) return;
-  const uint64_t tk = min(L.hdr->total_kib, L.cap_kib);  // (accepted blocks' KiB numbers are below cap_kib)
-  if ((uint64_t)blockIdx.x * kECRange >= tk) return;
-  const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-  const int q = lane & 3, sq = lane >> 2;
-  const uint64_t k0 = kLongSecret.acc[sq + 2 * q], k1 = kLongSecret.acc[sq + 2 * q + 1];
-  const bool lds_kp = n3 <= kECKpre;
-  if (lds_kp)
-    for (uint32_t x = tid; x <= n3; x += 256) kp[x] = L.kpre[x];
-  auto kpre = [&](uint32_t x) { return lds_kp ? kp[x] : L.kpre[x]; };
-  for (uint64_t G0 = (uint64_t)blockIdx.x * kECRange; G0 < tk; G0 += (uint64_t)gridDim.x * kECRange) {
-    if (tid == 0) ntodo = 0;
-    __syncthreads();
-    for (uint32_t x = tid; x < kECRange; x += 256) {
-      const uint64_t g = G0 + x;
-      if (g < tk && !L.kdone[g]) todo[atomicAdd(&ntodo, 1u)] = x;
-    }
-    __syncthreads();
-    const uint32_t nt = ntodo;
-    for (uint32_t t0 = 4 * wave; t0 < nt; t0 += 16) {
-      uint64_t g[4];
-      uint32_t bi[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        g[j] = t0 + j < nt ? G0 + todo[t0 + j] : G0 + todo[t0];
-        uint32_t lo = 0, hi = n3;  // the last block i with kpre[i] <= g
-        while (hi - lo > 1) {
-          const uint32_t mid = (lo + hi) >> 1;
-          if (kpre(mid) <= g[j]) lo = mid;
-          else hi = mid;
-        }
-        bi[j] = lo;
-      }
-      bool live[4];
-      const uint8_t* base[4];
-      uint32_t pos[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        const EncHuge* r = L.rec + bi[j];
-        live[j] = t0 + j < nt && r->accepted != 0;
-        const uint64_t dabs = (uint64_t)(uintptr_t)P.out + r->dst_off;
-        base[j] = reinterpret_cast<const uint8_t*>(dabs & ~15ULL);
-        pos[j] = (uint32_t)(dabs & 15) + kHdrLen + (uint32_t)(g[j] - kpre(bi[j])) * 1024 + 16 * lane;
-      }
-      Win16 w[4];
-#pragma unroll
-      for (int j = 0; j < 4; ++j) w[j] = live[j] ? read_win16(base[j], pos[j]) : Win16{0, 0};
-#pragma unroll
-      for (int j = 0; j < 4; ++j) {
-        uint64_t c0 = 0, c1 = 0;
-        stripe_part(w[j], k0, k1, c0, c1);
-        c0 = quad_group_sum64(c0);
-        c1 = quad_group_sum64(c1);
-        if (live[j] && lane < 4) {
-          L.contrib[8 * g[j] + 2 * q] = c0;
-          L.contrib[8 * g[j] + 2 * q + 1] = c1;
-        }
-      }
-    }
-    __syncthreads();  // (todo / ntodo are rewritten for the next range)
-  }
-}
-
-// A single-wave workgroup per block, its eight accumulators on lanes 0..7
-// (xxh3_chain8), then on the same wave the tail merge, the header
-// (Header::encode_into) and the status.  The contributions cross a kernel
-// boundary (an agent-scope fence per unit would write back the XCD's whole L2).
+// A four-wave workgroup per block.  Waves 1..3 hash the KiB blocks the records
+// kernel left (kdone clear: across two record units, into the index / trailer,
+// units over the LDS image, one-pass blocks) from the written payload: helper h
+// takes the 64-row chunks h, h + 3, ... in order and publishes each in LDS.
+// Wave 0 runs the eight accumulator chains on lanes 0..7 (xxh3_chain8), fetching
+// a chunk's rows once its helper has published it, then the tail merge, the
+// header (Header::encode_into) and the status.  The contributions cross a
+// kernel boundary (an agent-scope fence per unit would write back the XCD's
+// whole L2).
 constexpr uint32_t kEChainRing = 16;
-__global__ __launch_bounds__(64) void encode_huge_chain_kernel(EncodeParams P) {
+constexpr uint32_t kEChainHelpers = 3;
+__global__ __launch_bounds__(256) void encode_huge_chain_kernel(EncodeParams P) {
   __shared__ __attribute__((aligned(16))) uint8_t ring[kEChainRing * 1024];
+  __shared__ uint32_t prog[4];  // helper h: 64-row chunks of this block done (h, h + 3, ... in order)
   const EncHugeLayout L = enc_huge_layout(P);
   const uint32_t n3 = L.hdr->n3;
   if (!n3) return;
-  const uint32_t lane = threadIdx.x & 63, k = lane & 7, q = lane & 3;
+  const uint32_t tid = threadIdx.x, lane = tid & 63, k = lane & 7, q = lane & 3;
+  const uint32_t wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+  if (tid < 4) prog[tid] = 0;
+  __syncthreads();
   for (uint32_t i = blockIdx.x; i < n3; i += gridDim.x) {
     const EncHuge* r = L.rec + i;
-    if (!r->accepted) continue;
+    if (!r->accepted) continue;  // (uniform)
+    const uint32_t nbk = r->nbk;
+    const uint64_t kp = L.kpre[i];
+    if (wave > 0) {
+      const uint32_t h = wave - 1;
+      const uint64_t dabs = (uint64_t)(uintptr_t)P.out + r->dst_off;
+      const uint8_t* img = reinterpret_cast<const uint8_t*>(dabs & ~15ULL);
+      const uint32_t p0 = (uint32_t)(dabs & 15) + kHdrLen;
+      const uint64_t k0 = kLongSecret.acc[(lane >> 2) + 2 * q], k1 = kLongSecret.acc[(lane >> 2) + 2 * q + 1];
+      uint32_t done = 0;
+      for (uint32_t c = h; 64 * c < nbk; c += kEChainHelpers) {
+        const uint32_t g = 64 * c + lane;
+        uint64_t m = __ballot(g < nbk && !L.kdone[kp + g]);
+        while (m) {  // four rows at a time (independent loads and sums)
+          uint32_t gs[4];
+          bool live[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            live[j] = m != 0;
+            gs[j] = live[j] ? 64 * c + (uint32_t)__builtin_ctzll(m) : 64 * c;
+            m &= m - 1;
+          }
+          Win16 w[4];
+#pragma unroll
+          for (int j = 0; j < 4; ++j) w[j] = live[j] ? read_win16(img, p0 + 1024 * gs[j] + 16 * lane) : Win16{0, 0};
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            uint64_t c0 = 0, c1 = 0;
+            stripe_part(w[j], k0, k1, c0, c1);
+            c0 = quad_group_sum64(c0);
+            c1 = quad_group_sum64(c1);
+            if (live[j] && lane < 4) {
+              L.contrib[8 * (kp + gs[j]) + 2 * q] = c0;
+              L.contrib[8 * (kp + gs[j]) + 2 * q + 1] = c1;
+            }
+          }
+        }
+        vm_wait<0>();  // (the rows' stores, before the chain wave's DMA reads them)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup");
+        if (lane == 0) __hip_atomic_store(&prog[h], ++done, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+      }
+      __syncthreads();  // (the chain wave's end of this block)
+      __syncthreads();
+      continue;
+    }
     uint64_t a0, a1;
     xxh3_acc_init((int)(k >> 1), a0, a1);
     uint64_t x = (k & 1) ? a1 : a0;
-    if (r->nbk) x = xxh3_chain8<kEChainRing>(L.contrib + 8 * L.kpre[i], r->nbk, x, kLongSecret.acc[16 + k], ring);
+    // chunk qq of 16 rows lies in 64-row chunk qq / 4, helper (qq / 4) % 3's (qq / 4) / 3 + 1-th
+    auto wait = [&](uint64_t qq) {
+      const uint32_t c = (uint32_t)(qq / 4);
+      while (__hip_atomic_load(&prog[c % kEChainHelpers], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP) <
+             c / kEChainHelpers + 1)
+        __builtin_amdgcn_s_sleep(1);
+      __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "workgroup");
+    };
+    if (nbk) x = xxh3_chain8<kEChainRing>(L.contrib + 8 * kp, nbk, x, kLongSecret.acc[16 + k], ring, wait);
     // lane quad position q takes accumulators 2q, 2q + 1 (lanes 2q, 2q + 1 hold them)
     const uint64_t c0 = wave_shfl_u64(x, (int)(2 * q)), c1 = wave_shfl_u64(x, (int)(2 * q + 1));
     const uint64_t dabs = (uint64_t)(uintptr_t)P.out + r->dst_off;
@@ -2771,6 +2759,9 @@ __global__ __launch_bounds__(64) void encode_huge_chain_kernel(EncodeParams P) {
     xxh3_wave_tail_merge(img, pad + kHdrLen, plen, &kLongSecret, c0, c1, lo, hi);
     write_header_bytes(img, pad, P.type, lo, hi, plen);
     if (lane == 0) P.status[r->b] = ST_OK;
+    __syncthreads();  // every helper is past its last chunk of this block
+    if (lane < 4) prog[lane] = 0;
+    __syncthreads();
   }
 }
 
@@ -2897,7 +2888,7 @@ hipError_t launch_encode(const lsm_items& items, const uint32_t* starts, uint32_
     P.huge_pool = pool ? (uint8_t*)ws + base : nullptr;
     P.huge_pool_bytes = pool ? ws_bytes - base : 0;
     P.huge_cap = pool ? (uint32_t)cap : 0;
-    if (pool && (e = hipMemsetAsync(P.huge_pool, 0, 256, st)) != hipSuccess) return e;
+    if (pool && (e = fill_words_async(P.huge_pool, 64, 0, st)) != hipSuccess) return e;
     // (with a pool the E1p flag sits in the cleared pool header: one memset launch, not two)
     if (pool) P.e1p_flag = reinterpret_cast<uint32_t*>(P.huge_pool + 128);
   }
@@ -2908,7 +2899,7 @@ hipError_t launch_encode(const lsm_items& items, const uint32_t* starts, uint32_
   const bool e1p = P.type != 1 && P.plan_bpw <= kE1pMaxBpw && items.n_items > 0 && items.n_items < 0xFFFFFFFFull;
   if (e1p) {  // batches of huge blocks: the plan item-parallel
     P.hb_sh = 1;
-    if (!P.huge_pool && (e = hipMemsetAsync(P.e1p_flag, 0, 4, st)) != hipSuccess) return e;
+    if (!P.huge_pool && (e = fill_words_async(P.e1p_flag, 1, 0, st)) != hipSuccess) return e;
     const dim3 igrid((uint32_t)((items.n_items + 256 * kE1pPer - 1) / (256 * kE1pPer)));
     const dim3 lgrid((uint32_t)((items.n_items + 256 * kE1pLenPer - 1) / (256 * kE1pLenPer)));
     hipLaunchKernelGGL(encode_e1p_lengths_kernel, lgrid, dim3(256), 0, st, P);
@@ -2923,7 +2914,7 @@ hipError_t launch_encode(const lsm_items& items, const uint32_t* starts, uint32_
   // per workgroup most waves would idle, so those batches keep the workgroup walk)
   else if (P.plan_bpw >= 16 && P.ratio > 0.0f) {  // (only this plan kernel fills hbucket)
     P.hb_valid = 1;
-    if ((e = hipMemsetAsync(P.hb_fix, 0, 4, st)) != hipSuccess) return e;
+    if ((e = fill_words_async(P.hb_fix, 1, 0, st)) != hipSuccess) return e;
     hipLaunchKernelGGL(encode_plan_wave_kernel<true>, pgrid, dim3(256), 0, st, P);
     hipLaunchKernelGGL(encode_bucket_fixup_kernel, dim3(1024), dim3(256), 0, st, P);
   } else if (P.plan_bpw >= 16)
@@ -2939,6 +2930,9 @@ hipError_t launch_encode(const lsm_items& items, const uint32_t* starts, uint32_
   if ((e = launch_excl_scan(P.sizes, n_blocks, tiles, oo, st)) != hipSuccess) return e;
   static uint64_t attr_done = 0;
   if ((e = set_lds_attr((const void*)encode_write_list_kernel, kImgBig, &attr_done)) != hipSuccess) return e;
+  static uint64_t attr_mw = 0;
+  if ((e = set_lds_attr((const void*)encode_write_list_mw_kernel<kListBigWaves>, kImgBig, &attr_mw)) != hipSuccess)
+    return e;
   const dim3 ggrid((n_blocks + kGRun - 1) / kGRun), gblock(kGThreads);
   if (P.type == 1)
     hipLaunchKernelGGL((encode_group_kernel<true, false>), ggrid, gblock, 0, st, P);
@@ -2948,9 +2942,6 @@ hipError_t launch_encode(const lsm_items& items, const uint32_t* starts, uint32_
     hipLaunchKernelGGL((encode_group_kernel<false, true>), ggrid, gblock, 0, st, P);
   else
     hipLaunchKernelGGL((encode_group_kernel<false, false>), ggrid, gblock, 0, st, P);
-  static uint64_t attr_mw = 0;
-  if ((e = set_lds_attr((const void*)encode_write_list_mw_kernel<kListBigWaves>, kImgBig, &attr_mw)) != hipSuccess)
-    return e;
   // medium blocks (<= 20 KiB images): one wave each, eight workgroups per CU, was
   // faster than four waves each (2.26 vs 2.40 ms for the 16 KiB random-key class)
   hipLaunchKernelGGL(encode_write_list_kernel, dim3(2048), dim3(kWave), kImgMedium, st, P, kPlanMedium);
@@ -2959,9 +2950,7 @@ hipError_t launch_encode(const lsm_items& items, const uint32_t* starts, uint32_
   if (P.huge_pool) {  // huge blocks across the GPU (the ones it does not take stay flagged for E3 below)
     hipLaunchKernelGGL(encode_huge_plan_kernel, dim3(1), dim3(1024), 0, st, P);
     hipLaunchKernelGGL(encode_huge_records_kernel, dim3(kEHugeGrid), dim3(256), 0, st, P);
-    hipLaunchKernelGGL(encode_huge_contrib_kernel, dim3(kEHugeGrid), dim3(256), 0, st, P);
-    // (an unused 40 KiB LDS request: one chain workgroup per SIMD)
-    hipLaunchKernelGGL(encode_huge_chain_kernel, dim3(1024), dim3(64), 0, st, P);
+    hipLaunchKernelGGL(encode_huge_chain_kernel, dim3(min(n_blocks, 1024u)), dim3(256), 0, st, P);
   }
   hipLaunchKernelGGL(encode_large_kernel, dim3(512), dim3(kE3Threads), 0, st, P);
   return hipGetLastError();

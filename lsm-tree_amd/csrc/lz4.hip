@@ -17,6 +17,7 @@
 //                     blocks); anything larger is decoded by lane 0 straight
 //                     in HBM (rare: only oversize blocks).
 #include <hip/hip_runtime.h>
+#include "fill.hpp"
 
 #include "block_format.hpp"
 #include "decode.hpp"
@@ -385,7 +386,7 @@ static int lz4_decompress(const uint8_t* d_blocks, const uint64_t* d_block_off, 
   const hipStream_t st = (hipStream_t)stream;
   uint32_t* count = (uint32_t*)d_workspace;
   uint32_t* list = count + 4;
-  hipError_t e = hipMemsetAsync(count, 0, 4, st);
+  hipError_t e = fill_words_async(count, 1, 0, st);
   if (e != hipSuccess) return hip_status(e, "lsm_lz4_decompress_blocks");
   hipLaunchKernelGGL(lz4_small_kernel, dim3((n_blocks + 3) / 4), dim3(256), 0, st, d_blocks, d_block_off, n_blocks,
                      d_out, d_out_off, d_status, frame);

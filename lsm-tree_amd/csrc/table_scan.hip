@@ -22,6 +22,7 @@
 // lsm_scan_table_async keeps the counts on the device and launches each level
 // for the caller's bounds.
 #include <hip/hip_runtime.h>
+#include "fill.hpp"
 
 #include "decode.hpp"
 #include "lsmgpu.h"
@@ -252,7 +253,7 @@ extern "C" int lsm_scan_table(const uint8_t* d_file, uint64_t file_len, const ls
   for (uint32_t lvl = 0; lvl < levels; ++lvl) {
     DecodeParams P = index_params(d_file, w.lvl_off, n_lvl, w, cap_blocks + 1);
     hipError_t e = launch_decode(P, w.dec_ws, w.dec_bytes, st);
-    if (e == hipSuccess) e = hipMemsetAsync(w.flag, 0xFF, 16, st);
+    if (e == hipSuccess) e = fill_words_async(w.flag, 4, 0xFFFFFFFFu, st);
     if (e != hipSuccess) return fail(e);
     hipLaunchKernelGGL(first_failed_kernel, dim3((n_lvl + 255) / 256), dim3(256), 0, st, w.lvl_status, n_lvl,
                        w.flag + 1);
@@ -341,7 +342,7 @@ extern "C" int lsm_scan_table_async(const uint8_t* d_file, uint64_t file_len, co
     const uint32_t lvl_cap = data_level ? (data_blocks_hint ? data_blocks_hint : cap_blocks) : icap;
     hipLaunchKernelGGL(scan_level_check_kernel, dim3(1), dim3(256), 0, st, w.state, w.lvl_status, w.lvl_start,
                        lvl_cap, table->block_count, data_level ? 1u : 0u);
-    if ((e = hipMemsetAsync(w.flag, 0xFF, 16, st)) != hipSuccess) return fail(e);
+    if ((e = fill_words_async(w.flag, 4, 0xFFFFFFFFu, st)) != hipSuccess) return fail(e);
     uint64_t* dst = data_level ? d_block_off : w.lvl_off;
     // ranges [0, last]: the data decode reads up to cap + 1 offsets, the partition level icap + 1
     const uint32_t last = data_level ? cap_blocks : icap;

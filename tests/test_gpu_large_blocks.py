@@ -323,3 +323,53 @@ def test_huge_encode_pool_sizes(gpu):
         off = out["block_off"].cpu().numpy().view(np.uint64)
         assert (out["status"].cpu().numpy()[:nb] == 0).all() and (off == ref_off).all(), extra
         assert out["buf"].cpu().numpy()[:int(off[-1])].tobytes() == ref_buf.tobytes(), extra
+
+
+def test_huge_encode_concurrent_streams(gpu):
+    """Two host threads encoding ragged pool batches (group-class, listed and
+    huge blocks) on two streams at once, each through its own Encoder, five
+    times: bytes, offsets and statuses == the oracle's."""
+    import threading
+    import torch
+    sizes = [50, 200, 20000, 7, 1, 30000, 300, 13, 9000, 64, 65, 129, 2500, 16400]
+    cases = []
+    for seed in (31, 32):
+        items = counter_items(int(sum(sizes)), seed=seed, tomb_frac=0.05)
+        starts = np.concatenate([[0], np.cumsum(sizes)]).astype(np.uint32)
+        ref_buf, ref_off = pyoracle.encode_blocks(items, starts)
+        d_items = gpu.items_to_device(items)
+        d_starts = torch.from_numpy(starts.astype(np.int32)).cuda()
+        cases.append((d_items, d_starts, len(starts) - 1, ref_buf, ref_off))
+    torch.cuda.synchronize()
+
+    def check(out, nb, ref_buf, ref_off):
+        off = out["block_off"].cpu().numpy().view(np.uint64)
+        assert (out["status"].cpu().numpy()[:nb] == 0).all() and (off == ref_off).all()
+        assert out["buf"].cpu().numpy()[:int(off[-1])].tobytes() == ref_buf.tobytes()
+
+    results, errors = [None, None], []
+
+    def worker(t):
+        try:
+            d_items, d_starts, nb, _, _ = cases[t]
+            s = torch.cuda.Stream()
+            enc = gpu.Encoder()
+            with torch.cuda.stream(s):
+                out = enc.encode(d_items, d_starts, nb, pool=True)
+                for _ in range(4):
+                    out["buf"].zero_()
+                    enc.encode(d_items, d_starts, nb, out=out, stream=s, pool=True)
+            s.synchronize()
+            results[t] = out
+        except Exception as e:  # (reported by the main thread)
+            errors.append(e)
+
+    threads = [threading.Thread(target=worker, args=(t,)) for t in range(2)]
+    for t in threads:
+        t.start()
+    for t in threads:
+        t.join()
+    assert not errors, errors
+    for t in range(2):
+        check(results[t], cases[t][2], cases[t][3], cases[t][4])
+
