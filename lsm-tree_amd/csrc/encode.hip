@@ -1831,14 +1831,20 @@ __global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(4))) 
                     group_fits(s1 - s0, k1 - (k0 & ~15ULL), v1 - (v0 & ~15ULL), o1 - (o0 & ~15ULL), hsum);
     return Grp{b, (uint32_t)__builtin_ctzll(~__ballot(ok))};
   };
+  // the run's group-class blocks (listed / rejected ones are passed over at once)
+  const uint64_t gmask = __ballot(rb < b_end && (r_plan.step_flags >> 8) == 0);
   auto next_group = [&](uint32_t b) -> Grp {
     for (;;) {
       if (b >= b_end) return Grp{b, 0};
       const Grp g = form(b);
       if (g.k) return g;
-      const uint32_t fl = rl32(r_plan.step_flags, b - b_begin) >> 8;
-      if (fl == 0 && lane == 0) P.status[b] = ST_OVERFLOW;  // group class, but past out_cap
-      ++b;
+      const uint64_t rest = gmask >> (b - b_begin);
+      if (rest & 1) {
+        if (lane == 0) P.status[b] = ST_OVERFLOW;  // group class, but past out_cap
+        ++b;
+      } else {
+        b = rest ? b + (uint32_t)__builtin_ctzll(rest) : b_end;
+      }
     }
   };
   auto issue_dma = [&](const Grp& g) {
