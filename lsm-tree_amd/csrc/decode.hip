@@ -1184,7 +1184,9 @@ __global__ __launch_bounds__(kBigGWaves * kWave) void decode_big_kernel(DecodePa
         const uint32_t total = meta[0].st == ST_OK ? meta[0].bin_len : 0;
         for (uint32_t r = lane; r < total; r += kWave) owner[r] = 0;
         wave_sync();
+        __builtin_amdgcn_s_setprio(2);  // (the record walk is the block's longest role)
         phase_a<true>(stage, meta, owner, rec, 0, kWave, total, kBigGTile);
+        __builtin_amdgcn_s_setprio(0);
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "workgroup", "local");
         if (lane == 0) __hip_atomic_store(&sync->a_done, tag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
       } else {  // the per-KiB contributions, then wait for phase A
@@ -1536,8 +1538,11 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void d
       // phase A (serial LDS walks: latency) on wave 0, the contributions (VALU) on the
       // other waves meanwhile; without phase A on all four
       const bool split = fast;
-      if (fast && (split ? wave == 0 : true))
+      if (fast && (split ? wave == 0 : true)) {
+        if (split) __builtin_amdgcn_s_setprio(2);  // (the walk is the unit's longest role)
         phase_a<true>(stage, wmeta, owner, rec, split ? 0 : wave * kWave, split ? kWave : 4 * kWave, niv, kHugeTile);
+        __builtin_amdgcn_s_setprio(0);
+      }
       HUGE_PHASE(3);
       if (hash && r->nbk && (!split || wave != 0)) {  // the KiB blocks that start in [cs, ce)
         const uint32_t nbk = r->nbk;
