@@ -2771,9 +2771,9 @@ __global__ __launch_bounds__(256) void encode_huge_chain_kernel(EncodeParams P) 
   }
 }
 
-// Scan output: block offsets (low 40 bits of the prefix) and the list of the
-// listed blocks (high bits = their running count).
-// With the pool, huge blocks are also collected (hdr->count) for the whole-GPU E3.
+// The size scan's outputs: block offsets (low 40 bits of the prefix) and the
+// list of the listed blocks (high bits = their running count); with the pool,
+// the huge blocks are also collected (hdr->count) for the whole-GPU E3.
 struct EncodeOffOut {
   uint64_t* off;
   const uint64_t* sizes;
@@ -2784,18 +2784,59 @@ struct EncodeOffOut {
   uint32_t* huge_count;  // null: no pool
   uint32_t* huge_list;
   uint32_t huge_cap;
-  __device__ void operator()(uint64_t i, uint64_t prefix) const {
-    off[i] = prefix & kOffMask;
-    if (i < n && (sizes[i] & ~kOffMask)) {
-      list[prefix >> 40] = (uint32_t)i;
-      if (huge_count && (plans[i].step_flags >> 8) == kPlanHuge) {
-        const uint32_t slot = atomicAdd(huge_count, 1u);
-        if (slot < huge_cap) huge_list[slot] = (uint32_t)i;
+};
+
+// The size scan's apply pass (scan_tile_apply's shape, the outputs above): a
+// thread's kScanPerThread sizes, and for its listed blocks their plan flags,
+// are all read before the scan; the huge blocks take their list slots from one
+// atomic per wave (a per-block atomic on one counter serialised a batch of 240
+// huge blocks at 7.8 us).
+__global__ __launch_bounds__(kScanThreads) void encode_offsets_apply_kernel(const uint64_t* __restrict__ tile_offsets,
+                                                                            EncodeOffOut o) {
+  __shared__ uint64_t sh[kScanThreads / 64];
+  const uint64_t n = o.n;
+  const uint64_t base = (uint64_t)blockIdx.x * kScanTile + (uint64_t)threadIdx.x * kScanPerThread;
+  const uint32_t lane = threadIdx.x & (kWave - 1);
+  uint64_t v[kScanPerThread];
+  scan_load(o.sizes, base, n, v);
+  bool huge[kScanPerThread];
+  uint32_t hc = 0;
+  uint64_t s = 0;
+#pragma unroll
+  for (int i = 0; i < kScanPerThread; ++i) {
+    huge[i] = o.huge_count && base + i < n && (v[i] & ~kOffMask) &&
+              (o.plans[base + i].step_flags >> 8) == kPlanHuge;
+    hc += huge[i] ? 1u : 0u;
+    s += v[i];
+  }
+  uint64_t total;
+  uint64_t ex = block_excl_scan_u64(s, sh, total) + (tile_offsets ? tile_offsets[blockIdx.x] : 0);
+  uint32_t slot = 0;
+  if (o.huge_count) {  // (uniform)
+    const uint32_t incl = wave_incl_scan_u32(hc);
+    const uint32_t wtot = (uint32_t)__shfl((int)incl, kWave - 1);
+    uint32_t wb = 0;
+    if (lane == 0 && wtot) wb = atomicAdd(o.huge_count, wtot);
+    slot = (uint32_t)__shfl((int)wb, 0) + incl - hc;
+  }
+#pragma unroll
+  for (int i = 0; i < kScanPerThread; ++i) {
+    const uint64_t k = base + i;
+    if (k < n) {
+      o.off[k] = ex & kOffMask;
+      if (v[i] & ~kOffMask) o.list[ex >> 40] = (uint32_t)k;
+      if (huge[i]) {
+        if (slot < o.huge_cap) o.huge_list[slot] = (uint32_t)k;
+        ++slot;
       }
     }
-    if (i == n) *count = (uint32_t)(prefix >> 40);
+    if (k == n - 1) {
+      o.off[n] = (ex + v[i]) & kOffMask;
+      *o.count = (uint32_t)((ex + v[i]) >> 40);
+    }
+    ex += v[i];
   }
-};
+}
 
 #ifdef LSM_DIAG
 static unsigned long long* diag_phase_buffer() {
@@ -2933,7 +2974,12 @@ hipError_t launch_encode(const lsm_items& items, const uint32_t* starts, uint32_
     oo.huge_list = reinterpret_cast<uint32_t*>(P.huge_pool + 256);
     oo.huge_cap = P.huge_cap;
   }
-  if ((e = launch_excl_scan(P.sizes, n_blocks, tiles, oo, st)) != hipSuccess) return e;
+  {
+    const uint64_t* offs;
+    if ((e = launch_scan_tile_offsets(P.sizes, n_blocks, tiles, st, &offs)) != hipSuccess) return e;
+    hipLaunchKernelGGL(encode_offsets_apply_kernel, dim3((uint32_t)scan_tiles(n_blocks)), dim3(kScanThreads), 0, st,
+                       offs, oo);
+  }
   static uint64_t attr_done = 0;
   if ((e = set_lds_attr((const void*)encode_write_list_kernel, kImgBig, &attr_done)) != hipSuccess) return e;
   static uint64_t attr_mw = 0;

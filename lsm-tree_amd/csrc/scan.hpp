@@ -62,20 +62,29 @@ __global__ __launch_bounds__(kScanThreads) void scan_tile_reduce(const T* __rest
   if (threadIdx.x == 0) tile_sums[blockIdx.x] = total;
 }
 
-// Single workgroup: exclusive scan of the tile sums in place.
+// Single workgroup: exclusive scan of the tile sums in place, kScanPerThread
+// consecutive tiles per thread (one pass for up to kScanTile tiles: 2048 tiles
+// of 2048 inputs each).
 static __global__ __launch_bounds__(kScanThreads) void scan_tile_sums(uint64_t* __restrict__ sums, uint64_t n_tiles) {
   __shared__ uint64_t sh[kScanThreads / 64];
   uint64_t carry = 0;
-  for (uint64_t base = 0; base < n_tiles; base += kScanThreads) {
-    const uint64_t i = base + threadIdx.x;
-    uint64_t v = i < n_tiles ? sums[i] : 0;
+  for (uint64_t b0 = 0; b0 < n_tiles; b0 += kScanTile) {
+    const uint64_t base = b0 + (uint64_t)threadIdx.x * kScanPerThread;
+    uint64_t v[kScanPerThread];
+    scan_load(sums, base, n_tiles, v);
+    uint64_t s = 0;
+#pragma unroll
+    for (int i = 0; i < kScanPerThread; ++i) s += v[i];
     uint64_t total;
-    uint64_t ex = block_excl_scan_u64(v, sh, total);
-    if (i < n_tiles) sums[i] = carry + ex;
+    uint64_t ex = carry + block_excl_scan_u64(s, sh, total);
+#pragma unroll
+    for (int i = 0; i < kScanPerThread; ++i) {
+      if (base + i < n_tiles) sums[base + i] = ex;
+      ex += v[i];
+    }
     carry += total;
   }
 }
-
 // Out(i, prefix) is called for i in [0, n] with the exclusive prefix.  Each
 // thread reads its inputs before its first Out call, so Out may overwrite in[i].
 // tile_offsets == nullptr: a single tile (no tile sums to add).
@@ -102,20 +111,28 @@ __global__ __launch_bounds__(kScanThreads) void scan_tile_apply(const T* in, uin
 
 inline uint64_t scan_tiles(uint64_t n) { return (n + kScanTile - 1) / kScanTile; }
 
-// Enqueue the scan (u64 or u32 inputs, u64 prefixes); `tmp` holds scan_tiles(n) u64.  n >= 1.
-template <class T, class Out>
-inline hipError_t launch_excl_scan(const T* in, uint64_t n, uint64_t* tmp, Out out, hipStream_t st) {
+// The tile pre-passes of a scan with more than one tile (per-tile reduce, scan of
+// the tile sums into tmp); *offs = tmp then, else null (a single tile needs none).
+template <class T>
+inline hipError_t launch_scan_tile_offsets(const T* in, uint64_t n, uint64_t* tmp, hipStream_t st,
+                                           const uint64_t** offs) {
   const uint64_t tiles = scan_tiles(n);
-  if (tiles == 1) {  // (a batch of <= 2048 blocks: one launch, not three of ~4.5 us each)
-    hipLaunchKernelGGL((scan_tile_apply<T, Out>), dim3(1), dim3(kScanThreads), 0, st, in, n, (const uint64_t*)nullptr,
-                       out);
-    return hipGetLastError();
-  }
+  *offs = nullptr;
+  if (tiles == 1) return hipSuccess;  // (a batch of <= 2048 blocks: one launch, not three of ~4.5 us each)
   hipLaunchKernelGGL(scan_tile_reduce<T>, dim3((uint32_t)tiles), dim3(kScanThreads), 0, st, in, n, tmp);
   hipLaunchKernelGGL(scan_tile_sums, dim3(1), dim3(kScanThreads), 0, st, tmp, tiles);
-  hipLaunchKernelGGL((scan_tile_apply<T, Out>), dim3((uint32_t)tiles), dim3(kScanThreads), 0, st, in, n,
-                     (const uint64_t*)tmp, out);
+  *offs = tmp;
   return hipGetLastError();
 }
 
+// Enqueue the scan (u64 or u32 inputs, u64 prefixes); `tmp` holds scan_tiles(n) u64.  n >= 1.
+template <class T, class Out>
+inline hipError_t launch_excl_scan(const T* in, uint64_t n, uint64_t* tmp, Out out, hipStream_t st) {
+  const uint64_t* offs;
+  hipError_t e = launch_scan_tile_offsets(in, n, tmp, st, &offs);
+  if (e != hipSuccess) return e;
+  hipLaunchKernelGGL((scan_tile_apply<T, Out>), dim3((uint32_t)scan_tiles(n)), dim3(kScanThreads), 0, st, in, n, offs,
+                     out);
+  return hipGetLastError();
+}
 }  // namespace lsmgpu
