@@ -1495,7 +1495,8 @@ __device__ __forceinline__ void group_barrier_lds() {
 //   blocks   wave per block: its total from the wave parts, the plan as
 //            encode_plan_kernel's epilogue
 //   offsets  thread per item: erec = prefix - its block's first prefix (the
-//            packed word for blocks of <= kGItems items)
+//            packed word for blocks of <= kGItems items); huge blocks keep the
+//            prefix (their writers subtract pfirst)
 // A non-monotone item_start array rejects every block (the one-workgroup
 // plan rejects the run of blocks its workgroup holds).
 __device__ __forceinline__ uint32_t block_of_item(const EncodeParams& P, uint32_t i) {
@@ -1578,9 +1579,20 @@ __device__ __forceinline__ E1pItems<K> e1p_items(const EncodeParams& P) {
   return t;
 }
 
+// The huge-block pool header's collected-block count (EncHugeHdr::count), as a u32 index.
+constexpr uint32_t kEncHugeCountWord = 2;
+
 __global__ __launch_bounds__(256) void encode_e1p_lengths_kernel(EncodeParams P) {
-  for (uint64_t x = (uint64_t)blockIdx.x * 256 + threadIdx.x; x < P.n_blocks; x += (uint64_t)gridDim.x * 256)
-    if (clamped_start(P, (uint32_t)x + 1) < clamped_start(P, (uint32_t)x)) atomicOr(P.e1p_flag, 1u);
+  if (blockIdx.x == 0) {  // the starts' monotonicity over every block, the flag written whole (no prior clear)
+    int bad = 0;
+    for (uint32_t x = threadIdx.x; x < P.n_blocks; x += 256)
+      bad |= clamped_start(P, x + 1) < clamped_start(P, x) ? 1 : 0;
+    bad = __syncthreads_or(bad);
+    if (threadIdx.x == 0) {
+      P.e1p_flag[0] = bad ? 1u : 0u;
+      if (P.huge_pool) reinterpret_cast<uint32_t*>(P.huge_pool)[kEncHugeCountWord] = 0;  // (the size scan counts into it)
+    }
+  }
   const E1pItems<kE1pLenPer> T = e1p_items<kE1pLenPer>(P);
   const uint32_t ri = P.ri, lane = threadIdx.x & 63;
   bool live[kE1pLenPer], head[kE1pLenPer];
@@ -1729,12 +1741,17 @@ __global__ __launch_bounds__(256) void encode_e1p_offsets_kernel(EncodeParams P)
   const E1pItems<kE1pPer> T = e1p_items<kE1pPer>(P);
   if (P.e1p_flag[0]) return;
   const uint32_t ri = P.ri;
+  // (huge blocks keep the record prefix in erec: their writers subtract the block's first
+  // prefix themselves, so their items, nearly all of such a batch, cost only the flag load here)
   uint32_t fl[kE1pPer], er[kE1pPer], pf[kE1pPer], hb[kE1pPer];
+  bool cv[kE1pPer];
 #pragma unroll
-  for (uint32_t j = 0; j < kE1pPer; ++j) {  // every item's loads first
-    fl[j] = er[j] = pf[j] = hb[j] = 0;
-    if (T.in[j]) {
-      fl[j] = gload_pod(P.plans, T.b[j]).step_flags;
+  for (uint32_t j = 0; j < kE1pPer; ++j) fl[j] = T.in[j] ? gload_pod(P.plans, T.b[j]).step_flags : 0;
+#pragma unroll
+  for (uint32_t j = 0; j < kE1pPer; ++j) {  // every converted item's loads first
+    er[j] = pf[j] = hb[j] = 0;
+    cv[j] = T.in[j] && !((fl[j] >> 8) & kPlanBad) && (fl[j] >> 8) != kPlanHuge;
+    if (cv[j]) {
       er[j] = gload(P.erec, T.i[j]);
       pf[j] = gload(P.pfirst, T.b[j]);
       hb[j] = gload(P.hbucket, T.i[j]);
@@ -1742,7 +1759,7 @@ __global__ __launch_bounds__(256) void encode_e1p_offsets_kernel(EncodeParams P)
   }
 #pragma unroll
   for (uint32_t j = 0; j < kE1pPer; ++j) {
-    if (!T.in[j] || ((fl[j] >> 8) & kPlanBad)) continue;
+    if (!cv[j]) continue;
     const uint32_t n = T.e[j] - T.s[j], roff = er[j] - pf[j], jj = T.i[j] - T.s[j];
     const bool head = jj % ri == 0;
     const uint32_t x = head ? jj / ri : hb[j];
@@ -2287,6 +2304,7 @@ __global__ __launch_bounds__(kE3Threads) void encode_large_kernel(EncodeParams P
     const uint32_t p0 = pad + kHdrLen;
     const uint32_t bin_off = pl.recs + 1;
     const bool scan = n <= kGItems;  // (uniform) else erec holds each record's offset
+    const uint32_t pf = P.hb_sh ? P.pfirst[b] : 0u;  // (after E1p erec holds huge blocks' record prefixes)
     for (uint32_t j = tid; j < (scan ? kE3Threads : n); j += kE3Threads) {
       const bool head = j % ri == 0;
       ItemMeta m;
@@ -2294,7 +2312,7 @@ __global__ __launch_bounds__(kE3Threads) void encode_large_kernel(EncodeParams P
       if (j < n) {
         bool bad = false;
         m = load_item_lcp(P, s, j, ri, bad);
-        if (!scan) roff = P.erec[s + j];
+        if (!scan) roff = P.erec[s + j] - pf;  // (after E1p: the record prefix, see encode_e1p_offsets_kernel)
       }
       if (scan) {  // n <= kGItems <= kE3Threads: one pass
         const uint32_t rec = j < n ? (uint32_t)item_record_len(P, m, head) : 0u;
@@ -2405,6 +2423,7 @@ struct EncHugeHdr {
   uint32_t n3;         // planned entries
   uint64_t total_units;
 };
+static_assert(offsetof(EncHugeHdr, count) == 4 * kEncHugeCountWord, "E1p clears the count by index");
 // Pool: [hdr | 256][list u32 x cap][kpre u64 x (cap + 1)][upre u64 x (cap + 1)][EncHuge x cap]
 // [contributions, 64 B per KiB block][done flags, 1 B per KiB block]
 struct EncHugeLayout {
@@ -2585,7 +2604,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
         // records [j0, j1) assembled in LDS (image bytes [a0, a0 + lend)), then copied
         // out in 16-B pieces; a unit larger than the image writes straight to HBM
         const uint32_t j0 = k * h.ipu, j1 = min(h.n, j0 + h.ipu);
-        const uint32_t rb = gload(P.erec, (uint64_t)h.s + j0), re = j1 < h.n ? gload(P.erec, (uint64_t)h.s + j1) : pl.recs;
+        // (after E1p erec holds a huge block's record prefixes: offsets relative to its first)
+        const uint32_t pf = P.hb_sh ? gload(P.pfirst, h.b) : 0u;
+        const uint32_t rb = gload(P.erec, (uint64_t)h.s + j0) - pf;
+        const uint32_t re = j1 < h.n ? gload(P.erec, (uint64_t)h.s + j1) - pf : pl.recs;
         const uint32_t a0 = (p0 + rb) & ~15u, lend = p0 + re - a0;
         const bool staged = lend + 32 <= kEHugeImg;  // (uniform)
         uint8_t* limg = reinterpret_cast<uint8_t*>(lbuf) - a0;  // image offset x -> LDS limg + x
@@ -2596,7 +2618,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
             // (after E1p the shared prefix is in hbucket: no key reads before the copy)
             ItemMeta m = P.hb_sh ? load_item(P, (uint64_t)h.s + j, bad) : load_item_lcp(P, h.s, j, ri, bad);
             if (P.hb_sh && !head) m.sh = gload(P.hbucket, (uint64_t)h.s + j);
-            const uint32_t roff = gload(P.erec, (uint64_t)h.s + j);
+            const uint32_t roff = gload(P.erec, (uint64_t)h.s + j) - pf;
             RecordCopy rc;
             rc.issue(P, m, head, p0 + roff);
             rc.store(P, m, head, dst);
@@ -2927,6 +2949,11 @@ hipError_t launch_encode(const lsm_items& items, const uint32_t* starts, uint32_
   P.pfirst = (uint32_t*)w; w += al256(((size_t)n_blocks + 1) * 4);
   P.wpart = (uint64_t*)w;
   hipError_t e;
+  P.plan_bpw = plan_blocks_per_wg(items.n_items, n_blocks);
+  P.hb_valid = 0;
+  P.hb_sh = 0;
+  const dim3 pgrid((n_blocks + P.plan_bpw - 1) / P.plan_bpw);
+  const bool e1p = P.type != 1 && P.plan_bpw <= kE1pMaxBpw && items.n_items > 0 && items.n_items < 0xFFFFFFFFull;
   {  // the whole-GPU E3 pool, when the workspace carries one
     const size_t base = al256(encode_workspace_size(items.n_items, n_blocks));
     const uint64_t cap = enc_huge_cap(n_blocks, out_cap);
@@ -2935,18 +2962,12 @@ hipError_t launch_encode(const lsm_items& items, const uint32_t* starts, uint32_
     P.huge_pool = pool ? (uint8_t*)ws + base : nullptr;
     P.huge_pool_bytes = pool ? ws_bytes - base : 0;
     P.huge_cap = pool ? (uint32_t)cap : 0;
-    if (pool && (e = fill_words_async(P.huge_pool, 64, 0, st)) != hipSuccess) return e;
-    // (with a pool the E1p flag sits in the cleared pool header: one memset launch, not two)
-    if (pool) P.e1p_flag = reinterpret_cast<uint32_t*>(P.huge_pool + 128);
+    // (E1p's lengths kernel writes the E1p flag whole and clears the huge-block count:
+    // no clear launch; otherwise the pool header is cleared here)
+    if (pool && !e1p && (e = fill_words_async(P.huge_pool, 64, 0, st)) != hipSuccess) return e;
   }
-  P.plan_bpw = plan_blocks_per_wg(items.n_items, n_blocks);
-  P.hb_valid = 0;
-  P.hb_sh = 0;
-  const dim3 pgrid((n_blocks + P.plan_bpw - 1) / P.plan_bpw);
-  const bool e1p = P.type != 1 && P.plan_bpw <= kE1pMaxBpw && items.n_items > 0 && items.n_items < 0xFFFFFFFFull;
   if (e1p) {  // batches of huge blocks: the plan item-parallel
     P.hb_sh = 1;
-    if (!P.huge_pool && (e = fill_words_async(P.e1p_flag, 1, 0, st)) != hipSuccess) return e;
     const dim3 igrid((uint32_t)((items.n_items + 256 * kE1pPer - 1) / (256 * kE1pPer)));
     const dim3 lgrid((uint32_t)((items.n_items + 256 * kE1pLenPer - 1) / (256 * kE1pLenPer)));
     hipLaunchKernelGGL(encode_e1p_lengths_kernel, lgrid, dim3(256), 0, st, P);
