@@ -1856,11 +1856,8 @@ __global__ __launch_bounds__(kGroupWaves * kWave) __attribute__((amdgpu_waves_pe
 // oracle/batch.c: 0 unless the handle holds header + a 32-byte minimum payload,
 // and at most (payload - 32) / 3 (every record is >= 3 bytes), so a corrupt,
 // not-yet-verified trailer cannot reserve more than its bytes could hold.
-__global__ __launch_bounds__(256) void trailer_counts_kernel(const uint8_t* __restrict__ blocks,
-                                                             const uint64_t* __restrict__ off, uint32_t n,
-                                                             uint64_t* __restrict__ counts) {
-  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
-  if (b >= n) return;
+__device__ __forceinline__ uint64_t trailer_count(const uint8_t* __restrict__ blocks, const uint64_t* __restrict__ off,
+                                                  uint32_t b) {
   const uint64_t o = off[b], e = off[b + 1];
   uint64_t c = 0;
   if (e >= o && e - o >= kHdrLen + kTrailerLen + 1) {
@@ -1869,7 +1866,43 @@ __global__ __launch_bounds__(256) void trailer_counts_kernel(const uint8_t* __re
     const uint64_t most = (e - o - kHdrLen - 32) / 3;  // records are >= 3 bytes each
     c = c < most ? c : most;
   }
-  counts[b] = c;
+  return c;
+}
+
+// (workgroup 0 also clears the call's four list counters: no clear launch of their own)
+__global__ __launch_bounds__(256) void trailer_counts_kernel(const uint8_t* __restrict__ blocks,
+                                                             const uint64_t* __restrict__ off, uint32_t n,
+                                                             uint64_t* __restrict__ counts, uint32_t* __restrict__ clear4) {
+  if (blockIdx.x == 0 && threadIdx.x < 4) clear4[threadIdx.x] = 0;
+  const uint32_t b = blockIdx.x * blockDim.x + threadIdx.x;
+  if (b >= n) return;
+  counts[b] = trailer_count(blocks, off, b);
+}
+
+// Batches of at most one scan tile (kScanTile blocks): the counts and their
+// exclusive scan into item_start in one workgroup (one launch, not two), and
+// the four list counters cleared.
+__global__ __launch_bounds__(kScanThreads) void trailer_counts_scan_kernel(const uint8_t* __restrict__ blocks,
+                                                                           const uint64_t* __restrict__ off, uint32_t n,
+                                                                           uint32_t* __restrict__ item_start, uint64_t cap,
+                                                                           uint32_t* __restrict__ clear4) {
+  __shared__ uint64_t sh[kScanThreads / 64];
+  if (threadIdx.x < 4) clear4[threadIdx.x] = 0;
+  const uint32_t base = threadIdx.x * kScanPerThread;
+  uint64_t v[kScanPerThread], s = 0;
+#pragma unroll
+  for (int i = 0; i < kScanPerThread; ++i) {
+    v[i] = base + i < n ? trailer_count(blocks, off, base + i) : 0;
+    s += v[i];
+  }
+  uint64_t total;
+  uint64_t ex = block_excl_scan_u64(s, sh, total);
+#pragma unroll
+  for (int i = 0; i < kScanPerThread; ++i) {
+    if (base + i < n) item_start[base + i] = (uint32_t)(ex < cap ? ex : cap);
+    ex += v[i];
+    if (base + i + 1 == n) item_start[n] = (uint32_t)(ex < cap ? ex : cap);
+  }
 }
 
 struct ItemStartOut {
@@ -1921,11 +1954,15 @@ hipError_t launch_decode(const DecodeParams& P0, void* ws, size_t ws_bytes, hipS
   static_assert(huge_fixed_bytes(1) + 64 * 128 == 8704, "the threshold lsmgpu.h documents");
   P.huge_pool = ws_bytes >= pool0 + huge_fixed_bytes(1) + 64 * 128 ? (uint8_t*)ws + pool0 : nullptr;
   P.huge_pool_bytes = P.huge_pool ? ws_bytes - pool0 : 0;
-  hipError_t e = fill_words_async(dws, 4, 0, st);
-  if (e != hipSuccess) return e;
-  if (!(P.flags & LSM_DECODE_ITEM_START_VALID)) {
+  hipError_t e = hipSuccess;
+  if (P.flags & LSM_DECODE_ITEM_START_VALID) {
+    if ((e = fill_words_async(dws, 4, 0, st)) != hipSuccess) return e;
+  } else if (scan_tiles(P.n_blocks) == 1) {  // (the counts kernel clears the list counters)
+    hipLaunchKernelGGL(trailer_counts_scan_kernel, dim3(1), dim3(kScanThreads), 0, st, P.blocks, P.block_off,
+                       P.n_blocks, P.item_start_w, P.item_cap, (uint32_t*)dws);
+  } else {
     hipLaunchKernelGGL(trailer_counts_kernel, dim3((P.n_blocks + 255) / 256), dim3(256), 0, st, P.blocks,
-                       P.block_off, P.n_blocks, counts);
+                       P.block_off, P.n_blocks, counts, (uint32_t*)dws);
     if ((e = launch_excl_scan(counts, P.n_blocks, tiles, ItemStartOut{P.item_start_w, P.item_cap}, st)) != hipSuccess)
       return e;
   }
