@@ -220,8 +220,10 @@ struct TrailerInfo {
   uint32_t ri, step, bin_len, bin_off, hash_len, hash_off, item_count, rec_end;
 };
 
+// (mbase: where the marker byte before the binary index is read, when base is
+// a staged copy of the trailer bytes only)
 __device__ __forceinline__ int32_t read_trailer(const uint8_t* base, uint32_t p0, uint32_t plen,
-                                                TrailerInfo& t) {
+                                                TrailerInfo& t, const uint8_t* mbase = nullptr) {
   if (plen < kTrailerLen + 1) return ST_PARSE;
   const uint32_t tp = p0 + plen - kTrailerLen;
   const uint32_t w0 = read_u32_unaligned(base, tp);
@@ -234,7 +236,7 @@ __device__ __forceinline__ int32_t read_trailer(const uint8_t* base, uint32_t p0
   t.item_count = read_u32_unaligned(base, tp + 27);
   if (t.ri == 0 || (t.step != 2 && t.step != 4) || t.bin_len == 0 || t.bin_off == 0) return ST_PARSE;
   if ((uint64_t)t.bin_off + (uint64_t)t.bin_len * t.step > (uint64_t)(plen - kTrailerLen)) return ST_PARSE;
-  if ((read_u32_unaligned(base, p0 + t.bin_off - 1) & 0xFF) != kTrailerMarker) return ST_PARSE;
+  if ((read_u32_unaligned(mbase ? mbase : base, p0 + t.bin_off - 1) & 0xFF) != kTrailerMarker) return ST_PARSE;
   if ((uint64_t)t.bin_len != ((uint64_t)t.item_count + t.ri - 1) / t.ri) return ST_PARSE;
   t.rec_end = t.bin_off - 1;
   return ST_OK;

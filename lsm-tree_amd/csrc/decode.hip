@@ -178,7 +178,7 @@ __device__ __forceinline__ void meta_header_fields(const uint8_t* base, uint32_t
 // payloads over 65535 bytes cannot be stored in 16 bits: LSM_UNSUPPORTED,
 // decided here, after every header check and before the trailer is read.
 __device__ __forceinline__ void meta_trailer(const uint8_t* base, int32_t expect_type, uint32_t cap, BlockMeta& m,
-                                             bool compact) {
+                                             bool compact, const uint8_t* mbase = nullptr) {
   if (m.st != ST_OK) return;
   const uint32_t plen = m.len - kHdrLen;
   if (m.item_count != plen) { m.st = ST_TRUNCATED; return; }   // data_length vs handle
@@ -186,7 +186,7 @@ __device__ __forceinline__ void meta_trailer(const uint8_t* base, int32_t expect
   if (m.type == 2) { m.st = ST_UNSUPPORTED; return; }          // filter blocks are not KV blocks
   if (compact && (m.type == 1 || plen > 0xFFFFu)) { m.st = ST_UNSUPPORTED; return; }
   TrailerInfo t;
-  int32_t st = read_trailer(base, m.hb + kHdrLen, plen, t);
+  int32_t st = read_trailer(base, m.hb + kHdrLen, plen, t, mbase);
   if (st == ST_OK && m.type == 1 && t.ri != 1) st = ST_PARSE;   // index blocks: restart interval 1
   if (st == ST_OK && t.item_count > cap) st = ST_OVERFLOW;
   m.st = st;
@@ -909,8 +909,10 @@ __device__ __forceinline__ void defer3_block(const DecodeParams& P, uint32_t b) 
 }
 
 // Plan over the huge list, by one workgroup of nthr threads (nthr / 64 <= 16
-// waves); sh: 56 u64 of LDS.  Blocks it does not accept go to defer2.
-__device__ void huge_plan(const DecodeParams& P, uint64_t* sh, uint32_t nthr) {
+// waves); sh: 56 u64 of LDS; hstage: kHugePlanStage bytes of LDS per thread.
+// Blocks it does not accept go to defer2.
+constexpr uint32_t kHugePlanStage = 128;
+__device__ void huge_plan(const DecodeParams& P, uint64_t* sh, uint32_t nthr, uint8_t* hstage) {
   const uint32_t tid = threadIdx.x, lane = tid & 63, wave = tid >> 6, nw = nthr >> 6;
   const uint32_t n = gload(P.defer3_count, 0);
   const HugeLayout L = huge_layout(P, n);
@@ -943,12 +945,28 @@ __device__ void huge_plan(const DecodeParams& P, uint64_t* sh, uint32_t nthr) {
       item_base = gload(P.item_start, b);
       const uint32_t cap = gload(P.item_start, b + 1) - (uint32_t)item_base;
       const uint8_t* gbase = P.blocks + span0;
-      meta_header(gbase, (uint32_t)(off - span0), end >= off ? end - off : 0, m);
+      // the header's and the trailer's 64-B windows staged in LDS, all eight loads at once (the
+      // checks' serial reads then cost LDS round trips, not HBM ones); the trailer copy is
+      // addressed span-relative like gbase, and the marker byte before the binary index is read
+      // from HBM (blocks here span more than the 72 KiB stage; the input padding covers the reads)
+      uint8_t* hs = hstage + kHugePlanStage * tid;
+      const uint64_t tend = (max(end, off) + 15) & ~15ULL;
+      {
+        const u32x4* gh = reinterpret_cast<const u32x4*>(gbase);
+        const u32x4* gt = reinterpret_cast<const u32x4*>(P.blocks + tend - 64);
+        u32x4 x[8];
+#pragma unroll
+        for (int q = 0; q < 4; ++q) x[q] = gh[q], x[4 + q] = gt[q];
+#pragma unroll
+        for (int q = 0; q < 8; ++q) reinterpret_cast<u32x4*>(hs)[q] = x[q];
+      }
+      const uint8_t* tbase = hs + 128 - (tend - span0);  // (span offset o -> hs[128 - (tend - span0) + o])
+      meta_header(hs, (uint32_t)(off - span0), end >= off ? end - off : 0, m);
       acc = m.st == ST_OK;  // every header check, its checksum included
       if (acc) {
         const uint32_t plen = m.len - kHdrLen;
         nbk = hash ? (plen - 1) / 1024 : 0;  // (plen > 72 KiB here: the long path)
-        meta_trailer(gbase, P.expect_type, cap, m, P.compact);  // (after the payload checksum in oracle order)
+        meta_trailer(tbase, P.expect_type, cap, m, P.compact, gbase);  // (after the payload checksum in oracle order)
         span = ((max(end, off) + 15) & ~15ULL) - span0;
         npu = (nbk || m.st == ST_OK) ? (span + kHugeWin - 1) / kHugeWin : 0;
         niv = m.st == ST_OK ? trailer_of(m).bin_len + 1 : 0;  // (+1: the units kernel's end-of-block thread)
@@ -1010,7 +1028,8 @@ __device__ void huge_plan(const DecodeParams& P, uint64_t* sh, uint32_t nthr) {
 
 __global__ __launch_bounds__(1024) void decode_huge_plan_kernel(DecodeParams P) {
   __shared__ uint64_t sh[56];
-  huge_plan(P, sh, 1024);
+  extern __shared__ __attribute__((aligned(16))) uint8_t hstage[];  // kHugePlanStage B per thread
+  huge_plan(P, sh, 1024, hstage);
 }
 
 // Large blocks (SURVEY configs[4]: 16 / 64 KiB data blocks) listed by the
@@ -2001,8 +2020,11 @@ hipError_t launch_decode(const DecodeParams& P0, void* ws, size_t ws_bytes, hipS
     if ((e = hipLaunchKernel(big_k[variant], dim3(bgrid), dim3(kBigGWaves * kWave), args, kBigGLds, st)) != hipSuccess)
       return e;
   }
-  if (P.huge_pool && bgrid)  // the huge blocks the big-block kernel listed: plan (rejects go to defer2)
-    hipLaunchKernelGGL(decode_huge_plan_kernel, dim3(1), dim3(1024), 0, st, P);
+  if (P.huge_pool && bgrid) {  // the huge blocks the big-block kernel listed: plan (rejects go to defer2)
+    static uint64_t done_hp = 0;
+    if ((e = set_lds_attr((const void*)decode_huge_plan_kernel, 1024 * kHugePlanStage, &done_hp)) != hipSuccess) return e;
+    hipLaunchKernelGGL(decode_huge_plan_kernel, dim3(1), dim3(1024), 1024 * kHugePlanStage, st, P);
+  }
   const uint32_t dgrid = P.n_blocks < 1024 ? P.n_blocks : 1024;
   if (dgrid) {
     DecodeParams P2 = P;
