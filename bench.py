@@ -1120,15 +1120,34 @@ def roofline_entry(name, alg_bytes, ms, ceil, traffic_kernel, nb):
             "practical_peak": ceil, "frac_of_copy_ceiling": round(achieved / ceil["copy_GBps"], 4) if ceil else None}
 
 
+_LIB_SHA = None
+
+
+def lib_sha256():
+    """sha256 of the product library this process loaded (lsmgpu.LIB_PATH)."""
+    global _LIB_SHA
+    if _LIB_SHA is None:
+        import hashlib
+        import lsmgpu
+        _LIB_SHA = hashlib.sha256(Path(lsmgpu.LIB_PATH).read_bytes()).hexdigest()
+    return _LIB_SHA
+
+
 def load_trace_ms(kernels, n_blocks):
     """Mean duration (ms) of one launch of each (kernel, workgroups) pair, summed,
-    from the newest committed rocprofv3 kernel-trace summary
+    from a committed rocprofv3 kernel-trace summary
     (profiles/*_bench_kernels_by_grid.csv, scripts/trace_by_grid.py) of a bench
-    run over the same batch size; None when no profile has every pair."""
+    run over the same batch size BY THE SAME LIBRARY BUILD: the trace's sidecar
+    (*.lib.json, written by scripts/profile_round.sh) must carry the sha256 of
+    the liblsmgpu.so this process loaded.  None otherwise (a trace of an older
+    build would report stale kernel times beside the live ones)."""
     import csv
     best, src = None, None
     for p in sorted((ROOT / "profiles").glob("*_bench_kernels_by_grid.csv")):  # (round names sort in order)
+        side = p.with_name(p.name.replace(".csv", ".lib.json"))
         try:
+            if json.loads(side.read_text()).get("lib_sha256") != lib_sha256():
+                continue
             rows = list(csv.DictReader(p.open()))
         except Exception:
             continue
@@ -1143,27 +1162,32 @@ def load_trace_ms(kernels, n_blocks):
     return (round(best, 4), src) if best is not None else (None, None)
 
 
-def encode_roofline(name, enc_ms, key_val, n_items, nb, total_bytes, ceil, trace_kernels=None):
-    """Encode roofline: `frac` on the ABI's input bytes (u64 key / value offsets:
-    25 B of SoA per item beside the key and value bytes), `frac_survey` on SURVEY
-    §8(d)'s (4-byte offsets: 17 B per item).  kernel_ms is the whole
-    lsm_encode_blocks call timed with HIP events on its launch stream (plan +
-    scan + write kernels); kernel_ms_trace the same kernels' mean launch
-    durations from the committed rocprofv3 trace of a bench run, when one
-    exists."""
-    enc_alg = key_val + n_items * ENC_IN_PER_ITEM + 4 * (nb + 1) + total_bytes + 8 * (nb + 1) + 4 * nb
+def encode_roofline(name, enc_ms, key_val, n_items, nb, total_bytes, ceil, trace_kernels=None, off_bytes=8):
+    """Encode roofline.  `achieved` / `frac` count SURVEY §8(d)'s algorithmic
+    bytes (the key and value bytes, 17 B of item SoA per item with 4-byte
+    offsets, the blocks written); `achieved_abi` / `frac_abi` count what the
+    call's ABI reads and writes (off_bytes-wide key / value offsets: 25 B of SoA
+    per item with lsm_items' u64 offsets, 17 B with lsm_items32's u32 ones, plus
+    block_item_start, block_off and status).  kernel_ms is the whole encode call
+    timed with HIP events on its launch stream (plan + scan + write kernels);
+    kernel_ms_trace the same kernels' mean launch durations from a committed
+    rocprofv3 trace of this very library build, when one exists."""
+    enc_alg_abi = key_val + n_items * (ENC_IN_PER_ITEM - 2 * (8 - off_bytes)) + 4 * (nb + 1) + total_bytes + \
+        8 * (nb + 1) + 4 * nb
     enc_alg_survey = key_val + n_items * ENC_IN_PER_ITEM_SURVEY + total_bytes
-    r = roofline_entry(name, enc_alg, enc_ms, ceil, "lsm_encode_blocks", nb)
-    r["kernel_ms_source"] = "HIP events around the whole lsm_encode_blocks call on its launch stream"
-    r["alg_bytes_survey"] = enc_alg_survey
-    r["frac_survey"] = round(enc_alg_survey / (enc_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
+    r = roofline_entry(name, enc_alg_survey, enc_ms, ceil, "lsm_encode_blocks", nb)
+    r["alg_bytes_source"] = "SURVEY 8(d): key + value bytes + 17 B/item SoA (4-B offsets) + blocks written"
+    r["kernel_ms_source"] = "HIP events around the whole encode call on its launch stream"
+    r["alg_bytes_abi"] = enc_alg_abi
+    r["achieved_abi"] = round(enc_alg_abi / (enc_ms * 1e-3) / 1e9, 1)
+    r["frac_abi"] = round(enc_alg_abi / (enc_ms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
     if trace_kernels:
         tms, tsrc = load_trace_ms(trace_kernels, nb)
         if tms:
             r["kernel_ms_trace"] = tms
             r["kernel_ms_trace_source"] = tsrc
-            r["frac_trace"] = round(enc_alg / (tms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
-            r["frac_survey_trace"] = round(enc_alg_survey / (tms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
+            r["frac_trace"] = round(enc_alg_survey / (tms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
+            r["frac_abi_trace"] = round(enc_alg_abi / (tms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
     return r
 
 

@@ -52,7 +52,7 @@
 extern "C" {
 #endif
 
-#define LSM_ABI_VERSION 6
+#define LSM_ABI_VERSION 7
 #define LSM_HEADER_LEN 33  /* Header::serialized_len(), header.rs:64-76 */
 #define LSM_TRAILER_LEN 31 /* TRAILER_SIZE, trailer.rs:14-23 */
 /* d_blocks must be 16-byte aligned and readable for LSM_INPUT_PADDING bytes
@@ -73,7 +73,16 @@ typedef enum lsm_status {
     LSM_UNSUPPORTED = 9,   /* compression != None, filter block parse */
     LSM_BAD_ARG = 10,
     LSM_HIP_ERROR = 11,
-    LSM_DECOMPRESS = 12    /* Error::Decompress(Lz4): malformed LZ4 block   block/mod.rs:113-114 */
+    LSM_DECOMPRESS = 12,   /* Error::Decompress(Lz4): malformed LZ4 block   block/mod.rs:113-114 */
+    /* Internal hand-off mark, never the result of a completed call: a streamed
+     * huge-block checksum chain (lsm_decode_blocks_tuned, LSM_DECODE_HUGE_POOL,
+     * blocks >= 2 MiB) stopped waiting for the parse units of its block (no
+     * progress for 5 ms, e.g. other streams' kernels holding the CUs).  The
+     * call's fallback chain pass recomputes every block so marked after the
+     * parse kernel has ended and overwrites the mark with the block's real
+     * status; only diagnostic builds can skip that pass.  It is not a
+     * checksum mismatch (block/mod.rs:141-149 reports only real mismatches). */
+    LSM_INCOMPLETE = 13
 } lsm_status;
 
 /* BlockType codes, src/table/block/type.rs:13-22 */
@@ -140,11 +149,17 @@ typedef struct lsm_block_params {
     uint8_t compression;      /* 0 = CompressionType::None (the only supported value) */
     uint8_t reserved;         /* must be 0 (else LSM_BAD_ARG) */
     float hash_ratio;         /* data_block_hash_ratio (default 0.0) */
+    uint32_t flags;           /* LSM_ENCODE_HUGE_POOL or 0; any other bit is LSM_BAD_ARG */
 } lsm_block_params;
+/* Take the workspace pool of lsm_encode_workspace_size_ex: blocks whose image
+ * exceeds 96 KiB are written and hashed by work units across the whole GPU.
+ * Without this flag the pool is never used, whatever the workspace size; with
+ * it, a workspace too small for the pool's fixed part encodes without it. */
+#define LSM_ENCODE_HUGE_POOL 1u
 
 /* Tuning knobs for the decode kernel (0 = library default).  Any flag bit
- * other than LSM_DECODE_ITEM_START_VALID / LSM_DECODE_PAYLOAD_VERIFIED is
- * rejected with LSM_BAD_ARG. */
+ * other than LSM_DECODE_ITEM_START_VALID / LSM_DECODE_PAYLOAD_VERIFIED /
+ * LSM_DECODE_HUGE_POOL is rejected with LSM_BAD_ARG. */
 typedef struct lsm_decode_tuning {
     uint32_t blocks_per_wave;  /* consecutive blocks one workgroup owns (1..63, default 54) */
     uint32_t stage_bytes;      /* LDS stage bytes (256..65536, default 34560); larger blocks take the general path */
@@ -159,6 +174,14 @@ typedef struct lsm_decode_tuning {
  * stored bytes Block::from_reader verified before decompressing
  * (block/mod.rs:94-118); their frame headers carry the STORED checksum. */
 #define LSM_DECODE_PAYLOAD_VERIFIED 2u
+/* Take the workspace pool of lsm_decode_workspace_size_ex: blocks larger than
+ * 72 KiB are cut into work units across the whole GPU.  Without this flag the
+ * pool is never used, whatever the workspace size (lsm_decode_blocks, which
+ * takes no tuning, never uses it); with it, the pool is used when the
+ * workspace holds round_up(lsm_decode_workspace_size(n_blocks), 256) + 8704
+ * bytes or more (smaller: decoded without it; a pool too small for every
+ * huge block leaves the rest on the one-workgroup path). */
+#define LSM_DECODE_HUGE_POOL 4u
 
 /* Point-read results (DataBlock::point_read -> Option<InternalValue>,
  * data_block/mod.rs:412-472), one row per query; NULL fields other than item
@@ -192,16 +215,13 @@ int lsm_set_device(int device);
  * while their checksum is still being computed, so a block that then fails it
  * may have rows written): as in the reference, where Block::from_file returns
  * Err and no item is yielded, a caller uses no row of a failed block.
- * d_workspace: lsm_decode_workspace_size(n_blocks) bytes of device memory, or
- * lsm_decode_workspace_size_ex(n_blocks, blocks_bytes) bytes: with that much
- * (blocks_bytes >= the bytes the batch spans), blocks larger than 72 KiB (the
- * writer's up-to-4-MiB data blocks, writer/mod.rs:193-198; full block indexes)
- * are cut into work units across the whole GPU instead of one workgroup each.
- * Same outputs and statuses either way.  The pool is taken whenever
- * workspace_bytes >= round_up(lsm_decode_workspace_size(n_blocks), 256) + 8704
- * (a pool of 8 KiB past its 512-byte header), whatever buffer it came from: a
- * caller reusing a larger arena for a batch that should stay on the
- * one-workgroup path passes exactly lsm_decode_workspace_size(n_blocks). */
+ * d_workspace: lsm_decode_workspace_size(n_blocks) bytes of device memory, or,
+ * with LSM_DECODE_HUGE_POOL in tuning->flags, lsm_decode_workspace_size_ex(n_blocks,
+ * blocks_bytes) bytes (blocks_bytes >= the bytes the batch spans): then blocks
+ * larger than 72 KiB (the writer's up-to-4-MiB data blocks, writer/mod.rs:193-198;
+ * full block indexes) are cut into work units across the whole GPU instead of one
+ * workgroup each.  Same outputs and statuses either way.  The pool is taken only
+ * when the flag asks for it, never from the workspace size alone. */
 size_t lsm_decode_workspace_size(uint32_t n_blocks);
 size_t lsm_decode_workspace_size_ex(uint32_t n_blocks, uint64_t blocks_bytes);
 int lsm_decode_blocks(const uint8_t* d_blocks, const uint64_t* d_block_off, uint32_t n_blocks,
@@ -231,11 +251,12 @@ int lsm_decode_blocks16(const uint8_t* d_blocks, const uint64_t* d_block_off, ui
  * treats any LSM_BAD_ARG block as failing the whole batch.  Output blocks (header || payload) are packed back to back
  * into d_out; d_block_off (n_blocks+1 device u64) receives their offsets.
  * d_out needs lsm_encode_bound(...) bytes (status LSM_OVERFLOW otherwise).
- * d_workspace: lsm_encode_workspace_size(n_items, n_blocks) bytes, or
- * lsm_encode_workspace_size_ex(n_items, n_blocks, out_cap) bytes: with that
- * much, blocks whose image exceeds 96 KiB (the writer's up-to-4-MiB data
- * blocks, writer/mod.rs:193-198) are written and hashed by work units across
- * the whole GPU instead of one workgroup each.  Same bytes either way. */
+ * d_workspace: lsm_encode_workspace_size(n_items, n_blocks) bytes, or, with
+ * LSM_ENCODE_HUGE_POOL in params->flags, lsm_encode_workspace_size_ex(n_items,
+ * n_blocks, out_cap) bytes: then blocks whose image exceeds 96 KiB (the writer's
+ * up-to-4-MiB data blocks, writer/mod.rs:193-198) are written and hashed by work
+ * units across the whole GPU instead of one workgroup each.  Same bytes either
+ * way. */
 uint64_t lsm_encode_bound(uint64_t n_items, uint32_t n_blocks, uint64_t key_bytes, uint64_t val_bytes,
                           const lsm_block_params* params);
 size_t lsm_encode_workspace_size(uint64_t n_items, uint32_t n_blocks);

@@ -44,6 +44,7 @@ const char* lsm_status_name(int s) {
     case LSM_BAD_ARG: return "BAD_ARG";
     case LSM_HIP_ERROR: return "HIP_ERROR";
     case LSM_DECOMPRESS: return "DECOMPRESS";
+    case LSM_INCOMPLETE: return "INCOMPLETE";
     default: return "UNKNOWN";
   }
 }
@@ -88,7 +89,7 @@ static int decode_blocks_common(const uint8_t* d_blocks, const uint64_t* d_block
   P.item_start_w = d_item_start;
   P.status = d_status;
   P.flags = tuning ? tuning->flags : 0;
-  const uint32_t allowed = LSM_DECODE_ITEM_START_VALID | LSM_DECODE_PAYLOAD_VERIFIED |
+  const uint32_t allowed = LSM_DECODE_ITEM_START_VALID | LSM_DECODE_PAYLOAD_VERIFIED | LSM_DECODE_HUGE_POOL |
                            (lsmgpu::kDiagBuild ? lsmgpu::kDecodeDiagMask : 0u);
   if (P.flags & ~allowed) return LSM_BAD_ARG;
   auto pick = [&](uint32_t v, uint32_t dflt) { return v ? v : dflt; };
@@ -158,6 +159,7 @@ int lsm_encode_blocks(const lsm_items* d_items, const uint32_t* d_block_item_sta
   if (!d_items || !params || !d_block_item_start || !d_out || !d_block_off || !d_status) return LSM_BAD_ARG;
   if (params->compression != 0) return LSM_UNSUPPORTED;
   if (params->reserved != 0 && !lsmgpu::kDiagBuild) return LSM_BAD_ARG;
+  if (params->flags & ~LSM_ENCODE_HUGE_POOL) return LSM_BAD_ARG;
   if (params->block_type != LSM_BLOCK_DATA && params->block_type != LSM_BLOCK_INDEX &&
       params->block_type != LSM_BLOCK_META)
     return LSM_BAD_ARG;

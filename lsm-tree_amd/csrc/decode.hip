@@ -842,7 +842,9 @@ constexpr uint32_t kHugeRec = kHugeOwner + kHugeMaxIv;
 constexpr uint32_t kHugeLds = 64 + kHugeRec + 8 * (kHugeTile + 1);
 constexpr uint32_t kHugeWgsPerCU = 3;  // decode_huge_kernel's residency (3 waves per SIMD, ~51 KB of LDS)
 constexpr uint32_t kStreamRing = 12;    // the same for the chain waves inside decode_huge_kernel (4 per workgroup)
-constexpr uint32_t kStreamPolls = 1u << 18;  // flag polls before a chain wave gives a block up (hang guard)
+// A chain wave gives its block up after this long without progress (s_memrealtime ticks, 100 MHz:
+// 5 ms, ~25x a whole 4 MiB decode); the block is then re-verified by the fallback chain pass.
+constexpr uint64_t kStreamStallTicks = 500000;
 constexpr uint32_t kStreamChainWgs = 16;     // chain workgroups: 64 chain waves (a 1 KiB step of 20 ns each)
 constexpr uint32_t kStreamMinUnits = 64;     // stream the chains for batches holding a block of >= 2 MiB
 constexpr uint32_t kChainRing = 16;          // the chain kernel's ring (KiB of contribution rows in flight per wave)
@@ -1318,13 +1320,17 @@ __global__ __launch_bounds__(256) void decode_huge_units_kernel(DecodeParams P) 
 // every unit that writes into it: no L2 of this launch holds a line of the
 // chunk before that, and every block's rows are padded to whole chunks.
 // ready_upto: units [0, ready_upto) of the block are known done; polls 64
-// flags per load.  Returns false after kStreamPolls polls (hang guard).
+// flags per load.  Returns false (the caller gives the block up) after
+// kStreamStallTicks of wall time without progress: a bound in time, not in
+// polls, whose length does not depend on the load latency.
 __device__ __forceinline__ bool huge_wait_units(const HugeLayout& L, uint64_t ub, uint32_t need, uint32_t tag,
-                                                uint32_t npu, uint32_t& ready_upto) {
+                                                uint32_t npu, uint32_t& ready_upto, bool give_up) {
   const uint32_t lane = threadIdx.x & 63;
   need = min(need, npu);
-  for (uint32_t polls = 0; ready_upto < need; ++polls) {
-    if (polls >= kStreamPolls) return false;
+  if (ready_upto >= need) return true;
+  if (give_up) return false;  // (diagnostic builds: kDiagStreamGiveUp)
+  uint64_t t_prog = __builtin_amdgcn_s_memrealtime();
+  while (ready_upto < need) {
     const uint32_t c = ready_upto + lane;
     const uint32_t f = c < npu ? __hip_atomic_load(&L.uend[-1 - (int64_t)(ub + c)].z, __ATOMIC_RELAXED,
                                                     __HIP_MEMORY_SCOPE_AGENT)
@@ -1332,7 +1338,13 @@ __device__ __forceinline__ bool huge_wait_units(const HugeLayout& L, uint64_t ub
     const uint64_t done = __ballot(f == tag);
     const uint32_t adv = (uint32_t)__builtin_ctzll(~done);  // (done == ~0: 64)
     ready_upto = min(npu, ready_upto + (done == ~0ULL ? 64u : adv));
-    if (ready_upto < need && adv == 0) __builtin_amdgcn_s_sleep(2);
+    if (ready_upto < need && adv == 0) {
+      const uint64_t now = __builtin_amdgcn_s_memrealtime();
+      if (now - t_prog > kStreamStallTicks) return false;
+      __builtin_amdgcn_s_sleep(2);
+    } else {
+      t_prog = __builtin_amdgcn_s_memrealtime();
+    }
   }
   return true;
 }
@@ -1348,6 +1360,7 @@ __device__ void huge_chain_streamed(const DecodeParams& P, const HugeLayout& L, 
   const uint64_t ub = gload(L.ppre, i);
   const uint32_t npu = (uint32_t)(gload(L.ppre, i + 1) - ub);
   const uint32_t tag = P.huge_tag;
+  const bool give_up = kDiagBuild && (P.flags & kDiagStreamGiveUp);
   uint32_t ready_upto = 0;
   bool ok = true;
   int32_t st = ST_OK;
@@ -1361,7 +1374,7 @@ __device__ void huge_chain_streamed(const DecodeParams& P, const HugeLayout& L, 
       auto wait = [&](uint64_t c) {
         const uint64_t last = min((uint64_t)nbk - 1, 16 * c + 15);
         const uint32_t need = (uint32_t)((m.p0 + 1024 * last) / kHugeWin) + 1;
-        ok = ok && huge_wait_units(L, ub, need, tag, npu, ready_upto);
+        ok = ok && huge_wait_units(L, ub, need, tag, npu, ready_upto, give_up);
       };
       x = xxh3_chain8<kStreamRing>(L.contrib + 8 * gload(L.kpre, i), nbk, x, kLongSecret.acc[16 + k], ring, wait);
     }
@@ -1370,12 +1383,15 @@ __device__ void huge_chain_streamed(const DecodeParams& P, const HugeLayout& L, 
     xxh3_wave_tail_merge(P.blocks + r->span0, m.p0, m.len - kHdrLen, &kLongSecret, c0, c1, lo, hi);
     if (lo != m.ck_lo || hi != m.ck_hi) st = ST_CKSUM;
   }
-  ok = ok && huge_wait_units(L, ub, npu, tag, npu, ready_upto);  // every unit's parse result
+  ok = ok && huge_wait_units(L, ub, npu, tag, npu, ready_upto, give_up);  // every unit's parse result
   if (st == ST_OK) {
     const uint32_t bad = __hip_atomic_load(&r->parse_bad, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     st = m.st != ST_OK ? m.st : bad ? (int32_t)ST_PARSE : (int32_t)ST_OK;
   }
-  if (!ok) st = ST_CKSUM;  // (not reached: a unit that never finished)
+  // A chain that gave up decides nothing: its rows or parse results may be missing, so it
+  // marks the block for decode_huge_chain_kernel, which runs after this kernel has ended
+  // (every unit done) and writes the block's real status.
+  if (!ok) st = ST_INCOMPLETE;
   if (lane == 0) gstore(P.status, r->b, st);
 }
 
@@ -1644,8 +1660,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(3))) void d
 #undef HUGE_PHASE
 }
 
-// Chains of the huge blocks when they do not stream (decode_huge_kernel's
-// chain workgroups took them otherwise): a single-wave workgroup per block,
+// Chains of the huge blocks when they do not stream, and, when they stream,
+// of the blocks whose streamed chain gave up (status ST_INCOMPLETE; every
+// other block returns at once): a single-wave workgroup per block,
 // its eight accumulators on lanes 0..7 (xxh3_chain8), then on the same wave
 // the tail merge, the checksum compare and the status (oracle order: payload
 // checksum, then trailer, then parse).  The contributions cross a kernel
@@ -1654,13 +1671,16 @@ __global__ __launch_bounds__(64) void decode_huge_chain_kernel(DecodeParams P) {
   __shared__ __attribute__((aligned(16))) uint8_t ring[kChainRing * 1024];
   const HugeHdr* hp = reinterpret_cast<const HugeHdr*>(P.huge_pool);
   const uint32_t n = hp->n3;
-  if (!n || hp->stream) return;
+  if (!n) return;
+  const bool streamed = hp->stream != 0;
+  if (streamed && kDiagBuild && (P.flags & kDiagNoChainFallback)) return;
   const HugeLayout L = huge_layout(P, n);
   const bool hash = !(P.flags & LSM_DECODE_PAYLOAD_VERIFIED);
   const uint32_t lane = threadIdx.x & 63, k = lane & 7, q = lane & 3;
   for (uint32_t i = blockIdx.x; i < n; i += gridDim.x) {
     const HugeRec* r = L.rec + i;
     if (!r->accepted) continue;
+    if (streamed && gload(P.status, r->b) != ST_INCOMPLETE) continue;  // (the streamed chain decided it)
     const BlockMeta m = r->m;
     int32_t st = m.st != ST_OK ? m.st : r->parse_bad ? (int32_t)ST_PARSE : (int32_t)ST_OK;
     if (hash) {
@@ -1948,11 +1968,17 @@ size_t decode_workspace_size(uint32_t n_blocks) {
 // + the huge-block pool for a batch of blocks_bytes bytes: every huge block
 // spans more than kBigStage bytes, contributions 64 B per KiB, unit entries
 // 8 B per kHugeWin window (and one more per block).
+size_t decode_pool_min_bytes(uint32_t n_blocks) {
+  static_assert(huge_fixed_bytes(1) + 64 * 128 == 8704, "the threshold lsmgpu.h documents");
+  return ((decode_workspace_size(n_blocks) + 255) & ~(size_t)255) + huge_fixed_bytes(1) + 64 * 128;
+}
+
 size_t decode_workspace_size_ex(uint32_t n_blocks, uint64_t blocks_bytes) {
   const uint64_t most = blocks_bytes / kBigStage + 1;
   const uint64_t n3 = most < n_blocks ? most : n_blocks;
-  return decode_workspace_size(n_blocks) + huge_fixed_bytes(n3) + 64 * (blocks_bytes / 1024 + 1 + 16 * n3) +
-         16 * (blocks_bytes / kHugeWin + n3 + 1) + 256;
+  const size_t ex = decode_workspace_size(n_blocks) + huge_fixed_bytes(n3) + 64 * (blocks_bytes / 1024 + 1 + 16 * n3) +
+                    16 * (blocks_bytes / kHugeWin + n3 + 1) + 256;
+  return ex > decode_pool_min_bytes(n_blocks) ? ex : decode_pool_min_bytes(n_blocks);
 }
 
 uint32_t decode_lds_bytes(uint32_t stage_bytes, uint32_t tile_items, uint32_t blocks_per_wave) {
@@ -1974,8 +2000,9 @@ hipError_t launch_decode(const DecodeParams& P0, void* ws, size_t ws_bytes, hipS
   P.defer3_list = (uint32_t*)(dws + 256 + 2 * defer_bytes(P.n_blocks));
   const size_t base = decode_workspace_size(P.n_blocks);
   const size_t pool0 = (base + 255) & ~(size_t)255;
-  static_assert(huge_fixed_bytes(1) + 64 * 128 == 8704, "the threshold lsmgpu.h documents");
-  P.huge_pool = ws_bytes >= pool0 + huge_fixed_bytes(1) + 64 * 128 ? (uint8_t*)ws + pool0 : nullptr;
+  // the pool only when the caller asks for it (LSM_DECODE_HUGE_POOL; the ABI checked the size)
+  P.huge_pool = (P.flags & LSM_DECODE_HUGE_POOL) && ws_bytes >= decode_pool_min_bytes(P.n_blocks)
+                    ? (uint8_t*)ws + pool0 : nullptr;
   P.huge_pool_bytes = P.huge_pool ? ws_bytes - pool0 : 0;
   hipError_t e = hipSuccess;
   if (P.flags & LSM_DECODE_ITEM_START_VALID) {
@@ -2053,7 +2080,8 @@ hipError_t launch_decode(const DecodeParams& P0, void* ws, size_t ws_bytes, hipS
     // against a 2048-workgroup grid)
     const uint32_t ugrid = max(64u, kHugeWgsPerCU * (uint32_t)n_cu - chain_wgs);
     if ((e = hipLaunchKernel(hk, dim3(chain_wgs + ugrid), dim3(256), hargs, kHugeLds, st)) != hipSuccess) return e;
-    hipLaunchKernelGGL(decode_huge_chain_kernel, dim3(kHugeChainGrid), dim3(64), 0, st, P);  // (returns at once when streamed)
+    // (when streamed: only the blocks whose chain gave up, LSM_INCOMPLETE; the others return at once)
+    hipLaunchKernelGGL(decode_huge_chain_kernel, dim3(kHugeChainGrid), dim3(64), 0, st, P);
   }
   return hipGetLastError();
 }

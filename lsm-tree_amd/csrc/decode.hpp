@@ -56,8 +56,11 @@ constexpr bool kDiagBuild = false;
 constexpr uint32_t kDiagSkipHash = 0x100, kDiagSkipParse = 0x200, kDiagSkipStore = 0x400, kDiagSkipPhaseB = 0x800;
 // (group kernel, stage-only profiling: outputs and statuses invalid) no header / trailer wave; no stage DMA
 constexpr uint32_t kDiagSkipHeader = 0x1000, kDiagSkipDma = 0x2000;
-constexpr uint32_t kDecodeDiagMask =
-    kDiagSkipHash | kDiagSkipParse | kDiagSkipStore | kDiagSkipPhaseB | kDiagSkipHeader | kDiagSkipDma;
+// (huge-block pool, streamed chains) every chain wave gives up its first wait at once, as the
+// 5 ms no-progress guard would; the fallback chain pass is skipped (LSM_INCOMPLETE stays)
+constexpr uint32_t kDiagStreamGiveUp = 0x4000, kDiagNoChainFallback = 0x8000;
+constexpr uint32_t kDecodeDiagMask = kDiagSkipHash | kDiagSkipParse | kDiagSkipStore | kDiagSkipPhaseB |
+                                     kDiagSkipHeader | kDiagSkipDma | kDiagStreamGiveUp | kDiagNoChainFallback;
 
 // The > 64 KiB dynamic-LDS attribute acts on the CURRENT device: set it once
 // per device (a process may drive several GPUs, one host thread per device).
@@ -77,6 +80,8 @@ int hip_status(hipError_t e, const char* where);
 
 size_t decode_workspace_size(uint32_t n_blocks);
 size_t decode_workspace_size_ex(uint32_t n_blocks, uint64_t blocks_bytes);
+// smallest workspace that carries the pool (LSM_DECODE_HUGE_POOL): its header and 8 KiB
+size_t decode_pool_min_bytes(uint32_t n_blocks);
 uint32_t decode_lds_bytes(uint32_t stage_bytes, uint32_t tile_items, uint32_t blocks_per_wave);
 hipError_t launch_decode(const DecodeParams& P, void* workspace, size_t workspace_bytes, hipStream_t st);
 

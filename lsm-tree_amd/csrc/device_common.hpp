@@ -56,7 +56,8 @@ constexpr uint32_t kHashMaxPointers = 254;
 
 enum : int32_t {
   ST_OK = 0, ST_BAD_MAGIC = 1, ST_BAD_TYPE = 2, ST_HDR_CKSUM = 3, ST_CKSUM = 4, ST_PARSE = 5,
-  ST_OVERFLOW = 6, ST_TYPE_MISMATCH = 7, ST_TRUNCATED = 8, ST_UNSUPPORTED = 9, ST_BAD_ARG = 10
+  ST_OVERFLOW = 6, ST_TYPE_MISMATCH = 7, ST_TRUNCATED = 8, ST_UNSUPPORTED = 9, ST_BAD_ARG = 10,
+  ST_INCOMPLETE = 13  // LSM_INCOMPLETE: a streamed chain gave up waiting; the fallback pass re-verifies the block
 };
 
 // ---------------------------------------------------------------- XXH3 consts

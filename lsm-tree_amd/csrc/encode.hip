@@ -2863,7 +2863,7 @@ __global__ __launch_bounds__(kScanThreads) void encode_offsets_apply_kernel(cons
 #ifdef LSM_DIAG
 static unsigned long long* diag_phase_buffer() {
   static unsigned long long* d = nullptr;
-  if (!d && hipMalloc(&d, 16 * sizeof(unsigned long long)) == hipSuccess) hipMemset(d, 0, 16 * sizeof(unsigned long long));
+  if (!d && hipMalloc(&d, 16 * sizeof(unsigned long long)) == hipSuccess) (void)hipMemset(d, 0, 16 * sizeof(unsigned long long));
   return d;
 }
 #endif
@@ -2900,8 +2900,14 @@ static uint64_t enc_huge_cap(uint32_t n_blocks, uint64_t out_cap) {
 }
 
 size_t encode_workspace_size_ex(uint64_t n_items, uint32_t n_blocks, uint64_t out_cap) {
-  return encode_workspace_size(n_items, n_blocks) + enc_huge_fixed_bytes(enc_huge_cap(n_blocks, out_cap)) +
-         65 * (out_cap / 1024 + 1) + 256;
+  const size_t ex = encode_workspace_size(n_items, n_blocks) + enc_huge_fixed_bytes(enc_huge_cap(n_blocks, out_cap)) +
+                    65 * (out_cap / 1024 + 1) + 256;
+  return std::max(ex, encode_pool_min_bytes(n_items, n_blocks, out_cap));
+}
+
+size_t encode_pool_min_bytes(uint64_t n_items, uint32_t n_blocks, uint64_t out_cap) {
+  return al256(encode_workspace_size(n_items, n_blocks)) + enc_huge_fixed_bytes(enc_huge_cap(n_blocks, out_cap)) +
+         65 * 128;
 }
 
 uint64_t encode_bound(uint64_t n_items, uint32_t n_blocks, uint64_t key_bytes, uint64_t val_bytes,
@@ -2954,11 +2960,11 @@ hipError_t launch_encode(const lsm_items& items, const uint32_t* starts, uint32_
   P.hb_sh = 0;
   const dim3 pgrid((n_blocks + P.plan_bpw - 1) / P.plan_bpw);
   const bool e1p = P.type != 1 && P.plan_bpw <= kE1pMaxBpw && items.n_items > 0 && items.n_items < 0xFFFFFFFFull;
-  {  // the whole-GPU E3 pool, when the workspace carries one
+  {  // the whole-GPU E3 pool, when the caller asks for it (the ABI checked the size)
     const size_t base = al256(encode_workspace_size(items.n_items, n_blocks));
     const uint64_t cap = enc_huge_cap(n_blocks, out_cap);
-    const uint64_t fixed = enc_huge_fixed_bytes(cap);
-    const bool pool = cap && ws_bytes >= base + fixed + 65 * 128;
+    const bool pool = cap && (params.flags & LSM_ENCODE_HUGE_POOL) &&
+                      ws_bytes >= encode_pool_min_bytes(items.n_items, n_blocks, out_cap);
     P.huge_pool = pool ? (uint8_t*)ws + base : nullptr;
     P.huge_pool_bytes = pool ? ws_bytes - base : 0;
     P.huge_cap = pool ? (uint32_t)cap : 0;

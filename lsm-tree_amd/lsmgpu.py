@@ -20,7 +20,7 @@ LSM_INPUT_PADDING = 64
 
 STATUS = {0: "OK", 1: "BAD_MAGIC", 2: "BAD_TYPE", 3: "HDR_CKSUM", 4: "CKSUM", 5: "PARSE", 6: "OVERFLOW",
           7: "TYPE_MISMATCH", 8: "TRUNCATED", 9: "UNSUPPORTED", 10: "BAD_ARG", 11: "HIP_ERROR",
-          12: "DECOMPRESS"}
+          12: "DECOMPRESS", 13: "INCOMPLETE"}
 BLOCK_DATA, BLOCK_INDEX, BLOCK_FILTER, BLOCK_META = 0, 1, 2, 3
 
 
@@ -43,7 +43,7 @@ class LsmParsed16(C.Structure):
 
 class LsmBlockParams(C.Structure):
     _fields_ = [("restart_interval", C.c_uint8), ("block_type", C.c_uint8), ("compression", C.c_uint8),
-                ("reserved", C.c_uint8), ("hash_ratio", C.c_float)]
+                ("reserved", C.c_uint8), ("hash_ratio", C.c_float), ("flags", C.c_uint32)]
 
 
 class LsmPointResult(C.Structure):
@@ -61,8 +61,11 @@ class LsmTableScan(C.Structure):
                 ("global_seqno", C.c_uint64), ("block_count", C.c_uint64)]
 
 
-ABI_VERSION = 6
+ABI_VERSION = 7
 DECODE_ITEM_START_VALID = 1
+# lsm_decode_tuning.flags / lsm_block_params.flags: take the workspace pool (explicit opt-in)
+DECODE_HUGE_POOL = 4
+ENCODE_HUGE_POOL = 1
 # Mean block size (bytes) from which the wrappers hand the workspace pool for
 # blocks spread over the GPU (blocks > 72 KiB decode, > 96 KiB images encode).
 HUGE_AUTO_MEAN = 32 << 10
@@ -333,6 +336,9 @@ class Decoder:
                                                                   C.c_uint16 if dt == "int16" else C.c_uint8):
                     raise LsmError(f"compact decode: field {f} must be {dt}")
                 setattr(ps, f, out[f].data_ptr() if f in out else None)
+            if pool:
+                tuning = tuple(tuning or (0, 0, 0))
+                tuning = tuning[:3] + ((tuning[3] if len(tuning) > 3 else 0) | DECODE_HUGE_POOL,)
             t = C.byref(LsmDecodeTuning(*tuning)) if tuning is not None else None
             rc = lib().lsm_decode_blocks16(_ptr(blocks), _ptr(block_off), n_blocks, expect_type, C.byref(ps),
                                            item_cap, _ptr(out["item_start"]), _ptr(out["status"]), _ptr(ws),
@@ -342,6 +348,9 @@ class Decoder:
         ps = LsmParsed()
         for f, _ in PARSED_FIELDS:
             setattr(ps, f, out[f].data_ptr() if f in out else None)
+        if pool:  # the pool is an explicit opt-in (LSM_DECODE_HUGE_POOL), never implied by the size
+            tuning = tuple(tuning or (0, 0, 0))
+            tuning = tuning[:3] + ((tuning[3] if len(tuning) > 3 else 0) | DECODE_HUGE_POOL,)
         if tuning is not None:
             t = LsmDecodeTuning(*tuning)  # (blocks_per_wave, stage_bytes, tile_items[, flags])
             rc = lib().lsm_decode_blocks_tuned(_ptr(blocks), _ptr(block_off), n_blocks, expect_type, C.byref(ps),
@@ -392,12 +401,14 @@ class Encoder:
         it.handle_off = items["handle_off"].data_ptr() if "handle_off" in items else None
         it.handle_size = items["handle_size"].data_ptr() if "handle_size" in items else None
         it.n_items = n_items
-        params = LsmBlockParams(restart_interval, block_type, 0, 0, hash_ratio)
+        params = LsmBlockParams(restart_interval, block_type, 0, 0, hash_ratio, 0)
         key_bytes = int(items["keys"].numel())
         val_bytes = int(items["vals"].numel()) if "vals" in items else 0
         bound = lib().lsm_encode_bound(n_items, n_blocks, key_bytes, val_bytes, C.byref(params))
         if pool is None:
             pool = bound >= HUGE_AUTO_MEAN * max(n_blocks, 1)
+        if pool:  # the pool is an explicit opt-in (LSM_ENCODE_HUGE_POOL), never implied by the size
+            params.flags = ENCODE_HUGE_POOL
         need = (lib().lsm_encode_workspace_size_ex(n_items, n_blocks, bound) if pool
                 else lib().lsm_encode_workspace_size(n_items, n_blocks))
         if workspace_bytes is not None:

@@ -30,4 +30,6 @@ python3 scripts/traffic_summary.py $OUT/fetch $OUT/write $NB $BYTES $ITEMS $OUT/
 cat $OUT/traffic.json
 find $OUT/kt -name "*kernel_stats.csv" -exec cp {} $OUT/kernel_stats.csv \;
 python3 scripts/trace_by_grid.py $(find $OUT/kt -name "*kernel_trace.csv" | head -1) > $OUT/kernels_by_grid.csv
+# the library build the trace belongs to: bench.py uses a committed trace only for this same build
+python3 -c "import hashlib, json, sys; print(json.dumps({'lib_sha256': hashlib.sha256(open('lsm-tree_amd/liblsmgpu.so', 'rb').read()).hexdigest()}))" > $OUT/kernels_by_grid.lib.json
 head -20 $OUT/kernel_stats.csv

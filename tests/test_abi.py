@@ -52,7 +52,7 @@ def test_library_exports_exactly_the_header(L):
 
 def test_abi_version_and_status_names(L):
     lib = L.lib()
-    assert lib.lsm_abi_version() == L.ABI_VERSION == 6
+    assert lib.lsm_abi_version() == L.ABI_VERSION == 7
     for code, name in L.STATUS.items():
         assert lib.lsm_status_name(code).decode() == name
 
@@ -115,17 +115,22 @@ def test_bad_args_rejected_without_device(L):
         p = L.LsmBlockParams(16, 0, 0, bits, 0.0)
         assert lib.lsm_encode_blocks(C.byref(it), C.c_void_p(8), 1, C.byref(p), C.c_void_p(16), 100, C.c_void_p(24),
                                      C.c_void_p(32), C.c_void_p(48), 1 << 20, None) == 10
+    for flags in (2, 4, 0x100, 1 << 31):  # lsm_block_params.flags: only LSM_ENCODE_HUGE_POOL
+        p = L.LsmBlockParams(16, 0, 0, 0, 0.0, flags)
+        assert lib.lsm_encode_blocks(C.byref(it), C.c_void_p(8), 1, C.byref(p), C.c_void_p(16), 100, C.c_void_p(24),
+                                     C.c_void_p(32), C.c_void_p(48), 1 << 20, None) == 10
 
 
 def test_decode_tuning_flags_rejected(L):
-    """Only LSM_DECODE_ITEM_START_VALID and LSM_DECODE_PAYLOAD_VERIFIED are public
-    decode flags: diagnostic bits that would skip the hash, the parse or the
-    stores are LSM_BAD_ARG."""
+    """Only LSM_DECODE_ITEM_START_VALID, LSM_DECODE_PAYLOAD_VERIFIED and
+    LSM_DECODE_HUGE_POOL are public decode flags: diagnostic bits that would
+    skip the hash, the parse or the stores, or force the streamed chains to
+    give up, are LSM_BAD_ARG."""
     import ctypes as C
     lib = L.lib()
     ps = L.LsmParsed()
     ws = lib.lsm_decode_workspace_size(4)
-    for flags in (0x100, 0x200, 0x400, 0x800, 0x1000, 0x2000, 0x10000, 0x80000, 1 << 31):
+    for flags in (8, 0x100, 0x200, 0x400, 0x800, 0x1000, 0x2000, 0x4000, 0x8000, 0x10000, 0x80000, 1 << 31):
         t = L.LsmDecodeTuning(0, 0, 0, flags)
         assert lib.lsm_decode_blocks_tuned(C.c_void_p(0x1000), C.c_void_p(0x2000), 4, -1, C.byref(ps), 10,
                                            C.c_void_p(0x3000), C.c_void_p(0x4000), C.c_void_p(0x5000), ws,

@@ -1,7 +1,9 @@
 """The C-ABI entry points captured into a HIP graph (torch.cuda.CUDAGraph over
 the caller's stream) and replayed: lsm_encode_blocks with and without the
 workspace pool (4 KiB blocks; an item-parallel-planned batch of group-class,
-listed and 1 MiB blocks) and lsm_decode_blocks with and without the pool.
+listed and 1 MiB blocks; a batch holding a ~3.7 MiB block, whose pool decode
+streams its checksum chain inside the parse launch) and lsm_decode_blocks with
+and without the pool.
 Every replay's output == the oracle's (bytes, offsets, statuses, every
 decoded field).  A graph replays the launches the capture recorded, so every
 per-call clear must be a node that runs on each replay (csrc/fill.hpp)."""
@@ -16,6 +18,9 @@ pytestmark = pytest.mark.gpu
 BATCHES = {
     "4KiB": [52] * 300,
     "mixed": [50, 200, 20000, 7, 1, 30000, 300, 13, 9000, 64, 65, 129, 2500, 16400],
+    # a ~3.7 MiB block (>= 64 windows of 32 KiB): with the pool the decode streams its XXH3
+    # chain behind the parse units inside one launch (unit-done flags cleared per call)
+    "streamed": [52, 52429, 3300, 52],
 }
 
 

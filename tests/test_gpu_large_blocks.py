@@ -373,3 +373,56 @@ def test_huge_encode_concurrent_streams(gpu):
     for t in range(2):
         check(results[t], cases[t][2], cases[t][3], cases[t][4])
 
+
+
+# Diagnostic build (-DLSM_DIAG, lsm-tree_amd/.variants/libdiag.so, built by
+# __graft_entry__.build()): decode flag bits that force the streamed chains'
+# give-up path deterministically (csrc/decode.hpp).
+DIAG_STREAM_GIVE_UP = 0x4000
+DIAG_NO_CHAIN_FALLBACK = 0x8000
+
+
+@pytest.fixture(scope="module")
+def diag_lib(gpu):
+    from pathlib import Path
+    path = Path(gpu.HERE) / ".variants" / "libdiag.so"
+    if not path.exists():
+        pytest.fail(f"{path} not built (__graft_entry__.build() builds the diagnostic variant)")
+    saved, saved_path = gpu._lib, gpu.LIB_PATH
+    gpu._lib, gpu.LIB_PATH = None, path
+    try:
+        lib = gpu.lib()  # the diagnostic library with the same ctypes signatures
+    finally:
+        gpu._lib, gpu.LIB_PATH = saved, saved_path
+    return lib
+
+
+def test_streamed_chain_give_up(gpu, diag_lib):
+    """The streamed huge-block chains give a block up after 5 ms without progress
+    (other streams holding the CUs); the diagnostic flag makes every chain wave
+    give up at its first wait.  With the call's fallback chain pass every status
+    and row equals the oracle's (a give-up is never reported as a checksum
+    mismatch, block/mod.rs:141-149); with the pass skipped, exactly the blocks
+    whose chains gave up carry LSM_INCOMPLETE."""
+    items = counter_items(2 * 52429 + 3300, seed=29, tomb_frac=0.02)
+    starts = np.array([0, 52429, 55729, 2 * 52429 + 3300], np.uint32)  # ~3.7 MiB, ~230 KiB, ~3.5 MiB
+    buf, off = pyoracle.encode_blocks(items, starts)
+    blocks = [bytes(buf[int(off[i]):int(off[i + 1])]) for i in range(3)]
+    bad_ck = bytearray(blocks[2]); bad_ck[33 + 1_500_000] ^= 0x08
+    late = bytearray(blocks[0][33:]); late[-4] += 1
+    buf2, off2 = pack([blocks[0], blocks[1], bytes(bad_ck), pyoracle.block_write(bytes(late), 0), blocks[2]])
+    parsed, item_start, status = pyoracle.decode_blocks(buf2, off2)
+    assert list(status[:3]) == [0, 0, 4] and status[3] != 0 and status[4] == 0, status
+    saved = gpu._lib
+    gpu._lib = diag_lib
+    try:
+        g = gpu_decode(gpu, buf2, off2, tuning=(0, 0, 0, DIAG_STREAM_GIVE_UP), pool=True)
+        compare_decode(g, parsed, item_start, status)
+        g2 = gpu_decode(gpu, buf2, off2, tuning=(0, 0, 0, DIAG_STREAM_GIVE_UP | DIAG_NO_CHAIN_FALLBACK), pool=True)
+        g3 = gpu_decode(gpu, buf2, off2, pool=True)  # the diagnostic build without the flags: as the release
+        compare_decode(g3, parsed, item_start, status)
+    finally:
+        gpu._lib = saved
+    assert gpu.STATUS[13] == "INCOMPLETE"
+    # every block here has a valid header, so every one is a streamed huge block
+    assert (g2["status"] == 13).all(), g2["status"]

@@ -1,9 +1,10 @@
 """Host-side checks of the ctypes mirror's workspace handling (no GPU: the
 library is replaced by a recorder; the size functions are the real ones).
 
-lsm_decode_blocks takes the huge-block pool whenever the workspace it is
-handed is large enough (include/lsmgpu.h), so a Decoder reused across calls
-must hand a pool=False call exactly lsm_decode_workspace_size(n), however
+Since ABI 7 the huge-block pool is an explicit opt-in (LSM_DECODE_HUGE_POOL /
+LSM_ENCODE_HUGE_POOL, include/lsmgpu.h): a pool=True call passes the flag and
+the _ex workspace, a pool=False call neither.  A Decoder reused across calls
+still hands a pool=False call exactly lsm_decode_workspace_size(n), however
 large an earlier pool=True call grew its cached buffer."""
 import ctypes as C
 
@@ -41,8 +42,15 @@ def fake(monkeypatch):
 
 def _ws_arg(call):
     name, args = call
-    assert name == "lsm_decode_blocks"
+    assert name in ("lsm_decode_blocks", "lsm_decode_blocks_tuned")
     return args[9], args[8]  # workspace_bytes, workspace pointer
+
+
+def _pool_flag(call):
+    name, args = call
+    if name == "lsm_decode_blocks":  # (no tuning: never the pool)
+        return False
+    return bool(args[10]._obj.flags & lsmgpu.DECODE_HUGE_POOL)
 
 
 def test_decoder_pool_then_no_pool(fake):
@@ -58,6 +66,7 @@ def test_decoder_pool_then_no_pool(fake):
     full = fake.real.lsm_decode_workspace_size_ex(n, blocks.numel())
     got = [_ws_arg(c)[0] for c in fake.calls]
     assert got == [full, base, full]
+    assert [_pool_flag(c) for c in fake.calls] == [True, False, True]
     threshold = ((base + 255) & ~255) + 8704  # lsmgpu.h: the pool threshold
     assert base < threshold <= full
     # the cached buffer is reused (one allocation), only its view changes
@@ -77,3 +86,5 @@ def test_encoder_passes_exact_workspace(fake):
     e.encode(items, starts, n_blocks, pool=False)
     ws = [args[9] for name, args in fake.calls if name == "lsm_encode_blocks"]
     assert ws[1] == fake.real.lsm_encode_workspace_size(n_items, n_blocks) < ws[0]
+    flags = [args[3]._obj.flags for name, args in fake.calls if name == "lsm_encode_blocks"]
+    assert flags == [lsmgpu.ENCODE_HUGE_POOL, 0]
