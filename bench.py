@@ -1302,6 +1302,9 @@ def main():
     check_cut_rule(lsmgpu, 52, 16, 64)
     t_gen = time.perf_counter()
     items, starts, n_items = make_workload(torch, lsmgpu, nb, seed=0x5EED0002 + rank)
+    # the timed step encodes through lsm_encode_blocks32 (u32 key / value offsets: SURVEY 8(d)'s
+    # 4 + 4 B per item; the arenas are < 4 GiB); the u64-offset lsm_encode_blocks is timed beside it
+    items32 = dict(items, key_off=items["key_off"].to(torch.int32), val_off=items["val_off"].to(torch.int32))
     encoder = lsmgpu.Encoder(dev)
     enc = encoder.encode(items, starts, nb)
     torch.cuda.synchronize()
@@ -1312,7 +1315,7 @@ def main():
         f"in {time.perf_counter() - t_gen:.1f}s")
 
     def step():
-        encoder.encode(items, starts, nb, out=enc)
+        encoder.encode(items32, starts, nb, out=enc)
         dec_ctx.decode(enc["buf"], enc["block_off"], nb, out, n_items)
 
     step()
@@ -1364,7 +1367,8 @@ def main():
         return a.elapsed_time(b) / reps
 
     reps = max(5, args.steps // 2)
-    enc_ms = timed(lambda: encoder.encode(items, starts, nb, out=enc), reps)
+    enc_ms = timed(lambda: encoder.encode(items32, starts, nb, out=enc), reps)
+    enc64_ms = timed(lambda: encoder.encode(items, starts, nb, out=enc), reps)  # (u64 offsets: the same bytes)
     dec_ms = timed(lambda: dec_ctx.decode(enc["buf"], enc["block_off"], nb, out, n_items), reps)
     kdec_ms = timed(lambda: dec_ctx.decode(enc["buf"], enc["block_off"], nb, out, n_items,
                                            tuning=(0, 0, 0, lsmgpu.DECODE_ITEM_START_VALID)), reps)
@@ -1393,8 +1397,8 @@ def main():
     if tms:
         r_dec["kernel_ms_trace"], r_dec["kernel_ms_trace_source"] = tms, tsrc
         r_dec["read_only_frac_trace"] = round(total_bytes / (tms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
-    r_enc = encode_roofline("lsm_encode_blocks (encode_plan_wave_kernel + scan + encode_group_kernel)", enc_ms,
-                            key_val, n_items, nb, total_bytes, ceil,
+    r_enc = encode_roofline("lsm_encode_blocks32 (encode_plan_wave_kernel + scan + encode_group_kernel)", enc_ms,
+                            key_val, n_items, nb, total_bytes, ceil, off_bytes=4, trace_kernels=
                             [("encode_plan_wave_kernel<false>", (nb + 127) // 128),
                              ("encode_group_kernel<false, false, false>", (nb + 31) // 32)] if nb == 1 << 20 else None)
     dominant = r_enc if enc_ms >= kdec_ms else r_dec
@@ -1453,13 +1457,17 @@ def main():
                                    "device-resident",
                        "blocks_per_gpu": nb, "items_per_gpu": n_items, "block_bytes_per_gpu": total_bytes,
                        "restart_interval": 16, "hash_ratio": 0.0, "key_len": 16, "val_len": 64,
-                       "step": "lsm_encode_blocks (item SoA -> blocks) + lsm_decode_blocks (blocks -> parsed SoA)",
+                       "step": "lsm_encode_blocks32 (item SoA, u32 offsets -> blocks) + lsm_decode_blocks "
+                               "(blocks -> parsed SoA)",
                        "parallelism": f"shard{world} (independent block batches, no collective)"},
             "roofline": dominant,
             "roofline_decode": r_dec,
             "roofline_encode": r_enc,
             "cpu_baseline": cpu,
-            "encode": {"ms": round(enc_ms, 4), "GiB_per_s_written": round(total_bytes / (enc_ms * 1e-3) / 2 ** 30, 3)},
+            "encode": {"ms": round(enc_ms, 4), "GiB_per_s_written": round(total_bytes / (enc_ms * 1e-3) / 2 ** 30, 3),
+                       "entry": "lsm_encode_blocks32 (u32 key / value offsets)",
+                       "u64_offsets_ms": round(enc64_ms, 4),
+                       "u64_offsets_note": "lsm_encode_blocks (lsm_items, u64 offsets) on the same items: same bytes"},
             "decode": {"ms": round(dec_ms, 4), "GiB_per_s": round(total_bytes / (dec_ms * 1e-3) / 2 ** 30, 3),
                        "kernel_ms": round(kdec_ms, 4),
                        "note": "whole lsm_decode_blocks call (trailer counts + scan + decode kernel)"},

@@ -152,9 +152,10 @@ size_t lsm_encode_workspace_size_ex(uint64_t n_items, uint32_t n_blocks, uint64_
   return lsmgpu::encode_workspace_size_ex(n_items, n_blocks, out_cap);
 }
 
-int lsm_encode_blocks(const lsm_items* d_items, const uint32_t* d_block_item_start, uint32_t n_blocks,
-                      const lsm_block_params* params, uint8_t* d_out, uint64_t out_cap, uint64_t* d_block_off,
-                      int32_t* d_status, void* d_workspace, size_t workspace_bytes, void* stream) {
+static int encode_blocks_common(const lsm_items* d_items, bool off32, const uint32_t* d_block_item_start,
+                                uint32_t n_blocks, const lsm_block_params* params, uint8_t* d_out, uint64_t out_cap,
+                                uint64_t* d_block_off, int32_t* d_status, void* d_workspace, size_t workspace_bytes,
+                                void* stream) {
   if (n_blocks == 0) return LSM_OK;
   if (!d_items || !params || !d_block_item_start || !d_out || !d_block_off || !d_status) return LSM_BAD_ARG;
   if (params->compression != 0) return LSM_UNSUPPORTED;
@@ -171,8 +172,37 @@ int lsm_encode_blocks(const lsm_items* d_items, const uint32_t* d_block_item_sta
   if (!d_workspace || workspace_bytes < lsmgpu::encode_workspace_size(d_items->n_items, n_blocks))
     return LSM_BAD_ARG;
   hipError_t e = lsmgpu::launch_encode(*d_items, d_block_item_start, n_blocks, *params, d_out, out_cap,
-                                       d_block_off, d_status, d_workspace, workspace_bytes, (hipStream_t)stream);
+                                       d_block_off, d_status, d_workspace, workspace_bytes, (hipStream_t)stream, off32);
   return e == hipSuccess ? LSM_OK : set_hip_error(e, "lsm_encode_blocks");
+}
+
+int lsm_encode_blocks(const lsm_items* d_items, const uint32_t* d_block_item_start, uint32_t n_blocks,
+                      const lsm_block_params* params, uint8_t* d_out, uint64_t out_cap, uint64_t* d_block_off,
+                      int32_t* d_status, void* d_workspace, size_t workspace_bytes, void* stream) {
+  return encode_blocks_common(d_items, false, d_block_item_start, n_blocks, params, d_out, out_cap, d_block_off,
+                              d_status, d_workspace, workspace_bytes, stream);
+}
+
+int lsm_encode_blocks32(const lsm_items32* d_items, const uint32_t* d_block_item_start, uint32_t n_blocks,
+                        const lsm_block_params* params, uint8_t* d_out, uint64_t out_cap, uint64_t* d_block_off,
+                        int32_t* d_status, void* d_workspace, size_t workspace_bytes, void* stream) {
+  if (n_blocks == 0) return LSM_OK;
+  if (!d_items) return LSM_BAD_ARG;
+  if (d_items->n_items >= 0xFFFFFFFFull) return LSM_BAD_ARG;  // (u32 offsets: arrays of n_items + 1 entries)
+  // the same kernels: key_off / val_off are read as u32 arrays (EncodeParams::off32)
+  lsm_items it{};
+  it.keys = d_items->keys;
+  it.key_off = reinterpret_cast<const uint64_t*>(d_items->key_off);
+  it.vals = d_items->vals;
+  it.val_off = reinterpret_cast<const uint64_t*>(d_items->val_off);
+  it.seqno = d_items->seqno;
+  it.vtype = d_items->vtype;
+  it.handle_off = d_items->handle_off;
+  it.handle_size = d_items->handle_size;
+  it.n_items = d_items->n_items;
+  if (!it.key_off || (params && params->block_type != LSM_BLOCK_INDEX && !it.val_off)) return LSM_BAD_ARG;
+  return encode_blocks_common(&it, true, d_block_item_start, n_blocks, params, d_out, out_cap, d_block_off, d_status,
+                              d_workspace, workspace_bytes, stream);
 }
 
 uint64_t lsm_cut_blocks(const uint64_t* key_off, const uint64_t* val_off, uint64_t n_items, uint32_t block_size,

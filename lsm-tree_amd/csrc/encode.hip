@@ -134,9 +134,24 @@ struct EncodeParams {
   uint8_t* huge_pool;   // workspace past encode_workspace_size (null: E3 one workgroup per block)
   uint64_t huge_pool_bytes;
   uint32_t huge_cap;    // huge-list entries the pool's layout provides
+  uint32_t off32;       // it.key_off / it.val_off hold u32 offsets (lsm_encode_blocks32, lsm_items32)
 };
 
 __device__ __forceinline__ bool is_index(const EncodeParams& P) { return P.type == 1; }
+
+// Key / value offset i: u64 arrays (lsm_items) or u32 arrays (lsm_items32: SURVEY 8(d)'s 4 + 4 B
+// per item, arenas < 4 GiB).  P.off32 is batch-wide (a scalar branch per load site).
+__device__ __forceinline__ uint64_t off_at(const EncodeParams& P, const uint64_t* a, uint64_t i) {
+  return P.off32 ? (uint64_t)gload(reinterpret_cast<const uint32_t*>(a), i) : gload(a, i);
+}
+__device__ __forceinline__ uint64_t koff(const EncodeParams& P, uint64_t i) { return off_at(P, P.it.key_off, i); }
+__device__ __forceinline__ uint64_t voff(const EncodeParams& P, uint64_t i) { return off_at(P, P.it.val_off, i); }
+// offset base + t with a wave-uniform base (SGPR pointer) and a per-lane t < 2^29 (32-bit byte offsets)
+__device__ __forceinline__ uint64_t off_rel(const EncodeParams& P, const uint64_t* a, uint64_t base, uint32_t t) {
+  if (P.off32)
+    return *reinterpret_cast<const uint32_t*>(reinterpret_cast<const uint8_t*>(reinterpret_cast<const uint32_t*>(a) + base) + 4u * t);
+  return *reinterpret_cast<const uint64_t*>(reinterpret_cast<const uint8_t*>(a + base) + 8u * t);
+}
 
 // d_block_item_start[i] as E1 walks it: clamped to n_items, so no item field
 // past the arenas is read (the reference takes &[InternalValue],
@@ -313,8 +328,8 @@ struct RawItem {
 template <bool kIndex>
 __device__ __forceinline__ RawItem load_raw(const EncodeParams& P, uint64_t i) {
   RawItem r;
-  r.ko = P.it.key_off[i];
-  r.ko1 = P.it.key_off[i + 1];
+  r.ko = koff(P, i);
+  r.ko1 = koff(P, i + 1);
   r.seq = P.it.seqno[i];
   r.e = 0;
   r.hb = kNoBucket;
@@ -323,8 +338,8 @@ __device__ __forceinline__ RawItem load_raw(const EncodeParams& P, uint64_t i) {
     r.vo1 = P.it.handle_size[i];
     r.vt = 0;
   } else {
-    r.vo = P.it.val_off[i];
-    r.vo1 = P.it.val_off[i + 1];
+    r.vo = voff(P, i);
+    r.vo1 = voff(P, i + 1);
     r.vt = P.it.vtype[i];
   }
   return r;
@@ -338,8 +353,8 @@ __device__ __forceinline__ RawItem load_raw_rel(const EncodeParams& P, uint64_t 
     return *reinterpret_cast<const uint64_t*>(reinterpret_cast<const uint8_t*>(a + base) + 8u * k);
   };
   RawItem r;
-  r.ko = at64(P.it.key_off, t);
-  r.ko1 = at64(P.it.key_off, t + 1);
+  r.ko = off_rel(P, P.it.key_off, base, t);
+  r.ko1 = off_rel(P, P.it.key_off, base, t + 1);
   r.seq = at64(P.it.seqno, t);
   r.e = 0;
   r.hb = kNoBucket;
@@ -348,8 +363,8 @@ __device__ __forceinline__ RawItem load_raw_rel(const EncodeParams& P, uint64_t 
     r.vo1 = (P.it.handle_size + base)[t];
     r.vt = 0;
   } else {
-    r.vo = at64(P.it.val_off, t);
-    r.vo1 = at64(P.it.val_off, t + 1);
+    r.vo = off_rel(P, P.it.val_off, base, t);
+    r.vo1 = off_rel(P, P.it.val_off, base, t + 1);
     r.vt = (P.it.vtype + base)[t];
   }
   return r;
@@ -383,8 +398,8 @@ __device__ __forceinline__ ItemMeta cook_item(const RawItem& r, bool& bad) {
 
 __device__ __forceinline__ ItemMeta load_item(const EncodeParams& P, uint64_t i, bool& bad) {
   ItemMeta m;
-  m.ko = gload(P.it.key_off, i);  // (gload: global loads, not flat ones)
-  const uint64_t kl = gload(P.it.key_off, i + 1) - m.ko;
+  m.ko = koff(P, i);  // (global loads, not flat ones)
+  const uint64_t kl = koff(P, i + 1) - m.ko;
   if (kl > 0xFFFF) bad = true;
   m.klen = (uint32_t)min(kl, (uint64_t)0xFFFF);
   m.seq = gload(P.it.seqno, i);
@@ -395,8 +410,8 @@ __device__ __forceinline__ ItemMeta load_item(const EncodeParams& P, uint64_t i,
     m.vl = gload(P.it.handle_size, i);
     m.vt = 0;
   } else {
-    m.vo = gload(P.it.val_off, i);
-    const uint64_t vl = gload(P.it.val_off, i + 1) - m.vo;
+    m.vo = voff(P, i);
+    const uint64_t vl = voff(P, i + 1) - m.vo;
     m.vt = gload(P.it.vtype, i);
     if (!valid_vtype(m.vt)) bad = true;
     if (!is_tombstone(m.vt) && vl > 0xFFFFFFFFULL) bad = true;
@@ -413,8 +428,8 @@ __device__ __forceinline__ ItemMeta load_item_lcp(const EncodeParams& P, uint32_
   ItemMeta m = load_item(P, i, bad);
   if (!is_index(P) && j % ri != 0) {
     const uint64_t h = (uint64_t)s + (j / ri) * ri;
-    const uint64_t hko = P.it.key_off[h];
-    const uint32_t hkl = (uint32_t)min(P.it.key_off[h + 1] - hko, (uint64_t)0xFFFF);
+    const uint64_t hko = koff(P, h);
+    const uint32_t hkl = (uint32_t)min(koff(P, h + 1) - hko, (uint64_t)0xFFFF);
     m.sh = lcp_global(P.it.keys, hko, m.ko, min(hkl, m.klen));
   }
   return m;
@@ -966,8 +981,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void e
         hq[q] = 0;
         if (i < i_end && jjq[q] % ri != 0) {
           const uint64_t h = i - jjq[q] % ri;  // restart head of item i
-          const uint64_t hko = h >= base ? kos[h - base] : P.it.key_off[h];
-          const uint64_t hke = h + 1 >= base ? kos[h + 1 - base] : P.it.key_off[h + 1];
+          const uint64_t hko = h >= base ? kos[h - base] : koff(P, h);
+          const uint64_t hke = h + 1 >= base ? kos[h + 1 - base] : koff(P, h + 1);
           const uint32_t hkl = (uint32_t)min(hke - hko, (uint64_t)0xFFFF);
           nq[q] = min(hkl, m[q].klen);
           hq[q] = hko;
@@ -1048,8 +1063,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void e
   const uint32_t hash_w = (buckets > 0 && bin_len <= kHashMaxPointers) ? buckets : 0;
   const uint64_t total = kHdrLen + recs + 1 + (uint64_t)bin_len * step + hash_w + kTrailerLen;
   if (recs > 0xFFFFFFF0ULL || total > 0xFFFFFF00ULL) bad = true;
-  const uint64_t ks = P.it.key_off[s], ke = P.it.key_off[e];
-  const uint64_t vs = kIndex ? 0 : P.it.val_off[s], ve = kIndex ? 0 : P.it.val_off[e];
+  const uint64_t ks = koff(P, s), ke = koff(P, e);
+  const uint64_t vs = kIndex ? 0 : voff(P, s), ve = kIndex ? 0 : voff(P, e);
   uint32_t flags = 0;
   if (bad) {
     flags = kPlanBad;
@@ -1135,8 +1150,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
     };
 #pragma unroll
     for (uint32_t q = 0; q <= kPW; ++q) {
-      r.ko[q] = at64(P.it.key_off, min(t + q, n));
-      r.vo[q] = at64(P.it.val_off, min(t + q, n));
+      r.ko[q] = off_rel(P, P.it.key_off, base, min(t + q, n));
+      r.vo[q] = off_rel(P, P.it.val_off, base, min(t + q, n));
     }
 #pragma unroll
     for (uint32_t q = 0; q < kPW; ++q) {
@@ -1311,8 +1326,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
   const uint32_t hash_w = (buckets > 0 && bin_len <= kHashMaxPointers) ? buckets : 0;
   const uint64_t total = kHdrLen + recs + 1 + (uint64_t)bin_len * step + hash_w + kTrailerLen;
   if (recs > 0xFFFFFFF0ULL || total > 0xFFFFFF00ULL) bad = true;
-  const uint64_t ks = P.it.key_off[s], ke = P.it.key_off[e];
-  const uint64_t vs = P.it.val_off[s], ve = P.it.val_off[e];
+  const uint64_t ks = koff(P, s), ke = koff(P, e);
+  const uint64_t vs = voff(P, s), ve = voff(P, e);
   uint32_t flags = 0;
   if (bad) {
     flags = kPlanBad;
@@ -1608,8 +1623,8 @@ __global__ __launch_bounds__(256) void encode_e1p_lengths_kernel(EncodeParams P)
       r[j] = load_raw<false>(P, i);
       if (!head[j]) {
         const uint64_t h = (uint64_t)i - (i - T.s[j]) % ri;
-        hko[j] = gload(P.it.key_off, h);
-        hko1[j] = gload(P.it.key_off, h + 1);
+        hko[j] = koff(P, h);
+        hko1[j] = koff(P, h + 1);
       }
     }
   }
@@ -1717,8 +1732,8 @@ __global__ __launch_bounds__(256) void encode_e1p_blocks_kernel(EncodeParams P) 
   const uint32_t hash_w = (buckets > 0 && bin_len <= kHashMaxPointers) ? buckets : 0;
   const uint64_t total = kHdrLen + recs + 1 + (uint64_t)bin_len * step + hash_w + kTrailerLen;
   if (recs > 0xFFFFFFF0ULL || total > 0xFFFFFF00ULL) bad = true;
-  const uint64_t ks = P.it.key_off[s], ke = P.it.key_off[e];
-  const uint64_t vs = P.it.val_off[s], ve = P.it.val_off[e];
+  const uint64_t ks = koff(P, s), ke = koff(P, e);
+  const uint64_t vs = voff(P, s), ve = voff(P, e);
   uint32_t flags = 0;
   if (bad) {
     flags = kPlanBad;
@@ -1783,9 +1798,9 @@ __global__ __launch_bounds__(256) void encode_bucket_fixup_kernel(EncodeParams P
     if (!hw || hw >= kNeedHash) continue;
     for (uint32_t i = s + lane; i < e; i += kWave) {
       if (P.hbucket[i] != kNeedHash) continue;
-      const uint64_t ko = P.it.key_off[i];
+      const uint64_t ko = koff(P, i);
       // (E1 checked every key of a good block: <= 0xFFFF bytes; the cap is the same as E1's)
-      const uint32_t klen = (uint32_t)min(P.it.key_off[i + 1] - ko, (uint64_t)0xFFFF);
+      const uint32_t klen = (uint32_t)min(koff(P, i + 1) - ko, (uint64_t)0xFFFF);
       const uint64_t hv = xxh3_64_any(klen, BaseReader8{P.it.keys + ko, 0}, BaseReader64{P.it.keys + ko, 0});
       P.hbucket[i] = (uint16_t)(hv % hw);
     }
@@ -2340,8 +2355,8 @@ __global__ __launch_bounds__(kE3Threads) void encode_large_kernel(EncodeParams P
       __syncthreads();
       for (uint32_t j = tid; j < n; j += kE3Threads) {
         const uint64_t i = (uint64_t)s + j;
-        const uint64_t ko = P.it.key_off[i];
-        const uint32_t bk = key_bucket(P, ko, (uint32_t)(P.it.key_off[i + 1] - ko), pl.hash_w);
+        const uint64_t ko = koff(P, i);
+        const uint32_t bk = key_bucket(P, ko, (uint32_t)(koff(P, i + 1) - ko), pl.hash_w);
         if (bk >= base && bk < base + lim) {
           atomicMin(&hlo[bk - base], j / ri);
           atomicMax(&hhi[bk - base], j / ri);
@@ -2672,8 +2687,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
       __syncthreads();
       for (uint32_t j = tid; j < h.n; j += 256) {
         const uint64_t it = (uint64_t)h.s + j;
-        const uint64_t ko = P.it.key_off[it];
-        const uint32_t bk = key_bucket(P, ko, (uint32_t)(P.it.key_off[it + 1] - ko), pl.hash_w);
+        const uint64_t ko = koff(P, it);
+        const uint32_t bk = key_bucket(P, ko, (uint32_t)(koff(P, it + 1) - ko), pl.hash_w);
         if (bk >= base && bk < base + lim) {
           atomicMin(&hlo[bk - base], j / ri);
           atomicMax(&hhi[bk - base], j / ri);
@@ -2921,9 +2936,10 @@ uint64_t encode_bound(uint64_t n_items, uint32_t n_blocks, uint64_t key_bytes, u
 
 hipError_t launch_encode(const lsm_items& items, const uint32_t* starts, uint32_t n_blocks,
                          const lsm_block_params& params, uint8_t* out, uint64_t out_cap, uint64_t* block_off,
-                         int32_t* status, void* ws, size_t ws_bytes, hipStream_t st) {
+                         int32_t* status, void* ws, size_t ws_bytes, hipStream_t st, bool off32) {
   EncodeParams P;
   P.it = items;
+  P.off32 = off32 ? 1u : 0u;
   P.starts = starts;
   P.n_blocks = n_blocks;
   P.ri = params.block_type == 1 ? 1 : params.restart_interval;

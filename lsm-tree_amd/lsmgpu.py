@@ -30,6 +30,12 @@ class LsmItems(C.Structure):
                 ("handle_size", C.c_void_p), ("n_items", C.c_uint64)]
 
 
+class LsmItems32(C.Structure):  # lsm_items32: u32 key / value offsets (lsm_encode_blocks32)
+    _fields_ = [("keys", C.c_void_p), ("key_off", C.c_void_p), ("vals", C.c_void_p), ("val_off", C.c_void_p),
+                ("seqno", C.c_void_p), ("vtype", C.c_void_p), ("handle_off", C.c_void_p),
+                ("handle_size", C.c_void_p), ("n_items", C.c_uint64)]
+
+
 class LsmParsed(C.Structure):
     _fields_ = [("seqno", C.c_void_p), ("key_off", C.c_void_p), ("val_off", C.c_void_p), ("val_len", C.c_void_p),
                 ("key_len", C.c_void_p), ("prefix_len", C.c_void_p), ("vtype", C.c_void_p),
@@ -122,6 +128,10 @@ def lib():
         L.lsm_encode_blocks.argtypes = [C.POINTER(LsmItems), C.c_void_p, C.c_uint32, C.POINTER(LsmBlockParams),
                                         C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t,
                                         C.c_void_p]
+        L.lsm_encode_blocks32.restype = C.c_int
+        L.lsm_encode_blocks32.argtypes = [C.POINTER(LsmItems32), C.c_void_p, C.c_uint32, C.POINTER(LsmBlockParams),
+                                          C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t,
+                                          C.c_void_p]
         L.lsm_cut_blocks.restype = C.c_uint64
         L.lsm_cut_blocks.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p, C.c_uint64]
         L.lsm_xxh3_128_batch.restype = C.c_int
@@ -219,7 +229,8 @@ def lib():
 EXPORTED_SYMBOLS = ["lsm_abi_version", "lsm_status_name", "lsm_last_error", "lsm_device_count", "lsm_set_device",
                     "lsm_decode_workspace_size", "lsm_decode_workspace_size_ex", "lsm_decode_blocks", "lsm_decode_blocks_tuned", "lsm_decode_blocks16",
                     "lsm_encode_bound",
-                    "lsm_encode_workspace_size", "lsm_encode_workspace_size_ex", "lsm_encode_blocks", "lsm_cut_blocks", "lsm_xxh3_128_batch",
+                    "lsm_encode_workspace_size", "lsm_encode_workspace_size_ex", "lsm_encode_blocks", "lsm_encode_blocks32",
+                    "lsm_cut_blocks", "lsm_xxh3_128_batch",
                     "lsm_point_read_blocks", "lsm_xxh3_128_file_workspace_size", "lsm_xxh3_128_file",
                     "lsm_bloom_calculate_m", "lsm_bloom_shape", "lsm_bloom_filter_size", "lsm_hash64_keys",
                     "lsm_bloom_build", "lsm_bloom_contains", "lsm_lz4_workspace_size", "lsm_lz4_decompress_blocks",
@@ -386,12 +397,16 @@ class Encoder:
                out=None, stream=None, pool=None, workspace_bytes=None):
         """items: dict of cuda tensors keys(u8, padded) key_off(i64 n+1) vals(u8, padded) val_off(i64 n+1)
         seqno(i64) vtype(u8) [handle_off(i64) handle_size(i32)]; starts: int32 cuda [n_blocks+1].
+        key_off / val_off as int32 tensors (arenas < 4 GiB): lsm_encode_blocks32 (u32 offsets).
         pool=False: the base workspace only (blocks > 96 KiB on one workgroup each);
         None (default): the pool when the output bound averages 32 KiB per block or more;
         workspace_bytes: pass exactly that much workspace (tests of a pool too small)."""
         torch = _torch()
         n_items = items["seqno"].numel()
-        it = LsmItems()
+        off32 = items["key_off"].element_size() == 4
+        if off32 and "val_off" in items and items["val_off"].element_size() != 4:
+            raise LsmError("key_off and val_off must have the same width")
+        it = LsmItems32() if off32 else LsmItems()
         it.keys = items["keys"].data_ptr()
         it.key_off = items["key_off"].data_ptr()
         it.vals = items["vals"].data_ptr() if "vals" in items else items["keys"].data_ptr()
@@ -419,10 +434,10 @@ class Encoder:
             out = {"buf": torch.empty(bound + LSM_INPUT_PADDING, dtype=torch.uint8, device=self.device),
                    "block_off": torch.empty(n_blocks + 1, dtype=torch.int64, device=self.device),
                    "status": torch.empty(max(n_blocks, 1), dtype=torch.int32, device=self.device)}
-        rc = lib().lsm_encode_blocks(C.byref(it), _ptr(starts), n_blocks, C.byref(params), _ptr(out["buf"]),
-                                     bound, _ptr(out["block_off"]), _ptr(out["status"]), _ptr(self.ws),
-                                     need, _stream(stream))
-        _check(rc, "lsm_encode_blocks")
+        fn = lib().lsm_encode_blocks32 if off32 else lib().lsm_encode_blocks
+        rc = fn(C.byref(it), _ptr(starts), n_blocks, C.byref(params), _ptr(out["buf"]), bound,
+                _ptr(out["block_off"]), _ptr(out["status"]), _ptr(self.ws), need, _stream(stream))
+        _check(rc, "lsm_encode_blocks32" if off32 else "lsm_encode_blocks")
         return out
 
 
@@ -801,13 +816,17 @@ def cut_blocks(key_off, val_off, block_size):
     return starts[:nb + 1].copy()
 
 
-def items_to_device(items_np, device="cuda"):
-    """pyoracle.Items-like numpy SoA -> dict of padded cuda tensors for Encoder.encode."""
+def items_to_device(items_np, device="cuda", off32=False):
+    """pyoracle.Items-like numpy SoA -> dict of padded cuda tensors for Encoder.encode
+    (off32: int32 key / value offsets, encoded through lsm_encode_blocks32)."""
     import numpy as np
     torch = _torch()
     d = {"keys": to_device_bytes(items_np.keys, device), "vals": to_device_bytes(items_np.vals, device)}
-    d["key_off"] = torch.from_numpy(items_np.key_off.astype(np.int64)).to(device)
-    d["val_off"] = torch.from_numpy(items_np.val_off.astype(np.int64)).to(device)
+    ot = np.int32 if off32 else np.int64
+    if off32 and (int(items_np.key_off[-1]) >= 1 << 32 or int(items_np.val_off[-1]) >= 1 << 32):
+        raise LsmError("off32: arenas of 4 GiB or more need the u64 offsets")
+    d["key_off"] = torch.from_numpy(items_np.key_off.astype(np.uint32 if off32 else np.int64).view(ot)).to(device)
+    d["val_off"] = torch.from_numpy(items_np.val_off.astype(np.uint32 if off32 else np.int64).view(ot)).to(device)
     d["seqno"] = torch.from_numpy(items_np.seqno.view(np.int64)).to(device)
     d["vtype"] = torch.from_numpy(items_np.vtype).to(device)
     d["handle_off"] = torch.from_numpy(items_np.handle_off.view(np.int64)).to(device)

@@ -34,9 +34,13 @@ def child(reps, which):
               "k64c": dict(n_blocks=24552, items_per_block=820), "k64r": dict(n_blocks=20682, items_per_block=820,
                                                                            kind="random")}
     for name in which.split(","):
-        items, starts, n = bench.make_workload(torch, lsmgpu, **shapes[name])
-        nb = shapes[name]["n_blocks"]
-        hr = 1.33 if name == "h1" else 0.0
+        off32 = name.endswith("_32")  # the same shape through lsm_encode_blocks32 (u32 offsets)
+        base = name[:-3] if off32 else name
+        items, starts, n = bench.make_workload(torch, lsmgpu, **shapes[base])
+        if off32:
+            items = dict(items, key_off=items["key_off"].to(torch.int32), val_off=items["val_off"].to(torch.int32))
+        nb = shapes[base]["n_blocks"]
+        hr = 1.33 if base == "h1" else 0.0
         enc_ctx = lsmgpu.Encoder()
         enc = enc_ctx.encode(items, starts, nb, hash_ratio=hr)
         torch.cuda.synchronize()

@@ -14,7 +14,7 @@ C_TO_RUST = {
     "int": "c_int", "size_t": "usize", "float": "f32",
     "uint8_t": "u8", "uint16_t": "u16", "uint32_t": "u32", "uint64_t": "u64",
     "int32_t": "i32", "int64_t": "i64", "char": "c_char", "void": "c_void",
-    "lsm_items": "LsmItems", "lsm_parsed_items": "LsmParsedItems", "lsm_parsed_items16": "LsmParsedItems16",
+    "lsm_items": "LsmItems", "lsm_items32": "LsmItems32", "lsm_parsed_items": "LsmParsedItems", "lsm_parsed_items16": "LsmParsedItems16",
     "lsm_block_params": "LsmBlockParams", "lsm_decode_tuning": "LsmDecodeTuning",
     "lsm_point_result": "LsmPointResult", "lsm_table_scan": "LsmTableScan",
 }
