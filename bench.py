@@ -1399,8 +1399,8 @@ def main():
         r_dec["read_only_frac_trace"] = round(total_bytes / (tms * 1e-3) / 1e9 / HBM_PEAK_GBPS, 4)
     r_enc = encode_roofline("lsm_encode_blocks32 (encode_plan_wave_kernel + scan + encode_group_kernel)", enc_ms,
                             key_val, n_items, nb, total_bytes, ceil, off_bytes=4, trace_kernels=
-                            [("encode_plan_wave_kernel<false>", (nb + 127) // 128),
-                             ("encode_group_kernel<false, false, false>", (nb + 31) // 32)] if nb == 1 << 20 else None)
+                            [("encode_plan_wave_kernel<false, 4>", (nb + 127) // 128),
+                             ("encode_group_kernel<false, false, false, 4>", (nb + 31) // 32)] if nb == 1 << 20 else None)
     dominant = r_enc if enc_ms >= kdec_ms else r_dec
 
     extra = {}

@@ -128,10 +128,11 @@ def lib():
         L.lsm_encode_blocks.argtypes = [C.POINTER(LsmItems), C.c_void_p, C.c_uint32, C.POINTER(LsmBlockParams),
                                         C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t,
                                         C.c_void_p]
-        L.lsm_encode_blocks32.restype = C.c_int
-        L.lsm_encode_blocks32.argtypes = [C.POINTER(LsmItems32), C.c_void_p, C.c_uint32, C.POINTER(LsmBlockParams),
-                                          C.c_void_p, C.c_uint64, C.c_void_p, C.c_void_p, C.c_void_p, C.c_size_t,
-                                          C.c_void_p]
+        if hasattr(L, "lsm_encode_blocks32"):  # (variant builds of earlier trees lack it: A/B scripts)
+            L.lsm_encode_blocks32.restype = C.c_int
+            L.lsm_encode_blocks32.argtypes = [C.POINTER(LsmItems32), C.c_void_p, C.c_uint32,
+                                              C.POINTER(LsmBlockParams), C.c_void_p, C.c_uint64, C.c_void_p,
+                                              C.c_void_p, C.c_void_p, C.c_size_t, C.c_void_p]
         L.lsm_cut_blocks.restype = C.c_uint64
         L.lsm_cut_blocks.argtypes = [C.c_void_p, C.c_void_p, C.c_uint64, C.c_uint32, C.c_void_p, C.c_uint64]
         L.lsm_xxh3_128_batch.restype = C.c_int

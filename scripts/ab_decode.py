@@ -1,7 +1,8 @@
 #!/usr/bin/env python3
 """A/B timing of library variants on the decode bench workloads.
 
-usage: scripts/ab_decode.py LIB1 LIB2 ... [--rounds 3] [--which c1,c3] [--modes full,compact]
+usage: scripts/ab_decode.py LIB1 LIB2 ... [--rounds 3] [--which c1,c3] [--modes full,compact,call]
+(modes full / compact: the decode with item_start precomputed; call: the whole lsm_decode_blocks call)
 Each round runs every library in its own child process (interleaved); a child
 encodes the workload once, then times lsm_decode_blocks (item_start
 precomputed) in each output mode, interleaved within the child as well, and
@@ -51,8 +52,9 @@ def child(reps, which, modes):
             for m in modes:
                 e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 e0.record()
-                for _ in range(reps):
-                    dec.decode(enc["buf"], enc["block_off"], nb, outs[m], n, tuning=tune, compact=m == "compact")
+                for _ in range(reps):  # (mode "call": the whole call, item_start counted and scanned too)
+                    dec.decode(enc["buf"], enc["block_off"], nb, outs[m], n, tuning=None if m == "call" else tune,
+                               compact=m == "compact")
                 e1.record()
                 torch.cuda.synchronize()
                 times[m].append(e0.elapsed_time(e1) / reps)
@@ -60,6 +62,7 @@ def child(reps, which, modes):
             o = outs[m]
             bad = int((o["status"][:nb] != 0).sum())
             ck = int(sum(int(o[f][:n].to(torch.int64).sum()) for f in ("key_off", "val_off", "val_len", "key_len")))
+            ck += int(o["item_start"][:nb + 1].to(torch.int64).sum())
             res[f"{name}.{m}"] = {"ms": round(min(times[m]), 4), "bad": bad, "ck": ck}
         del enc, outs
         torch.cuda.empty_cache()
