@@ -318,6 +318,11 @@ struct SpanCopy {
 };
 
 // One item's fields, loaded once per lane (all loads independent).
+// 16-B copy-out store of the list / huge-block kernels (non-temporal: plain stores measured
+// 0 to +2 % slower for the configs[4] classes, profiles/r06_experiments.txt; the group
+// kernel's copy-out is plain)
+__device__ __forceinline__ void copy_store16(u32x4* dst, const u32x4& v) { __builtin_nontemporal_store(v, dst); }
+
 struct ItemMeta {
   uint64_t ko, vo, seq;
   uint32_t klen, vl, vt, sh;
@@ -629,7 +634,7 @@ __device__ __forceinline__ void finish_block_lds(const EncodeParams& P, uint32_t
     const uint32_t lo = c * 16, hi = lo + 16;
     if (lo >= pad && hi <= pad + total) {
       // streaming output: non-temporal (measured 2 % faster than a plain store)
-      __builtin_nontemporal_store(reinterpret_cast<const u32x4*>(img)[c], reinterpret_cast<u32x4*>(gdst) + c);
+      copy_store16(reinterpret_cast<u32x4*>(gdst) + c, reinterpret_cast<const u32x4*>(img)[c]);
     } else {
       for (uint32_t k = max(lo, pad); k < min(hi, pad + total); ++k) gdst[k] = img[k];
     }
@@ -799,7 +804,7 @@ __device__ __forceinline__ void write_block_lds_mw(const EncodeParams& P, uint32
   for (uint32_t c = tid; c < chunks; c += kT) {
     const uint32_t clo = c * 16, chi = clo + 16;
     if (clo >= pad && chi <= pad + total) {
-      __builtin_nontemporal_store(reinterpret_cast<const u32x4*>(img)[c], reinterpret_cast<u32x4*>(gdst) + c);
+      copy_store16(reinterpret_cast<u32x4*>(gdst) + c, reinterpret_cast<const u32x4*>(img)[c]);
     } else {
       for (uint32_t k = max(clo, pad); k < min(chi, pad + total); ++k) gdst[k] = img[k];
     }
@@ -2670,7 +2675,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
           const uint32_t lo = (p0 + rb) - a0, c0 = (lo + 15) >> 4, c1 = lend >> 4;
           const u32x4* src = reinterpret_cast<const u32x4*>(lbuf);
           u32x4* dst = reinterpret_cast<u32x4*>(img + a0);
-          for (uint32_t c = c0 + tid; c < c1; c += 256) __builtin_nontemporal_store(src[c], dst + c);
+          for (uint32_t c = c0 + tid; c < c1; c += 256) copy_store16(dst + c, src[c]);
           // the partial pieces at both ends (shared with the neighbouring units' records)
           auto* gb = (__attribute__((address_space(1))) uint8_t*)(img + a0);
           const uint8_t* lb = reinterpret_cast<const uint8_t*>(lbuf);
