@@ -26,6 +26,7 @@
 #include <math.h>
 
 #include <algorithm>
+#include <type_traits>
 
 #include "block_format.hpp"
 #include "decode.hpp"
@@ -333,18 +334,33 @@ constexpr uint32_t kNoBucket = 0xFFFF;
 
 constexpr uint32_t kNeedHash = 0xFFFE;  // E1 left this key (> 16 bytes) to encode_bucket_fixup_kernel
 
-// An item's fields exactly as loaded (E2's one-group-ahead prefetch).
-struct RawItem {
-  uint64_t ko, ko1, vo, vo1, seq;
+// An item's fields exactly as loaded (E2's one-group-ahead prefetch).  The
+// offsets keep the width they were loaded with (RawItemT<4>: u32), so nothing
+// widens them before cook_item consumes them: a zero-extension at the load
+// made the compiler wait for the prefetched loads right there (the u32 group
+// kernel ran 5 % slower with u64 fields here).
+template <int kOW = 0, bool kIdx = false>
+struct RawItemT {
+  typedef typename std::conditional<kOW == 4, uint32_t, uint64_t>::type off_t;
+  typedef typename std::conditional<kOW == 4 && !kIdx, uint32_t, uint64_t>::type voff_t;  // (index: handle offset)
+  off_t ko, ko1;
+  voff_t vo, vo1;  // (vo1: the index handle size for index blocks)
+  uint64_t seq;
   uint32_t vt, e, hb;
 };
+typedef RawItemT<0> RawItem;
 
 // Plain loads of item i's fields (no arithmetic, so no wait is forced here).
 template <bool kIndex, int kOW = 0>
-__device__ __forceinline__ RawItem load_raw(const EncodeParams& P, uint64_t i) {
-  RawItem r;
-  r.ko = koff<kOW>(P, i);
-  r.ko1 = koff<kOW>(P, i + 1);
+__device__ __forceinline__ RawItemT<kOW, kIndex> load_raw(const EncodeParams& P, uint64_t i) {
+  RawItemT<kOW, kIndex> r;
+  if (kOW == 4) {
+    r.ko = gload(reinterpret_cast<const uint32_t*>(P.it.key_off), i);
+    r.ko1 = gload(reinterpret_cast<const uint32_t*>(P.it.key_off), i + 1);
+  } else {
+    r.ko = koff<kOW>(P, i);
+    r.ko1 = koff<kOW>(P, i + 1);
+  }
   r.seq = P.it.seqno[i];
   r.e = 0;
   r.hb = kNoBucket;
@@ -353,8 +369,13 @@ __device__ __forceinline__ RawItem load_raw(const EncodeParams& P, uint64_t i) {
     r.vo1 = P.it.handle_size[i];
     r.vt = 0;
   } else {
-    r.vo = voff<kOW>(P, i);
-    r.vo1 = voff<kOW>(P, i + 1);
+    if (kOW == 4) {
+      r.vo = gload(reinterpret_cast<const uint32_t*>(P.it.val_off), i);
+      r.vo1 = gload(reinterpret_cast<const uint32_t*>(P.it.val_off), i + 1);
+    } else {
+      r.vo = voff<kOW>(P, i);
+      r.vo1 = voff<kOW>(P, i + 1);
+    }
     r.vt = P.it.vtype[i];
   }
   return r;
@@ -387,10 +408,10 @@ __device__ __forceinline__ RawItem load_raw_rel(const EncodeParams& P, uint64_t 
 
 // Derived fields of a raw item and the writer's argument checks (key length
 // <= u16, a known value type, value length <= u32).
-template <bool kIndex>
-__device__ __forceinline__ ItemMeta cook_item(const RawItem& r, bool& bad) {
+template <bool kIndex, class R>
+__device__ __forceinline__ ItemMeta cook_item(const R& r, bool& bad) {
   ItemMeta m;
-  const uint64_t kl = r.ko1 - r.ko;
+  const uint64_t kl = (uint64_t)r.ko1 - (uint64_t)r.ko;  // (widened first: a decreasing pair is bad at any width)
   if (kl > 0xFFFF) bad = true;
   m.ko = r.ko;
   m.klen = (uint32_t)min(kl, (uint64_t)0xFFFF);
@@ -403,7 +424,7 @@ __device__ __forceinline__ ItemMeta cook_item(const RawItem& r, bool& bad) {
   if (kIndex) {
     m.vl = (uint32_t)r.vo1;
   } else {
-    const uint64_t vl = r.vo1 - r.vo;
+    const uint64_t vl = (uint64_t)r.vo1 - (uint64_t)r.vo;
     if (!valid_vtype(m.vt)) bad = true;
     if (!is_tombstone(m.vt) && vl > 0xFFFFFFFFULL) bad = true;
     m.vl = (uint32_t)vl;
@@ -1153,8 +1174,9 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
   uint32_t* wkls = kls[wave];
   Win16* wkwin = kwin[wave];
   // a lane's two consecutive items: key / value offsets [t, t + 3), seqnos and types [t, t + 2)
-  struct StepRaw {
-    uint64_t ko[kPW + 1], vo[kPW + 1], seq[kPW];
+  struct StepRaw {  // (offsets at their loaded width: see RawItemT)
+    typename RawItemT<kOW>::off_t ko[kPW + 1], vo[kPW + 1];
+    uint64_t seq[kPW];
     uint32_t vt[kPW];
   };
   auto load_step = [&](uint32_t base, StepRaw& r) {
@@ -1165,8 +1187,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
     };
 #pragma unroll
     for (uint32_t q = 0; q <= kPW; ++q) {
-      r.ko[q] = off_rel<kOW>(P, P.it.key_off, base, min(t + q, n));
-      r.vo[q] = off_rel<kOW>(P, P.it.val_off, base, min(t + q, n));
+      r.ko[q] = (typename RawItemT<kOW>::off_t)off_rel<kOW>(P, P.it.key_off, base, min(t + q, n));
+      r.vo[q] = (typename RawItemT<kOW>::off_t)off_rel<kOW>(P, P.it.val_off, base, min(t + q, n));
     }
 #pragma unroll
     for (uint32_t q = 0; q < kPW; ++q) {
@@ -1174,14 +1196,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
       r.vt[q] = (P.it.vtype + base)[min(t + q, n - 1)];
     }
   };
-  StepRaw raw, nxt;
+  StepRaw raw;
   if (ia < ie) load_step(ia, raw);
   uint64_t carry = 0;     // record bytes of this wave's items before the step
   uint64_t hk_ko = 0;     // the last restart head of the previous step: key offset, key length
   uint32_t hk_kl = 0;
   Win16 hk_win{0, 0};
   for (uint32_t base = ia; base < ie; base += kPWStep) {
-    if (base + kPWStep < ie) load_step(base + kPWStep, nxt);  // in flight under this step
     const uint32_t t0 = kPW * lane;
     ItemMeta m[kPW];
     uint32_t jq[kPW], jjq[kPW];
@@ -1219,6 +1240,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
       wkos[t0 + q] = m[q].ko;
       wkls[t0 + q] = m[q].klen;
     }
+    // the next step's item fields, into the registers just consumed (no copy at the
+    // step's end, which made the compiler wait for them there), in flight under this
+    // step; issued before the key windows, which the step waits for
+    if (base + kPWStep < ie) load_step(base + kPWStep, raw);
     // ---- shared prefix with the restart head: every item loads its own first 16
     // key bytes once; the others of its interval read the head's from LDS
     Win16 wa[kPW], wb[kPW];
@@ -1327,7 +1352,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
       }
     }
     wave_lds_sync();  // (the next step rewrites kos / kls)
-    raw = nxt;
   }
   __syncthreads();
   if (tid >= nb) return;
@@ -1920,7 +1944,7 @@ __global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(4))) 
   // item 2 or 4 threads (tpi = 1 << tsh), which split its value copy; thread t
   // serves item t >> tsh, part t & (tpi - 1).
   auto tpi_shift = [&](uint32_t n) -> uint32_t { return n <= kGThreads / 4 ? 2u : n <= kGThreads / 2 ? 1u : 0u; };
-  auto load_items = [&](const Grp& g, RawItem& r) {
+  auto load_items = [&](const Grp& g, RawItemT<kOW, kIndex>& r) {
     const uint32_t r0 = g.b - b_begin;
     const uint32_t i0 = rl32(r_start, r0), n = rl32(r_start, r0 + g.k) - i0;
     const uint64_t i = (uint64_t)i0 + min(tid >> tpi_shift(n), n - 1);
@@ -1928,7 +1952,7 @@ __global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(4))) 
     r.e = P.erec[i];
     if (kPlanBkt) r.hb = P.hbucket[i];
   };
-  auto cook = [&](const RawItem& r) {
+  auto cook = [&](const RawItemT<kOW, kIndex>& r) {
     bool bad = false;  // (vetted by the plan pass)
     return cook_item<kIndex>(r, bad);
   };
@@ -1942,7 +1966,7 @@ __global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(4))) 
   uint32_t ph_n = 0;
 #endif
   Grp G = next_group(b_begin);
-  RawItem raw{};
+  RawItemT<kOW, kIndex> raw{};
   if (G.k) {
     issue_dma(G);
     load_items(G, raw);

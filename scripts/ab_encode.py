@@ -32,7 +32,10 @@ def child(reps, which):
               "k16c": dict(n_blocks=97817, items_per_block=205), "k16r": dict(n_blocks=82754, items_per_block=205,
                                                                            kind="random"),
               "k64c": dict(n_blocks=24552, items_per_block=820), "k64r": dict(n_blocks=20682, items_per_block=820,
-                                                                           kind="random")}
+                                                                           kind="random"),
+              # the large-block legs (bench_large_blocks: the writer's 1 / 4 MiB data blocks, the workspace pool)
+              "l1m": dict(n_blocks=240, items_per_block=13108, seed=0x5EED0007),
+              "l4m": dict(n_blocks=60, items_per_block=52429, seed=0x5EED0007)}
     for name in which.split(","):
         off32 = name.endswith("_32")  # the same shape through lsm_encode_blocks32 (u32 offsets)
         base = name[:-3] if off32 else name
