@@ -432,10 +432,11 @@ __device__ __forceinline__ ItemMeta cook_item(const R& r, bool& bad) {
   return m;
 }
 
+template <int kOW = 0>
 __device__ __forceinline__ ItemMeta load_item(const EncodeParams& P, uint64_t i, bool& bad) {
   ItemMeta m;
-  m.ko = koff(P, i);  // (global loads, not flat ones)
-  const uint64_t kl = koff(P, i + 1) - m.ko;
+  m.ko = koff<kOW>(P, i);  // (global loads, not flat ones)
+  const uint64_t kl = koff<kOW>(P, i + 1) - m.ko;
   if (kl > 0xFFFF) bad = true;
   m.klen = (uint32_t)min(kl, (uint64_t)0xFFFF);
   m.seq = gload(P.it.seqno, i);
@@ -446,8 +447,8 @@ __device__ __forceinline__ ItemMeta load_item(const EncodeParams& P, uint64_t i,
     m.vl = gload(P.it.handle_size, i);
     m.vt = 0;
   } else {
-    m.vo = voff(P, i);
-    const uint64_t vl = voff(P, i + 1) - m.vo;
+    m.vo = voff<kOW>(P, i);
+    const uint64_t vl = voff<kOW>(P, i + 1) - m.vo;
     m.vt = gload(P.it.vtype, i);
     if (!valid_vtype(m.vt)) bad = true;
     if (!is_tombstone(m.vt) && vl > 0xFFFFFFFFULL) bad = true;
@@ -458,14 +459,15 @@ __device__ __forceinline__ ItemMeta load_item(const EncodeParams& P, uint64_t i,
 
 // Item j of the block starting at item s, with its shared prefix against the
 // restart head (encoder.rs:140-143, util.rs:125-130).
+template <int kOW = 0>
 __device__ __forceinline__ ItemMeta load_item_lcp(const EncodeParams& P, uint32_t s, uint32_t j, uint32_t ri,
                                                   bool& bad) {
   const uint64_t i = (uint64_t)s + j;
-  ItemMeta m = load_item(P, i, bad);
+  ItemMeta m = load_item<kOW>(P, i, bad);
   if (!is_index(P) && j % ri != 0) {
     const uint64_t h = (uint64_t)s + (j / ri) * ri;
-    const uint64_t hko = koff(P, h);
-    const uint32_t hkl = (uint32_t)min(koff(P, h + 1) - hko, (uint64_t)0xFFFF);
+    const uint64_t hko = koff<kOW>(P, h);
+    const uint32_t hkl = (uint32_t)min(koff<kOW>(P, h + 1) - hko, (uint64_t)0xFFFF);
     m.sh = lcp_global(P.it.keys, hko, m.ko, min(hkl, m.klen));
   }
   return m;
@@ -666,6 +668,7 @@ __device__ __forceinline__ void finish_block_lds(const EncodeParams& P, uint32_t
 // Listed block b (any item count) assembled by one wave in the LDS image at
 // `smem` (16-B aligned, at least e2_need bytes); shared prefixes and the plan
 // come from the fused pass.
+template <int kOW>
 __device__ __forceinline__ void write_block_lds(const EncodeParams& P, uint32_t b, uint8_t* smem) {
   const int lane = threadIdx.x & 63;
   const uint32_t s = P.starts[b], e = P.starts[b + 1];
@@ -700,7 +703,7 @@ __device__ __forceinline__ void write_block_lds(const EncodeParams& P, uint32_t 
     uint32_t rec = 0;
     if (j < n) {
       bool bad = false;
-      m = load_item_lcp(P, s, j, ri, bad);
+      m = load_item_lcp<kOW>(P, s, j, ri, bad);
       rec = (uint32_t)item_record_len(P, m, head);
     }
     const uint32_t incl = wave_incl_scan_u32(rec);
@@ -726,7 +729,7 @@ __device__ __forceinline__ void write_block_lds(const EncodeParams& P, uint32_t 
 // payload xxh3_128 (per-KiB contributions on every wave into `contrib`, the
 // scramble chain and the merge on wave 0), the header and the copy-out.  One
 // wave per 20-96 KiB block ran the 64 KiB classes at 0.18 TB/s.
-template <uint32_t kLW>
+template <uint32_t kLW, int kOW>
 __device__ __forceinline__ void write_block_lds_mw(const EncodeParams& P, uint32_t b, uint8_t* smem, uint32_t* psum,
                                                    uint64_t* contrib) {
   constexpr uint32_t kT = kLW * kWave;
@@ -764,7 +767,7 @@ __device__ __forceinline__ void write_block_lds_mw(const EncodeParams& P, uint32
     uint32_t rec = 0;
     if (j < n) {
       bool bad = false;
-      m = load_item_lcp(P, s, j, ri, bad);
+      m = load_item_lcp<kOW>(P, s, j, ri, bad);
       rec = (uint32_t)item_record_len(P, m, head);
     }
     const uint32_t incl = wave_incl_scan_u32(rec);
@@ -1636,6 +1639,7 @@ __device__ __forceinline__ E1pItems<K> e1p_items(const EncodeParams& P) {
 // The huge-block pool header's collected-block count (EncHugeHdr::count), as a u32 index.
 constexpr uint32_t kEncHugeCountWord = 2;
 
+template <int kOW>
 __global__ __launch_bounds__(256) void encode_e1p_lengths_kernel(EncodeParams P) {
   if (blockIdx.x == 0) {  // the starts' monotonicity over every block, the flag written whole (no prior clear)
     int bad = 0;
@@ -1650,7 +1654,7 @@ __global__ __launch_bounds__(256) void encode_e1p_lengths_kernel(EncodeParams P)
   const E1pItems<kE1pLenPer> T = e1p_items<kE1pLenPer>(P);
   const uint32_t ri = P.ri, lane = threadIdx.x & 63;
   bool live[kE1pLenPer], head[kE1pLenPer];
-  RawItem r[kE1pLenPer];
+  RawItemT<kOW> r[kE1pLenPer];
   uint64_t hko[kE1pLenPer], hko1[kE1pLenPer];
 #pragma unroll
   for (uint32_t j = 0; j < kE1pLenPer; ++j) {  // every item's loads first
@@ -1659,11 +1663,11 @@ __global__ __launch_bounds__(256) void encode_e1p_lengths_kernel(EncodeParams P)
     head[j] = (i - T.s[j]) % ri == 0;
     hko[j] = hko1[j] = 0;
     if (live[j]) {
-      r[j] = load_raw<false>(P, i);
+      r[j] = load_raw<false, kOW>(P, i);
       if (!head[j]) {
         const uint64_t h = (uint64_t)i - (i - T.s[j]) % ri;
-        hko[j] = koff(P, h);
-        hko1[j] = koff(P, h + 1);
+        hko[j] = koff<kOW>(P, h);
+        hko1[j] = koff<kOW>(P, h + 1);
       }
     }
   }
@@ -2297,17 +2301,18 @@ __global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(4))) 
 }
 
 // Listed medium / big blocks: one wave per workgroup, grid-stride over the list.
+template <int kOW>
 __global__ __launch_bounds__(kWave) void encode_write_list_kernel(EncodeParams P, uint32_t plan_flag) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   const uint32_t count = P.list_count[0];
   for (uint32_t li = blockIdx.x; li < count; li += gridDim.x) {
     const uint32_t b = P.lists[li];
-    if ((P.plans[b].step_flags >> 8) == plan_flag) write_block_lds(P, b, smem);
+    if ((P.plans[b].step_flags >> 8) == plan_flag) write_block_lds<kOW>(P, b, smem);
   }
 }
 
 // Listed medium / big blocks, kLW waves per block (write_block_lds_mw).
-template <uint32_t kLW>
+template <uint32_t kLW, int kOW>
 __global__ __launch_bounds__(kLW * kWave) void encode_write_list_mw_kernel(EncodeParams P, uint32_t plan_flag) {
   extern __shared__ __attribute__((aligned(16))) uint8_t smem[];
   __shared__ uint32_t psum[kLW];
@@ -2315,7 +2320,7 @@ __global__ __launch_bounds__(kLW * kWave) void encode_write_list_mw_kernel(Encod
   const uint32_t count = P.list_count[0];
   for (uint32_t li = blockIdx.x; li < count; li += gridDim.x) {
     const uint32_t b = P.lists[li];
-    if ((P.plans[b].step_flags >> 8) == plan_flag) write_block_lds_mw<kLW>(P, b, smem, psum, contrib);
+    if ((P.plans[b].step_flags >> 8) == plan_flag) write_block_lds_mw<kLW, kOW>(P, b, smem, psum, contrib);
   }
 }
 
@@ -2332,6 +2337,7 @@ __global__ __launch_bounds__(kLW * kWave) void encode_write_list_mw_kernel(Encod
 //            blocks into LDS contributions, then wave 0 carries the scramble
 //            chain (as decode_chunked), the tail merge and the header.
 constexpr uint32_t kE3Waves = 8, kE3Threads = kE3Waves * kWave;
+template <int kOW>
 __global__ __launch_bounds__(kE3Threads) void encode_large_kernel(EncodeParams P) {
   __shared__ uint32_t hlo[kE3HashChunk], hhi[kE3HashChunk];
   __shared__ uint64_t contrib[8 * 64];
@@ -2366,7 +2372,7 @@ __global__ __launch_bounds__(kE3Threads) void encode_large_kernel(EncodeParams P
       uint32_t roff = 0;
       if (j < n) {
         bool bad = false;
-        m = load_item_lcp(P, s, j, ri, bad);
+        m = load_item_lcp<kOW>(P, s, j, ri, bad);
         if (!scan) roff = P.erec[s + j] - pf;  // (after E1p: the record prefix, see encode_e1p_offsets_kernel)
       }
       if (scan) {  // n <= kGItems <= kE3Threads: one pass
@@ -2395,8 +2401,8 @@ __global__ __launch_bounds__(kE3Threads) void encode_large_kernel(EncodeParams P
       __syncthreads();
       for (uint32_t j = tid; j < n; j += kE3Threads) {
         const uint64_t i = (uint64_t)s + j;
-        const uint64_t ko = koff(P, i);
-        const uint32_t bk = key_bucket(P, ko, (uint32_t)(koff(P, i + 1) - ko), pl.hash_w);
+        const uint64_t ko = koff<kOW>(P, i);
+        const uint32_t bk = key_bucket(P, ko, (uint32_t)(koff<kOW>(P, i + 1) - ko), pl.hash_w);
         if (bk >= base && bk < base + lim) {
           atomicMin(&hlo[bk - base], j / ri);
           atomicMax(&hhi[bk - base], j / ri);
@@ -2593,6 +2599,7 @@ __global__ __launch_bounds__(1024) void encode_huge_plan_kernel(EncodeParams P) 
 }
 
 // Record units (u < nru of a block) and the tail unit (u == nru).
+template <int kOW>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void encode_huge_records_kernel(EncodeParams P) {
   __shared__ __attribute__((aligned(16))) uint32_t lbuf[2 * kE3HashChunk];  // record image | vote arrays
   uint32_t* hlo = lbuf;
@@ -2640,7 +2647,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
         const bool head = j % ri == 0;
         ItemMeta m;
         bool bad = false;
-        if (j < h.n) m = load_item_lcp(P, h.s, j, ri, bad);
+        if (j < h.n) m = load_item_lcp<kOW>(P, h.s, j, ri, bad);
         const uint32_t rec = j < h.n ? (uint32_t)item_record_len(P, m, head) : 0u;
         const uint32_t incl = wave_incl_scan_u32(rec);
         if (lane == kWave - 1) psum[wave] = incl;
@@ -2671,7 +2678,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
             const bool head = j % ri == 0;
             bool bad = false;
             // (after E1p the shared prefix is in hbucket: no key reads before the copy)
-            ItemMeta m = P.hb_sh ? load_item(P, (uint64_t)h.s + j, bad) : load_item_lcp(P, h.s, j, ri, bad);
+            ItemMeta m = P.hb_sh ? load_item<kOW>(P, (uint64_t)h.s + j, bad) : load_item_lcp<kOW>(P, h.s, j, ri, bad);
             if (P.hb_sh && !head) m.sh = gload(P.hbucket, (uint64_t)h.s + j);
             const uint32_t roff = gload(P.erec, (uint64_t)h.s + j) - pf;
             RecordCopy rc;
@@ -2727,8 +2734,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
       __syncthreads();
       for (uint32_t j = tid; j < h.n; j += 256) {
         const uint64_t it = (uint64_t)h.s + j;
-        const uint64_t ko = koff(P, it);
-        const uint32_t bk = key_bucket(P, ko, (uint32_t)(koff(P, it + 1) - ko), pl.hash_w);
+        const uint64_t ko = koff<kOW>(P, it);
+        const uint32_t bk = key_bucket(P, ko, (uint32_t)(koff<kOW>(P, it + 1) - ko), pl.hash_w);
         if (bk >= base && bk < base + lim) {
           atomicMin(&hlo[bk - base], j / ri);
           atomicMax(&hhi[bk - base], j / ri);
@@ -3032,7 +3039,8 @@ hipError_t launch_encode(const lsm_items& items, const uint32_t* starts, uint32_
     P.hb_sh = 1;
     const dim3 igrid((uint32_t)((items.n_items + 256 * kE1pPer - 1) / (256 * kE1pPer)));
     const dim3 lgrid((uint32_t)((items.n_items + 256 * kE1pLenPer - 1) / (256 * kE1pLenPer)));
-    hipLaunchKernelGGL(encode_e1p_lengths_kernel, lgrid, dim3(256), 0, st, P);
+    if (P.off32) hipLaunchKernelGGL(encode_e1p_lengths_kernel<4>, lgrid, dim3(256), 0, st, P);
+    else hipLaunchKernelGGL(encode_e1p_lengths_kernel<8>, lgrid, dim3(256), 0, st, P);
     if ((e = launch_excl_scan(P.erec, items.n_items, tiles, E1pOut{P.erec, P.pfirst + n_blocks, items.n_items},
                               st)) != hipSuccess)
       return e;
@@ -3065,14 +3073,17 @@ hipError_t launch_encode(const lsm_items& items, const uint32_t* starts, uint32_
     hipLaunchKernelGGL(encode_offsets_apply_kernel, dim3((uint32_t)scan_tiles(n_blocks)), dim3(kScanThreads), 0, st,
                        offs, oo);
   }
-  static uint64_t attr_done = 0;
-  if ((e = set_lds_attr((const void*)encode_write_list_kernel, kImgBig, &attr_done)) != hipSuccess) return e;
-  static uint64_t attr_mw = 0;
-  if ((e = set_lds_attr((const void*)encode_write_list_mw_kernel<kListBigWaves>, kImgBig, &attr_mw)) != hipSuccess)
-    return e;
+  // (the cold kernels too are instantiated per offset width: a run-time width branch per
+  // item load cost the 1 / 4 MiB encodes 5-6 %, profiles/r06_experiments.txt)
+  const bool w4 = P.off32 != 0;
+  const void* list_k = w4 ? (const void*)encode_write_list_kernel<4> : (const void*)encode_write_list_kernel<8>;
+  const void* list_mw_k = w4 ? (const void*)encode_write_list_mw_kernel<kListBigWaves, 4>
+                             : (const void*)encode_write_list_mw_kernel<kListBigWaves, 8>;
+  static uint64_t attr_done[2] = {0, 0}, attr_mw[2] = {0, 0};
+  if ((e = set_lds_attr(list_k, kImgBig, &attr_done[w4])) != hipSuccess) return e;
+  if ((e = set_lds_attr(list_mw_k, kImgBig, &attr_mw[w4])) != hipSuccess) return e;
   const dim3 ggrid((n_blocks + kGRun - 1) / kGRun), gblock(kGThreads);
   // (kernels instantiated per offset width: straight-line item loads)
-  const bool w4 = P.off32 != 0;
   if (P.type == 1)
     hipLaunchKernelGGL(w4 ? (encode_group_kernel<true, false, false, 4>) : (encode_group_kernel<true, false, false, 8>),
                        ggrid, gblock, 0, st, P);
@@ -3087,9 +3098,15 @@ hipError_t launch_encode(const lsm_items& items, const uint32_t* starts, uint32_
                        ggrid, gblock, 0, st, P);
   // medium blocks (<= 20 KiB images): one wave each, eight workgroups per CU, was
   // faster than four waves each (2.26 vs 2.40 ms for the 16 KiB random-key class)
-  hipLaunchKernelGGL(encode_write_list_kernel, dim3(2048), dim3(kWave), kImgMedium, st, P, kPlanMedium);
-  hipLaunchKernelGGL(encode_write_list_mw_kernel<kListBigWaves>, dim3(512), dim3(kListBigWaves * kWave), kImgBig, st,
-                     P, kPlanBig);
+  if (w4) {
+    hipLaunchKernelGGL(encode_write_list_kernel<4>, dim3(2048), dim3(kWave), kImgMedium, st, P, kPlanMedium);
+    hipLaunchKernelGGL((encode_write_list_mw_kernel<kListBigWaves, 4>), dim3(512), dim3(kListBigWaves * kWave),
+                       kImgBig, st, P, kPlanBig);
+  } else {
+    hipLaunchKernelGGL(encode_write_list_kernel<8>, dim3(2048), dim3(kWave), kImgMedium, st, P, kPlanMedium);
+    hipLaunchKernelGGL((encode_write_list_mw_kernel<kListBigWaves, 8>), dim3(512), dim3(kListBigWaves * kWave),
+                       kImgBig, st, P, kPlanBig);
+  }
   if (P.huge_pool) {  // huge blocks across the GPU (the ones it does not take stay flagged for E3 below)
     hipLaunchKernelGGL(encode_huge_plan_kernel, dim3(1), dim3(1024), 0, st, P);
     // one resident wave of record workgroups (no partly filled last wave: 256 KiB encode
@@ -3102,10 +3119,13 @@ hipError_t launch_encode(const lsm_items& items, const uint32_t* starts, uint32_
       if ((e = hipDeviceGetAttribute(&n_cu, hipDeviceAttributeMultiprocessorCount, dev)) != hipSuccess) return e;
       if (dev < 64) __atomic_store_n(&cu_count[dev], n_cu, __ATOMIC_RELAXED);
     }
-    hipLaunchKernelGGL(encode_huge_records_kernel, dim3(kEHugeWgsPerCU * (uint32_t)n_cu), dim3(256), 0, st, P);
+    const dim3 rgrid(kEHugeWgsPerCU * (uint32_t)n_cu);
+    if (w4) hipLaunchKernelGGL(encode_huge_records_kernel<4>, rgrid, dim3(256), 0, st, P);
+    else hipLaunchKernelGGL(encode_huge_records_kernel<8>, rgrid, dim3(256), 0, st, P);
     hipLaunchKernelGGL(encode_huge_chain_kernel, dim3(min(n_blocks, 1024u)), dim3(256), 0, st, P);
   }
-  hipLaunchKernelGGL(encode_large_kernel, dim3(512), dim3(kE3Threads), 0, st, P);
+  if (w4) hipLaunchKernelGGL(encode_large_kernel<4>, dim3(512), dim3(kE3Threads), 0, st, P);
+  else hipLaunchKernelGGL(encode_large_kernel<8>, dim3(512), dim3(kE3Threads), 0, st, P);
   return hipGetLastError();
 }
 

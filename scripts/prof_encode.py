@@ -19,6 +19,8 @@ def main():
     ap.add_argument("--blocks", type=int, default=1 << 20)
     ap.add_argument("--reps", type=int, default=5)
     ap.add_argument("--workload", default="counter", choices=["counter", "prefix16k"])
+    ap.add_argument("--off64", action="store_true", help="u64 key / value offsets (lsm_encode_blocks); default: "
+                    "u32 (lsm_encode_blocks32), as bench.py's timed step")
     ap.add_argument("--diag-bits", type=int, default=0, help="lsm_block_params.reserved for the timed loop (diagnostic build)")
     ap.add_argument("--phases", action="store_true", help="per-phase cycles of the group kernel (diagnostic build)")
     ap.add_argument("--ablate", action="store_true", help="diagnostic ablations (lsm_block_params.reserved bits)")
@@ -29,10 +31,13 @@ def main():
         items, starts, n_items = bench.make_workload(torch, lsmgpu, nb)
     else:
         items, starts, n_items = bench.make_workload(torch, lsmgpu, nb, items_per_block=56, key_len=40, val_len=256)
+    off_bytes = 8 if args.off64 else 4
+    if not args.off64:
+        items = dict(items, key_off=items["key_off"].to(torch.int32), val_off=items["val_off"].to(torch.int32))
     if args.diag_bits:
         lsmgpu.lib()
         orig_p = lsmgpu.LsmBlockParams
-        lsmgpu.LsmBlockParams = lambda ri, bt, c, r, hr: orig_p(ri, bt, c, args.diag_bits, hr)
+        lsmgpu.LsmBlockParams = lambda ri, bt, c, r, hr, *f: orig_p(ri, bt, c, args.diag_bits, hr, *f)
     enc_ctx = lsmgpu.Encoder()
     enc = enc_ctx.encode(items, starts, nb)
     torch.cuda.synchronize()
@@ -49,7 +54,7 @@ def main():
         import ctypes as C
         L = lsmgpu.lib()
         orig = lsmgpu.LsmBlockParams
-        lsmgpu.LsmBlockParams = lambda ri, bt, c, r, hr: orig(ri, bt, c, 0x80, hr)
+        lsmgpu.LsmBlockParams = lambda ri, bt, c, r, hr, *f: orig(ri, bt, c, 0x80, hr, *f)
         buf = (C.c_uint64 * 16)()
         rc0 = L.lsm_diag_encode_phases(buf)
         enc_ctx.encode(items, starts, nb, out=enc)
@@ -73,8 +78,8 @@ def main():
             orig = lsmgpu.LsmBlockParams
             class P2(C.Structure):  # noqa: E306
                 _fields_ = orig._fields_
-            def mk(ri, bt, c, r, hr, bits=bits):
-                return orig(ri, bt, c, bits, hr)
+            def mk(ri, bt, c, r, hr, *f, bits=bits):
+                return orig(ri, bt, c, bits, hr, *f)
             lsmgpu.LsmBlockParams = mk
             enc_ctx.encode(items, starts, nb, out=enc)
             torch.cuda.synchronize()
@@ -86,8 +91,8 @@ def main():
             lsmgpu.LsmBlockParams = orig
             print(f"  ablate {name:20s} {e0.elapsed_time(e1) / args.reps:.3f} ms", flush=True)
     key_val = int(items["key_off"][n_items].item()) + int(items["val_off"][n_items].item())
-    alg = key_val + n_items * bench.ENC_IN_PER_ITEM + 4 * (nb + 1) + total + 8 * (nb + 1) + 4 * nb
-    print(f"encode {args.workload}: {nb} blocks {n_items} items {total} bytes  {ms:.3f} ms  "
+    alg = key_val + n_items * (bench.ENC_IN_PER_ITEM - 2 * (8 - off_bytes)) + 4 * (nb + 1) + total + 8 * (nb + 1) + 4 * nb
+    print(f"encode {args.workload} (u{8 * off_bytes} offsets): {nb} blocks {n_items} items {total} bytes  {ms:.3f} ms  "
           f"{total / ms / 1e6:.1f} GB/s written  alg_bytes {alg}", flush=True)
 
 

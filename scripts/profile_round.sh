@@ -24,9 +24,9 @@ BYTES=$(echo "$line" | sed 's/.* bytes \([0-9]*\) items.*/\1/')
 ITEMS=$(echo "$line" | sed 's/.* items \([0-9]*\).*/\1/')
 EALG=$(grep "alg_bytes" $OUT/efetch.log | sed 's/.*alg_bytes \([0-9]*\).*/\1/')
 EITEMS=$(grep "alg_bytes" $OUT/efetch.log | sed 's/.*blocks \([0-9]*\) items.*/\1/')
-# (the counter workload: 16 B keys, 64 B values)
+# (the counter workload: 16 B keys, 64 B values; u32 offsets, as bench.py's timed encode)
 python3 scripts/traffic_summary.py $OUT/fetch $OUT/write $NB $BYTES $ITEMS $OUT/efetch $OUT/ewrite $EALG \
-  $EITEMS $((16 * EITEMS)) $((64 * EITEMS)) > $OUT/traffic.json
+  $EITEMS $((16 * EITEMS)) $((64 * EITEMS)) 4 > $OUT/traffic.json
 cat $OUT/traffic.json
 find $OUT/kt -name "*kernel_stats.csv" -exec cp {} $OUT/kernel_stats.csv \;
 python3 scripts/trace_by_grid.py $(find $OUT/kt -name "*kernel_trace.csv" | head -1) > $OUT/kernels_by_grid.csv

@@ -10,7 +10,9 @@ LDS-DMA all report exactly half).  WRITE_SIZE is exact for 16-B stores, u32
 stores (r05_fetch_calib.json) and the decode SoA's 1-8 B stores
 (scripts/write_calib.py, round 2).
 Usage: traffic_summary.py DEC_FETCH DEC_WRITE DEC_BLOCKS DEC_BYTES DEC_ITEMS
-                          ENC_FETCH ENC_WRITE ENC_ALG_BYTES ITEMS KEY_BYTES VAL_BYTES > profiles/traffic_rNN.json
+                          ENC_FETCH ENC_WRITE ENC_ALG_BYTES ITEMS KEY_BYTES VAL_BYTES [OFF_BYTES]
+                          > profiles/traffic_rNN.json
+(OFF_BYTES: the width of the encode's key / value offsets, 8 or 4 (lsm_encode_blocks32); default 8)
 """
 import csv
 import json
@@ -67,14 +69,15 @@ def main():
                                          "plan + scan + group kernels summed per launch; FETCH_SIZE x2 and WRITE_SIZE "
                                          "raw, both calibrated (profiles/r05_fetch_calib.json)")
         # per kernel: what each pass of the two-pass design must move (bytes per launch):
-        #   plan  reads the item SoA (8 + 8 + 8 + 1 B) and each key's first 16 bytes,
+        #   plan  reads the item SoA (8 + 8 + 8 + 1 B; 4 + 4 + 8 + 1 with u32 offsets) and each key's first 16 bytes,
         #         writes erec (4 B per item) and per block size, plan, key / value span starts (40 B)
         #   group reads keys, values, the item SoA again, erec, the block plans (40 B) and offsets,
         #         writes the blocks and their statuses
         items, key_bytes, val_bytes = int(a[8]), int(a[9]), int(a[10])
-        out_bytes = int(a[7]) - (key_bytes + val_bytes + items * 25 + 16 * dblocks + 4)
-        plan_alg = items * (25 + 16 + 4) + dblocks * 40
-        group_alg = key_bytes + val_bytes + items * (25 + 4) + dblocks * 48 + out_bytes
+        soa = 25 - 2 * (8 - (int(a[11]) if len(a) > 11 else 8))  # item SoA bytes per item
+        out_bytes = int(a[7]) - (key_bytes + val_bytes + items * soa + 16 * dblocks + 4)
+        plan_alg = items * (soa + 16 + 4) + dblocks * 40
+        group_alg = key_bytes + val_bytes + items * (soa + 4) + dblocks * 48 + out_bytes
         for k, alg in (("encode_plan_wave_kernel", plan_alg), ("encode_group_kernel", group_alg)):
             f1, n1 = per_dispatch(a[5], "FETCH_SIZE", [k], True)
             w1, _ = per_dispatch(a[6], "WRITE_SIZE", [k], True)
