@@ -1400,7 +1400,7 @@ def main():
     r_enc = encode_roofline("lsm_encode_blocks32 (encode_plan_wave_kernel + scan + encode_group_kernel)", enc_ms,
                             key_val, n_items, nb, total_bytes, ceil, off_bytes=4, trace_kernels=
                             [("encode_plan_wave_kernel<false, 4>", (nb + 127) // 128),
-                             ("encode_group_kernel<false, false, false, 4>", (nb + 31) // 32)] if nb == 1 << 20 else None)
+                             ("encode_group_kernel<false, false, false, 4, false>", (nb + 31) // 32)] if nb == 1 << 20 else None)
     dominant = r_enc if enc_ms >= kdec_ms else r_dec
 
     extra = {}

@@ -164,13 +164,23 @@ typedef struct lsm_block_params {
     uint8_t compression;      /* 0 = CompressionType::None (the only supported value) */
     uint8_t reserved;         /* must be 0 (else LSM_BAD_ARG) */
     float hash_ratio;         /* data_block_hash_ratio (default 0.0) */
-    uint32_t flags;           /* LSM_ENCODE_HUGE_POOL or 0; any other bit is LSM_BAD_ARG */
+    uint32_t flags;           /* LSM_ENCODE_HUGE_POOL | LSM_ENCODE_RUN_PLAN or 0; any other bit is LSM_BAD_ARG */
 } lsm_block_params;
 /* Take the workspace pool of lsm_encode_workspace_size_ex: blocks whose image
  * exceeds 96 KiB are written and hashed by work units across the whole GPU.
  * Without this flag the pool is never used, whatever the workspace size; with
  * it, a workspace too small for the pool's fixed part encodes without it. */
 #define LSM_ENCODE_HUGE_POOL 1u
+/* Plan each 32-block run inside the write kernel (block offsets by a decoupled
+ * look-back across runs) instead of a plan pass and a size scan before it.  Taken
+ * for data blocks without a hash index and without the pool, 1-512 items per
+ * block on average; the library also takes it by itself at >= 128 items per block
+ * (16 KiB blocks of short records: faster there, slower for 4 KiB blocks).  Same
+ * bytes and statuses either way, except: a run whose predecessors' offsets do not
+ * arrive within 100 ms (never seen) reports LSM_INCOMPLETE for its blocks and every
+ * later run's, and an item_start array that is not strictly increasing rejects the
+ * blocks of the 32-block run that holds the fault. */
+#define LSM_ENCODE_RUN_PLAN 2u
 
 /* Tuning knobs for the decode kernel (0 = library default).  Any flag bit
  * other than LSM_DECODE_ITEM_START_VALID / LSM_DECODE_PAYLOAD_VERIFIED /

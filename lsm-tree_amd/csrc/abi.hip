@@ -160,7 +160,7 @@ static int encode_blocks_common(const lsm_items* d_items, bool off32, const uint
   if (!d_items || !params || !d_block_item_start || !d_out || !d_block_off || !d_status) return LSM_BAD_ARG;
   if (params->compression != 0) return LSM_UNSUPPORTED;
   if (params->reserved != 0 && !lsmgpu::kDiagBuild) return LSM_BAD_ARG;
-  if (params->flags & ~LSM_ENCODE_HUGE_POOL) return LSM_BAD_ARG;
+  if (params->flags & ~(LSM_ENCODE_HUGE_POOL | LSM_ENCODE_RUN_PLAN)) return LSM_BAD_ARG;
   if (params->block_type != LSM_BLOCK_DATA && params->block_type != LSM_BLOCK_INDEX &&
       params->block_type != LSM_BLOCK_META)
     return LSM_BAD_ARG;

@@ -26,6 +26,7 @@
 #include <math.h>
 
 #include <algorithm>
+#include <cstddef>
 #include <type_traits>
 
 #include "block_format.hpp"
@@ -846,6 +847,15 @@ constexpr uint32_t kErecHead = 0x8000u;
 // Group write kernel (E2) budget, see encode_group_kernel.
 constexpr uint32_t kGWaves = 4, kGThreads = kGWaves * kWave;
 constexpr uint32_t kGRun = 32;          // blocks per workgroup (<= 63: one lane each)
+#ifndef LSM_EXP_GRUNF
+#define LSM_EXP_GRUNF 32
+#endif
+constexpr uint32_t kGRunFused = LSM_EXP_GRUNF;  // the same with the fused run-level plan
+#ifndef LSM_EXP_FUSED_AUTO
+#define LSM_EXP_FUSED_AUTO 128
+#endif
+constexpr uint64_t kFusedAutoItems = LSM_EXP_FUSED_AUTO;  // items per block from which the fused plan is taken
+static_assert(kGRunFused <= 63, "one lane per block and one for the run's end");
 constexpr uint32_t kGBlocks = 16;    // blocks per group
 constexpr uint32_t kGItems = kGThreads;        // items per group (one thread each)
 constexpr uint32_t kGSlack = 48;               // readable bytes past each staged span
@@ -1135,20 +1145,36 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(1))) void e
 // step's key windows are in flight.
 constexpr uint32_t kPW = 2;  // consecutive items per lane
 constexpr uint32_t kPWStep = kPW * kWave;
-template <bool kBkt, int kOW>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void encode_plan_wave_kernel(EncodeParams P) {
-  __shared__ uint32_t bst[kPlanBlocks + 1];
-  __shared__ unsigned long long bfirst[kPlanBlocks], bend[kPlanBlocks], lhead[kPlanBlocks];
-  __shared__ unsigned long long kos[4][kPWStep];
-  __shared__ uint32_t kls[4][kPWStep];
-  __shared__ Win16 kwin[4][kPWStep];  // each item's first 16 key bytes
-  __shared__ uint32_t badf[kPlanBlocks];
-  __shared__ uint32_t wcut[5];
-  __shared__ uint32_t mono;
+struct PlanWaveLds {
+  uint32_t bst[kPlanBlocks + 1];
+  uint32_t badf[kPlanBlocks];
+  uint32_t wcut[5];
+  uint32_t mono;
+  unsigned long long bfirst[kPlanBlocks], bend[kPlanBlocks], lhead[kPlanBlocks];
+  unsigned long long kos[4][kPWStep];
+  uint32_t kls[4][kPWStep];
+  Win16 kwin[4][kPWStep];  // each item's first 16 key bytes
+};
+
+// The plan of blocks [b0, b0 + nb) on one 256-thread workgroup (all threads call it).
+// kFused (encode_group_kernel's run-level plan): each block's plan and size also go to
+// fplan / fsize in LDS (thread j = block b0 + j), and P.sizes is not written (the fused
+// kernel keeps its look-back words there).
+template <bool kBkt, int kOW, bool kFused>
+__device__ __forceinline__ void plan_wave_run(const EncodeParams& P, uint32_t b0, uint32_t nb, PlanWaveLds& S,
+                                              BlockPlan* fplan, uint64_t* fsize) {
+  uint32_t* const bst = S.bst;
+  unsigned long long* const bfirst = S.bfirst;
+  unsigned long long* const bend = S.bend;
+  unsigned long long* const lhead = S.lhead;
+  auto& kos = S.kos;
+  auto& kls = S.kls;
+  auto& kwin = S.kwin;
+  uint32_t* const badf = S.badf;
+  uint32_t* const wcut = S.wcut;
+  uint32_t& mono = S.mono;
   const uint32_t tid = threadIdx.x, lane = tid & (kWave - 1);
   const uint32_t wave = __builtin_amdgcn_readfirstlane(tid / kWave);
-  const uint32_t b0 = blockIdx.x * P.plan_bpw;
-  const uint32_t nb = min(P.plan_bpw, P.n_blocks - b0);
   if (tid <= nb) bst[tid] = clamped_start(P, b0 + tid);
   if (tid < nb) {
     bfirst[tid] = bend[tid] = lhead[tid] = 0;
@@ -1368,8 +1394,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
   const uint32_t hash_w = (buckets > 0 && bin_len <= kHashMaxPointers) ? buckets : 0;
   const uint64_t total = kHdrLen + recs + 1 + (uint64_t)bin_len * step + hash_w + kTrailerLen;
   if (recs > 0xFFFFFFF0ULL || total > 0xFFFFFF00ULL) bad = true;
-  const uint64_t ks = koff(P, s), ke = koff(P, e);
-  const uint64_t vs = voff(P, s), ve = voff(P, e);
+  const uint64_t ks = koff<kOW>(P, s), ke = koff<kOW>(P, e);
+  const uint64_t vs = voff<kOW>(P, s), ve = voff<kOW>(P, e);
   uint32_t flags = 0;
   if (bad) {
     flags = kPlanBad;
@@ -1378,14 +1404,31 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
     const uint64_t need = e2_need(total, hash_w);
     flags = need <= kImgMedium ? kPlanMedium : need <= kImgBig ? kPlanBig : kPlanHuge;
   }
-  P.plans[b] = BlockPlan{(uint32_t)recs, bin_len, hash_w, step | (flags << 8)};
-  P.sizes[b] = (bad ? 0 : total) | ((flags & (kPlanMedium | kPlanBig | kPlanHuge)) ? kListedOne : 0);
+  const BlockPlan pl{(uint32_t)recs, bin_len, hash_w, step | (flags << 8)};
+  const uint64_t size = (bad ? 0 : total) | ((flags & (kPlanMedium | kPlanBig | kPlanHuge)) ? kListedOne : 0);
+  P.plans[b] = pl;
+  if (kFused) {
+    fplan[tid] = pl;
+    fsize[tid] = size;
+    // (a listed block's status until its list kernel writes it: stays if the run's
+    // output offset never arrives, see run_lookback)
+    if (size & ~kOffMask) P.status[b] = ST_INCOMPLETE;
+  } else {
+    P.sizes[b] = size;
+  }
   P.kspan[b] = ks;
   P.vspan[b] = vs;
   if (b + 1 == P.n_blocks) {
     P.kspan[b + 1] = ke;
     P.vspan[b + 1] = ve;
   }
+}
+
+template <bool kBkt, int kOW>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void encode_plan_wave_kernel(EncodeParams P) {
+  __shared__ PlanWaveLds S;
+  const uint32_t b0 = blockIdx.x * P.plan_bpw;
+  plan_wave_run<kBkt, kOW, false>(P, b0, min(P.plan_bpw, P.n_blocks - b0), S, nullptr, nullptr);
 }
 
 // ------------------------------------------------ E2: group write kernel
@@ -1428,6 +1471,11 @@ struct GroupLds {
   GBlk blk[kGBlocks];
   LongSecret secret;
 };
+// (the fused kernel's run-level plan keeps its LDS over vals + img, and its per-block
+// outputs in uni, before the first group's DMA)
+static_assert(offsetof(GroupLds, uni) - offsetof(GroupLds, vals) >= sizeof(PlanWaveLds), "plan LDS over the stage");
+static_assert(offsetof(GroupLds, vals) % 16 == 0, "plan LDS alignment");
+static_assert(kGRunFused * (sizeof(BlockPlan) + 8) + 16 <= kGUnion, "fused plan outputs in uni");
 
 
 // n bytes src[s ..) (LDS) -> dst[d ..) (LDS): byte stores for the dst bytes
@@ -1850,16 +1898,76 @@ __global__ __launch_bounds__(256) void encode_bucket_fixup_kernel(EncodeParams P
   }
 }
 
-template <bool kIndex, bool kHash, bool kPlanBkt, int kOW>
+// ---- the fused plan's run offsets: a decoupled look-back over the runs (one word per
+// run in P.sizes, cleared before the launch): bits 62-63 the state (1: this run's own
+// bytes, 2: the inclusive prefix through this run), bit 61 poison, bits 0-60 the value
+// (output bytes in bits 0-39, listed blocks above, as P.sizes' words).  A run publishes
+// its own total as soon as its plan is done, before it looks back, and looks back only
+// at lower runs, which were dispatched before it: every wait ends.  The wait is also
+// bounded in time (100 ms without progress): a run that gives up publishes poison, and
+// its blocks and every later run's report LSM_INCOMPLETE instead of bytes at a wrong
+// offset.
+constexpr uint64_t kLbAgg = 1ULL << 62, kLbIncl = 2ULL << 62, kLbPoison = 1ULL << 61, kLbVal = kLbPoison - 1;
+constexpr uint64_t kLookbackTicks = 10000000;  // s_memrealtime runs at 100 MHz
+// diagnostic builds: lsm_block_params.reserved bit 0x20 makes every run but the first give up
+// at once (tests/test_gpu_encode_fused.py checks the poison path end to end)
+constexpr uint32_t kDiagLookbackGiveUp = 0x20;
+
+__device__ __forceinline__ uint64_t lb_load(const uint64_t* p) {
+  return __hip_atomic_load(p, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+__device__ __forceinline__ void lb_store(uint64_t* p, uint64_t v) {
+  __hip_atomic_store(p, v, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+}
+
+// One wave: publishes `agg` for `run`, returns the sum of the runs before it.
+__device__ __noinline__ uint64_t run_lookback(uint64_t* lb, uint32_t run, uint64_t agg, uint32_t diag, bool& poisoned) {
+  const int lane = threadIdx.x & (kWave - 1);
+  if (lane == 0) lb_store(lb + run, (run == 0 ? kLbIncl : kLbAgg) | agg);
+  uint64_t excl = 0;
+  bool poison = false;
+  if (run != 0) {
+    int64_t top = (int64_t)run - 1;  // lane l looks at run top - l
+    uint64_t t0 = __builtin_amdgcn_s_memrealtime();
+    for (;;) {
+      const int64_t idx = top - lane;
+      const uint64_t v = idx >= 0 ? lb_load(lb + idx) : kLbIncl;  // (before run 0: an inclusive 0)
+      const uint64_t incl_m = __ballot((v >> 62) == 2), ready_m = __ballot((v >> 62) != 0);
+      const uint32_t stop = incl_m ? (uint32_t)__builtin_ctzll(incl_m) : 64u;  // the nearest inclusive prefix
+      const uint64_t need = stop >= 63 ? ~0ULL : (2ULL << stop) - 1;
+      if ((ready_m & need) == need && !(kDiagBuild && (diag & kDiagLookbackGiveUp))) {
+        const bool mine = (uint32_t)lane <= stop;
+        poison = poison || __ballot(mine && (v & kLbPoison)) != 0;
+        excl += wave_bcast_u64(wave_incl_scan_u64(mine ? (v & kLbVal) : 0), kWave - 1);
+        if (stop < 64) break;
+        top -= 64;
+        t0 = __builtin_amdgcn_s_memrealtime();
+        continue;
+      }
+      if (__builtin_amdgcn_s_memrealtime() - t0 > kLookbackTicks || (kDiagBuild && (diag & kDiagLookbackGiveUp))) {
+        poison = true;
+        break;
+      }
+      __builtin_amdgcn_s_sleep(1);
+    }
+    if (lane == 0) lb_store(lb + run, kLbIncl | (poison ? kLbPoison : 0) | ((excl + agg) & kLbVal));
+  }
+  poisoned = poison;
+  return excl;
+}
+
+template <bool kIndex, bool kHash, bool kPlanBkt, int kOW, bool kFused = false>
 __global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(4))) void encode_group_kernel(EncodeParams P) {
+  static_assert(!kFused || (!kIndex && !kHash), "the fused plan is for data blocks without a hash index");
   __shared__ GroupLds L;
   typedef __attribute__((address_space(3))) void lds_void_t;
   typedef const __attribute__((address_space(1))) void gbl_void_t;
   const uint32_t tid = threadIdx.x;
   const uint32_t wave = __builtin_amdgcn_readfirstlane(tid / kWave);
   const int lane = tid & (kWave - 1);
-  const uint32_t b_begin = blockIdx.x * kGRun;
-  const uint32_t b_end = min(b_begin + kGRun, P.n_blocks);
+  constexpr uint32_t kRun = kFused ? kGRunFused : kGRun;
+  const uint32_t b_begin = blockIdx.x * kRun;
+  const uint32_t b_end = min(b_begin + kRun, P.n_blocks);
   const uint32_t ri = kIndex ? 1 : P.ri;
   constexpr bool index = kIndex;
   if (tid < sizeof(LongSecret) / 8)
@@ -1868,9 +1976,53 @@ __global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(4))) 
   const uint32_t rb = b_begin + lane;
   const bool in_run = rb <= b_end;
   const uint32_t r_start = in_run ? P.starts[rb] : 0;
-  const uint64_t r_off = in_run ? P.block_off[rb] : 0;
-  const uint64_t r_ks = in_run ? P.kspan[rb] : 0, r_vs = in_run ? P.vspan[rb] : 0;
-  const BlockPlan r_plan = (in_run && rb < b_end) ? P.plans[rb] : BlockPlan{0, 0, 0, 0};
+  uint64_t r_off, r_ks, r_vs;
+  BlockPlan r_plan;
+  bool run_ok = true;
+  if (kFused) {
+    // the plan pass's code on this run's blocks (its LDS over the stage, before the first
+    // DMA), then the run's output offset by the look-back: no plan launch, no size scan,
+    // and the item fields and keys this loop reads again are the ones the plan just read
+    BlockPlan* const fplan = reinterpret_cast<BlockPlan*>(L.uni);               // [kRun]
+    uint64_t* const fsize = reinterpret_cast<uint64_t*>(L.uni) + 2 * kRun;      // [kRun]
+    uint64_t* const fbase = fsize + kRun;                                       // prefix, poison
+    plan_wave_run<false, kOW, true>(P, b_begin, b_end - b_begin, *reinterpret_cast<PlanWaveLds*>(L.vals), fplan,
+                                    fsize);
+    __syncthreads();
+    r_plan = rb < b_end ? fplan[lane] : BlockPlan{0, 0, 0, 0};
+    const uint64_t sz = rb < b_end ? fsize[lane] : 0;
+    const uint64_t incl = wave_incl_scan_u64(sz);
+    if (wave == 0) {
+      bool poisoned;
+      const uint64_t base = run_lookback(P.sizes, blockIdx.x, wave_bcast_u64(incl, kWave - 1), P.diag, poisoned);
+      if (lane == 0) {
+        fbase[0] = base;
+        fbase[1] = poisoned ? 1 : 0;
+      }
+    }
+    __syncthreads();
+    const uint64_t ex = fbase[0] + incl - sz;
+    run_ok = fbase[1] == 0;
+    r_off = in_run ? (ex & kOffMask) : 0;
+    if (wave == 0 && rb < b_end) {
+      P.block_off[rb] = r_off;
+      if (!run_ok) P.status[rb] = ST_INCOMPLETE;
+      else if (sz & ~kOffMask) P.lists[ex >> 40] = rb;
+    }
+    if (wave == 0 && rb == b_end && b_end == P.n_blocks) {  // the last run: the total and the list length
+      P.block_off[rb] = r_off;
+      P.list_count[0] = run_ok ? (uint32_t)(ex >> 40) : 0u;
+    }
+    const uint32_t cs = in_run ? clamped_start(P, rb) : 0;
+    r_ks = in_run ? koff<kOW>(P, cs) : 0;
+    r_vs = in_run ? voff<kOW>(P, cs) : 0;
+    __syncthreads();  // (L.uni is the group loop's from here)
+  } else {
+    r_off = in_run ? P.block_off[rb] : 0;
+    r_ks = in_run ? P.kspan[rb] : 0;
+    r_vs = in_run ? P.vspan[rb] : 0;
+    r_plan = (in_run && rb < b_end) ? P.plans[rb] : BlockPlan{0, 0, 0, 0};
+  }
   const uint32_t r_hash = r_plan.hash_w;
   const uint32_t r_hpre = wave_incl_scan_u32(r_hash) - r_hash;  // exclusive prefix over the run
   // payload hash units (1 KiB, long path only) per block, exclusive prefix over the run
@@ -1969,7 +2121,7 @@ __global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(4))) 
   uint32_t ph_acc[12] = {};
   uint32_t ph_n = 0;
 #endif
-  Grp G = next_group(b_begin);
+  Grp G = run_ok ? next_group(b_begin) : Grp{b_end, 0};
   RawItemT<kOW, kIndex> raw{};
   if (G.k) {
     issue_dma(G);
@@ -3035,7 +3187,24 @@ hipError_t launch_encode(const lsm_items& items, const uint32_t* starts, uint32_
     // no clear launch; otherwise the pool header is cleared here)
     if (pool && !e1p && (e = fill_words_async(P.huge_pool, 64, 0, st)) != hipSuccess) return e;
   }
-  if (e1p) {  // batches of huge blocks: the plan item-parallel
+  // The run-level plan fused into the group kernel (decoupled look-back for the offsets):
+  // data blocks without a hash index, up to 512 items per block on average, no pool, and
+  // fewer than 2^21 blocks (the listed count's bits in a look-back word); asked for
+  // (LSM_ENCODE_RUN_PLAN) or at >= kFusedAutoItems items per block on average, where it
+  // measured faster (profiles/r06_experiments.txt, ab6h / ab6i).
+#ifdef LSM_NO_FUSED_PLAN
+  constexpr bool kFusedOk = false;
+#else
+  constexpr bool kFusedOk = true;
+#endif
+  const uint64_t avg_items = n_blocks ? items.n_items / n_blocks : 0;
+  const bool fused = kFusedOk && !e1p && P.type != 1 && !(P.ratio > 0.0f) && !P.huge_pool && P.plan_bpw >= 32 &&
+                     n_blocks > 0 && n_blocks < (1u << 21) &&
+                     ((params.flags & LSM_ENCODE_RUN_PLAN) || avg_items >= kFusedAutoItems);
+  if (fused) {  // the look-back words (P.sizes, unused by this path) start cleared
+    if ((e = fill_words_grid_async(P.sizes, 2 * ((n_blocks + kGRunFused - 1) / kGRunFused), 0, st)) != hipSuccess)
+      return e;
+  } else if (e1p) {  // batches of huge blocks: the plan item-parallel
     P.hb_sh = 1;
     const dim3 igrid((uint32_t)((items.n_items + 256 * kE1pPer - 1) / (256 * kE1pPer)));
     const dim3 lgrid((uint32_t)((items.n_items + 256 * kE1pLenPer - 1) / (256 * kE1pLenPer)));
@@ -3067,7 +3236,7 @@ hipError_t launch_encode(const lsm_items& items, const uint32_t* starts, uint32_
     oo.huge_list = reinterpret_cast<uint32_t*>(P.huge_pool + 256);
     oo.huge_cap = P.huge_cap;
   }
-  {
+  if (!fused) {
     const uint64_t* offs;
     if ((e = launch_scan_tile_offsets(P.sizes, n_blocks, tiles, st, &offs)) != hipSuccess) return e;
     hipLaunchKernelGGL(encode_offsets_apply_kernel, dim3((uint32_t)scan_tiles(n_blocks)), dim3(kScanThreads), 0, st,
@@ -3093,6 +3262,10 @@ hipError_t launch_encode(const lsm_items& items, const uint32_t* starts, uint32_
   else if (P.ratio > 0.0f)
     hipLaunchKernelGGL(w4 ? (encode_group_kernel<false, true, false, 4>) : (encode_group_kernel<false, true, false, 8>),
                        ggrid, gblock, 0, st, P);
+  else if (fused)
+    hipLaunchKernelGGL(w4 ? (encode_group_kernel<false, false, false, 4, true>)
+                          : (encode_group_kernel<false, false, false, 8, true>),
+                       dim3((n_blocks + kGRunFused - 1) / kGRunFused), gblock, 0, st, P);
   else
     hipLaunchKernelGGL(w4 ? (encode_group_kernel<false, false, false, 4>) : (encode_group_kernel<false, false, false, 8>),
                        ggrid, gblock, 0, st, P);

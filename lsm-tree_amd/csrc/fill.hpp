@@ -20,4 +20,17 @@ static inline hipError_t fill_words_async(void* p, uint32_t n_words, uint32_t v,
   return hipGetLastError();
 }
 
+// The same over many words (one thread per word): the fused encode's look-back words.
+static __global__ __launch_bounds__(256) void fill_words_grid_kernel(uint32_t* __restrict__ p, uint32_t n, uint32_t v) {
+  const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+  if (i < n) p[i] = v;
+}
+
+static inline hipError_t fill_words_grid_async(void* p, uint32_t n_words, uint32_t v, hipStream_t st) {
+  if (!n_words) return hipSuccess;
+  hipLaunchKernelGGL(fill_words_grid_kernel, dim3((n_words + 255) / 256), dim3(256), 0, st,
+                     reinterpret_cast<uint32_t*>(p), n_words, v);
+  return hipGetLastError();
+}
+
 }  // namespace lsmgpu

@@ -72,6 +72,7 @@ DECODE_ITEM_START_VALID = 1
 # lsm_decode_tuning.flags / lsm_block_params.flags: take the workspace pool (explicit opt-in)
 DECODE_HUGE_POOL = 4
 ENCODE_HUGE_POOL = 1
+ENCODE_RUN_PLAN = 2
 # Mean block size (bytes) from which the wrappers hand the workspace pool for
 # blocks spread over the GPU (blocks > 72 KiB decode, > 96 KiB images encode).
 HUGE_AUTO_MEAN = 32 << 10
@@ -395,7 +396,7 @@ class Encoder:
         self.ws = None
 
     def encode(self, items, starts, n_blocks, restart_interval=16, hash_ratio=0.0, block_type=BLOCK_DATA,
-               out=None, stream=None, pool=None, workspace_bytes=None):
+               out=None, stream=None, pool=None, workspace_bytes=None, run_plan=False):
         """items: dict of cuda tensors keys(u8, padded) key_off(i64 n+1) vals(u8, padded) val_off(i64 n+1)
         seqno(i64) vtype(u8) [handle_off(i64) handle_size(i32)]; starts: int32 cuda [n_blocks+1].
         key_off / val_off as int32 tensors (arenas < 4 GiB): lsm_encode_blocks32 (u32 offsets).
@@ -425,6 +426,8 @@ class Encoder:
             pool = bound >= HUGE_AUTO_MEAN * max(n_blocks, 1)
         if pool:  # the pool is an explicit opt-in (LSM_ENCODE_HUGE_POOL), never implied by the size
             params.flags = ENCODE_HUGE_POOL
+        if run_plan:  # LSM_ENCODE_RUN_PLAN (the library also takes it by itself for long blocks)
+            params.flags |= ENCODE_RUN_PLAN
         need = (lib().lsm_encode_workspace_size_ex(n_items, n_blocks, bound) if pool
                 else lib().lsm_encode_workspace_size(n_items, n_blocks))
         if workspace_bytes is not None:

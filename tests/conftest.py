@@ -67,3 +67,21 @@ def gpu():
     import lsmgpu
     lsmgpu.lib()
     return lsmgpu
+
+
+@pytest.fixture(scope="session")
+def diag_lib(gpu):
+    """The diagnostic build (lsm-tree_amd/.variants/libdiag.so, -DLSM_DIAG: the flag bits
+    that force the guard paths), loaded beside the product library with the same ctypes
+    signatures; tests swap it in for one call."""
+    from pathlib import Path
+    path = Path(gpu.HERE) / ".variants" / "libdiag.so"
+    if not path.exists():
+        pytest.fail(f"{path} not built (__graft_entry__.build() builds the diagnostic variant)")
+    saved, saved_path = gpu._lib, gpu.LIB_PATH
+    gpu._lib, gpu.LIB_PATH = None, path
+    try:
+        lib = gpu.lib()
+    finally:
+        gpu._lib, gpu.LIB_PATH = saved, saved_path
+    return lib

@@ -115,7 +115,7 @@ def test_bad_args_rejected_without_device(L):
         p = L.LsmBlockParams(16, 0, 0, bits, 0.0)
         assert lib.lsm_encode_blocks(C.byref(it), C.c_void_p(8), 1, C.byref(p), C.c_void_p(16), 100, C.c_void_p(24),
                                      C.c_void_p(32), C.c_void_p(48), 1 << 20, None) == 10
-    for flags in (2, 4, 0x100, 1 << 31):  # lsm_block_params.flags: only LSM_ENCODE_HUGE_POOL
+    for flags in (4, 8, 0x100, 1 << 31):  # lsm_block_params.flags: only LSM_ENCODE_HUGE_POOL | LSM_ENCODE_RUN_PLAN
         p = L.LsmBlockParams(16, 0, 0, 0, 0.0, flags)
         assert lib.lsm_encode_blocks(C.byref(it), C.c_void_p(8), 1, C.byref(p), C.c_void_p(16), 100, C.c_void_p(24),
                                      C.c_void_p(32), C.c_void_p(48), 1 << 20, None) == 10

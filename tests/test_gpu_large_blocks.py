@@ -382,21 +382,6 @@ DIAG_STREAM_GIVE_UP = 0x4000
 DIAG_NO_CHAIN_FALLBACK = 0x8000
 
 
-@pytest.fixture(scope="module")
-def diag_lib(gpu):
-    from pathlib import Path
-    path = Path(gpu.HERE) / ".variants" / "libdiag.so"
-    if not path.exists():
-        pytest.fail(f"{path} not built (__graft_entry__.build() builds the diagnostic variant)")
-    saved, saved_path = gpu._lib, gpu.LIB_PATH
-    gpu._lib, gpu.LIB_PATH = None, path
-    try:
-        lib = gpu.lib()  # the diagnostic library with the same ctypes signatures
-    finally:
-        gpu._lib, gpu.LIB_PATH = saved, saved_path
-    return lib
-
-
 def test_streamed_chain_give_up(gpu, diag_lib):
     """The streamed huge-block chains give a block up after 5 ms without progress
     (other streams holding the CUs); the diagnostic flag makes every chain wave
