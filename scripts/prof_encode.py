@@ -32,6 +32,8 @@ def main():
     else:
         items, starts, n_items = bench.make_workload(torch, lsmgpu, nb, items_per_block=56, key_len=40, val_len=256)
     off_bytes = 8 if args.off64 else 4
+    # (the arena sizes from the u64 offsets: a u32 offset past 2^31 reads back negative)
+    key_val = int(items["key_off"][n_items].item()) + int(items["val_off"][n_items].item())
     if not args.off64:
         items = dict(items, key_off=items["key_off"].to(torch.int32), val_off=items["val_off"].to(torch.int32))
     if args.diag_bits:
@@ -90,7 +92,6 @@ def main():
             torch.cuda.synchronize()
             lsmgpu.LsmBlockParams = orig
             print(f"  ablate {name:20s} {e0.elapsed_time(e1) / args.reps:.3f} ms", flush=True)
-    key_val = int(items["key_off"][n_items].item()) + int(items["val_off"][n_items].item())
     alg = key_val + n_items * (bench.ENC_IN_PER_ITEM - 2 * (8 - off_bytes)) + 4 * (nb + 1) + total + 8 * (nb + 1) + 4 * nb
     print(f"encode {args.workload} (u{8 * off_bytes} offsets): {nb} blocks {n_items} items {total} bytes  {ms:.3f} ms  "
           f"{total / ms / 1e6:.1f} GB/s written  alg_bytes {alg}", flush=True)
