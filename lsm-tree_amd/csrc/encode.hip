@@ -894,50 +894,16 @@ static_assert(kPlanBlocks <= 255, "thread nb loads the run's end: nb < 256 threa
 constexpr uint32_t kPlanPer = 2;          // consecutive items per thread
 constexpr uint32_t kPlanChunk = 256 * kPlanPer;      // items per chunk
 
-// 16 bytes at p (global, any alignment): two aligned 16-B loads and a funnel
-// shift (reads up to 31 bytes past p; the arenas are padded).
+// 16 bytes at p (global, any alignment): one unaligned 16-B load (the arenas are
+// padded).  Two aligned loads and a funnel shift issued twice the loads and ~10 VALU
+// more per window, and held 20 more VGPRs in the plan kernel (113 -> 93, u32 offsets):
+// 1-1.5 % faster encodes (profiles/r06_experiments.txt, ab6k).
 __device__ __forceinline__ Win16 gwin16(const uint8_t* p) {
-  const uint64_t a = (uint64_t)(uintptr_t)p;
-  const u32x4* w = reinterpret_cast<const u32x4*>(a & ~15ULL);
-  const u32x4 x = w[0], y = w[1];
-  uint64_t w0 = (uint64_t)x.x | ((uint64_t)x.y << 32), w1 = (uint64_t)x.z | ((uint64_t)x.w << 32);
-  uint64_t w2 = (uint64_t)y.x | ((uint64_t)y.y << 32);
-  const uint64_t w3 = (uint64_t)y.z | ((uint64_t)y.w << 32);
-  const uint32_t s = (uint32_t)(a & 15);
-  if (s & 8) {
-    w0 = w1;
-    w1 = w2;
-    w2 = w3;
-  }
-  const uint32_t sh = (s & 7) * 8;
   Win16 r;
-  r.lo = sh ? (w0 >> sh) | (w1 << (64 - sh)) : w0;
-  r.hi = sh ? (w1 >> sh) | (w2 << (64 - sh)) : w1;
+  __builtin_memcpy(&r, p, 16);
   return r;
 }
-
-// gwin16 that skips the second 16-B load when p is 16-byte aligned
-__device__ __forceinline__ Win16 gwin16a(const uint8_t* p) {
-  const uint64_t a = (uint64_t)(uintptr_t)p;
-  const u32x4* w = reinterpret_cast<const u32x4*>(a & ~15ULL);
-  const uint32_t s = (uint32_t)(a & 15);
-  const u32x4 x = w[0];
-  u32x4 y = {0, 0, 0, 0};
-  if (s) y = w[1];
-  uint64_t w0 = (uint64_t)x.x | ((uint64_t)x.y << 32), w1 = (uint64_t)x.z | ((uint64_t)x.w << 32);
-  uint64_t w2 = (uint64_t)y.x | ((uint64_t)y.y << 32);
-  const uint64_t w3 = (uint64_t)y.z | ((uint64_t)y.w << 32);
-  if (s & 8) {
-    w0 = w1;
-    w1 = w2;
-    w2 = w3;
-  }
-  const uint32_t sh = (s & 7) * 8;
-  Win16 r;
-  r.lo = sh ? (w0 >> sh) | (w1 << (64 - sh)) : w0;
-  r.hi = sh ? (w1 >> sh) | (w2 << (64 - sh)) : w1;
-  return r;
-}
+__device__ __forceinline__ Win16 gwin16a(const uint8_t* p) { return gwin16(p); }
 
 // Shared prefix past an equal first 16 bytes: 16 bytes per step (rare: long
 // common key prefixes; kept narrow so the common path's registers stay low).

@@ -49,6 +49,11 @@ def child(reps, which):
         torch.cuda.synchronize()
         total = int(enc["block_off"][nb].item())
         bad = int((enc["status"][:nb] != 0).sum())
+        # untimed warm-up calls: without them the first shape of a child ran ~3-5 % slow
+        # (clocks / allocator still settling), which biased cross-shape comparisons
+        for _ in range(5):
+            enc_ctx.encode(items, starts, nb, hash_ratio=hr, out=enc)
+        torch.cuda.synchronize()
         e0, e1 = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
         e0.record()
         for _ in range(reps):
