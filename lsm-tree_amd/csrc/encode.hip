@@ -2327,77 +2327,89 @@ __global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(4))) 
     // the merge (or the short path), then the header.  Lane q of the quad
     // holds accumulator pair q; the chain is one instruction stream for all
     // the group's blocks.
-    if (wave == (iter & (kGWaves - 1)) && !(kDiagBuild && (P.diag & 10))) {
-      const uint32_t jb = (uint32_t)lane >> 2;
-      const int q = lane & 3;
-      const bool in = jb < k;
-      const GBlk& B = L.blk[in ? jb : 0];
-      const uint32_t p0 = B.img + kHdrLen, plen = B.plen;
-      uint64_t lo = 0, hi = 0;
-      if (in && plen > 240) {
-        uint64_t a0 = q == 0 ? (uint64_t)P32_3 : q == 1 ? P64_2 : q == 2 ? P64_4 : P64_5;
-        uint64_t a1 = q == 0 ? P64_1 : q == 1 ? P64_3 : q == 2 ? (uint64_t)P32_2 : (uint64_t)P32_1;
-        const uint64_t scr0 = L.secret.acc[16 + 2 * q], scr1 = L.secret.acc[16 + 2 * q + 1];
-        const uint64_t* cb = contrib + 8 * B.u0 + 2 * q;
-        // four KiB blocks' contributions per batch, read without branches (past
-        // the block they read other contributions in L.uni, unused)
-        for (uint32_t n0 = 0; n0 < B.nbk; n0 += 4) {
-          uint64_t c0[4], c1[4];
+    // The copy-out runs in two parts: the waves other than the chain wave store every whole
+    // 16-B piece of the span that holds no header byte while the chain wave computes the
+    // checksums and headers; after the barrier the header pieces (three per block) and the
+    // partial pieces at both ends follow.  (Before, the whole copy-out waited for the chain.)
+    const uint32_t cw = iter & (kGWaves - 1);  // the chain wave of this group
+    const uint32_t total = (uint32_t)(rl64(r_off, r0 + k) - obase);
+    const uint32_t end = (kDiagBuild && (P.diag & 4)) ? pad : pad + total;
+    const uint32_t c0 = (pad + 15) >> 4, c1 = end >> 4;  // the whole 16-B pieces [c0, c1)
+    const u32x4* const csrc = reinterpret_cast<const u32x4*>(L.img);
+    u32x4* const cdst = reinterpret_cast<u32x4*>(dabs & ~15ULL);
+    // the chain wave's header pieces, taken before the barrier (the next group's block
+    // table overwrites L.blk before that group's first barrier)
+    const uint32_t hpc = (wave == cw && (uint32_t)lane < 3 * k) ? (L.blk[lane / 3].img >> 4) + lane % 3 : ~0u;
+    if (wave == cw) {
+      if (!(kDiagBuild && (P.diag & 10))) {
+        const uint32_t jb = (uint32_t)lane >> 2;
+        const int q = lane & 3;
+        const bool in = jb < k;
+        const GBlk& B = L.blk[in ? jb : 0];
+        const uint32_t p0 = B.img + kHdrLen, plen = B.plen;
+        uint64_t lo = 0, hi = 0;
+        if (in && plen > 240) {
+          uint64_t a0 = q == 0 ? (uint64_t)P32_3 : q == 1 ? P64_2 : q == 2 ? P64_4 : P64_5;
+          uint64_t a1 = q == 0 ? P64_1 : q == 1 ? P64_3 : q == 2 ? (uint64_t)P32_2 : (uint64_t)P32_1;
+          const uint64_t scr0 = L.secret.acc[16 + 2 * q], scr1 = L.secret.acc[16 + 2 * q + 1];
+          const uint64_t* cb = contrib + 8 * B.u0 + 2 * q;
+          // four KiB blocks' contributions per batch, read without branches (past
+          // the block they read other contributions in L.uni, unused)
+          for (uint32_t n0 = 0; n0 < B.nbk; n0 += 4) {
+            uint64_t c0[4], c1[4];
 #pragma unroll
-          for (uint32_t t = 0; t < 4; ++t) {
-            c0[t] = cb[8 * (n0 + t)];
-            c1[t] = cb[8 * (n0 + t) + 1];
-          }
+            for (uint32_t t = 0; t < 4; ++t) {
+              c0[t] = cb[8 * (n0 + t)];
+              c1[t] = cb[8 * (n0 + t) + 1];
+            }
 #pragma unroll
-          for (uint32_t t = 0; t < 4; ++t) {
-            if (n0 + t < B.nbk) {
-              a0 = xxh3_scr(a0, c0[t], scr0);
-              a1 = xxh3_scr(a1, c1[t], scr1);
+            for (uint32_t t = 0; t < 4; ++t) {
+              if (n0 + t < B.nbk) {
+                a0 = xxh3_scr(a0, c0[t], scr0);
+                a1 = xxh3_scr(a1, c1[t], scr1);
+              }
             }
           }
+          a0 += cb[8 * B.nbk];
+          a1 += cb[8 * B.nbk + 1];
+          lo = mul_fold64(a0 ^ L.secret.mlo[2 * q], a1 ^ L.secret.mlo[2 * q + 1]);
+          hi = mul_fold64(a0 ^ L.secret.mhi[2 * q], a1 ^ L.secret.mhi[2 * q + 1]);
         }
-        a0 += cb[8 * B.nbk];
-        a1 += cb[8 * B.nbk + 1];
-        lo = mul_fold64(a0 ^ L.secret.mlo[2 * q], a1 ^ L.secret.mlo[2 * q + 1]);
-        hi = mul_fold64(a0 ^ L.secret.mhi[2 * q], a1 ^ L.secret.mhi[2 * q + 1]);
+        lo = quad_sum64(lo);  // (every lane: DPP reads of inactive lanes are undefined)
+        hi = quad_sum64(hi);
+        if (in) {
+          if (plen > 240) {
+            lo = xxh3_avalanche((uint64_t)plen * P64_1 + lo);
+            hi = xxh3_avalanche(~((uint64_t)plen * P64_2) + hi);
+          } else {
+            xxh3_128_short(plen, BaseReader8{L.img, p0}, BaseReader64{L.img, p0}, lo, hi);
+          }
+          write_header_quad(L.img, B.img, P.type, lo, hi, plen, q);
+          if (q == 0) P.status[G.b + jb] = ST_OK;
+        }
       }
-      lo = quad_sum64(lo);  // (every lane: DPP reads of inactive lanes are undefined)
-      hi = quad_sum64(hi);
-      if (in) {
-        if (plen > 240) {
-          lo = xxh3_avalanche((uint64_t)plen * P64_1 + lo);
-          hi = xxh3_avalanche(~((uint64_t)plen * P64_2) + hi);
-        } else {
-          xxh3_128_short(plen, BaseReader8{L.img, p0}, BaseReader64{L.img, p0}, lo, hi);
-        }
-        write_header_quad(L.img, B.img, P.type, lo, hi, plen, q);
-        if (q == 0) P.status[G.b + jb] = ST_OK;
+    } else {  // (no vmcnt wait here: the next group's DMA may still be landing)
+      const uint32_t t3 = ((wave + kGWaves - cw - 1) & (kGWaves - 1)) * kWave + (uint32_t)lane;  // 0 .. 191
+      constexpr uint32_t kT3 = (kGWaves - 1) * kWave;
+      // block j's header pieces are [hc_j, hc_j + 3) (33 bytes from any offset); its
+      // header-free pieces run from hc_j + 3 to the next block's hc
+      uint32_t hc = __builtin_amdgcn_readfirstlane(L.blk[0].img) >> 4;
+      for (uint32_t jb = 0; jb < k; ++jb) {
+        const uint32_t hn = jb + 1 < k ? __builtin_amdgcn_readfirstlane(L.blk[jb + 1].img) >> 4 : c1;
+        for (uint32_t c = max(hc + 3, c0) + t3; c < min(hn, c1); c += kT3)
+          *(__attribute__((address_space(1))) u32x4*)(cdst + c) = csrc[c];  // (plain stores, r06)
+        hc = hn;
       }
     }
     group_barrier_lds();
     ENC_PHASE(6);
     __builtin_amdgcn_s_waitcnt(0x0070);  // vmcnt(0): the next group's DMA pieces and item fields
     ENC_PHASE(7);
-    // ---- copy-out: the group's span [block_off[b], block_off[b + k]) in 16 B pieces
+    // ---- copy-out, part 2: the header pieces and the partial pieces at both ends
     {
-      const uint32_t total = (uint32_t)(rl64(r_off, r0 + k) - obase);
-      uint8_t* gdst = reinterpret_cast<uint8_t*>(dabs & ~15ULL);
-      const uint32_t end = (kDiagBuild && (P.diag & 4)) ? pad : pad + total;
-      const uint32_t c0 = (pad + 15) >> 4, c1 = end >> 4;  // the whole 16-B pieces [c0, c1)
-      const u32x4* src = reinterpret_cast<const u32x4*>(L.img);
-      u32x4* dst = reinterpret_cast<u32x4*>(gdst);
-      for (uint32_t c = c0 + tid; c < c1; c += 4 * kGThreads) {  // four pieces in flight per thread
-        u32x4 v[4];
-#pragma unroll
-        for (uint32_t t = 0; t < 4; ++t)
-          if (c + t * kGThreads < c1) v[t] = src[c + t * kGThreads];
-#pragma unroll
-        for (uint32_t t = 0; t < 4; ++t)
-          if (c + t * kGThreads < c1)  // (plain stores: 2.3-2.5 % faster than non-temporal ones, r06)
-            *(__attribute__((address_space(1))) u32x4*)(dst + c + t * kGThreads) = v[t];
-      }
-      // the partial pieces at both ends (shared with the neighbouring groups' bytes)
-      auto* gb = (__attribute__((address_space(1))) uint8_t*)gdst;
+      if (hpc >= c0 && hpc < c1) *(__attribute__((address_space(1))) u32x4*)(cdst + hpc) = csrc[hpc];
+      // (shared with the neighbouring groups' bytes)
+      auto* gb = (__attribute__((address_space(1))) uint8_t*)cdst;
       if (tid == 0)
         for (uint32_t x = pad; x < min(16 * c0, end); ++x) gb[x] = L.img[x];
       if (tid == kWave && c1 >= c0)
