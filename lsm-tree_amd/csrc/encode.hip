@@ -1416,7 +1416,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(4))) void e
 //          into 1 KiB units (XXH3 per-KiB contributions, then one short
 //          serial scramble chain per block)
 //   header wave 0, lane per block: header fields + 29-byte checksum
-//   out    one contiguous 16 B/lane copy of the group's span
+//   out    16 B/lane copy of the group's span: the header-free pieces by three waves
+//          while the fourth runs the chains, then the header pieces
 // Blocks that do not fit are written by the list / HBM kernels.
 struct GBlk {
   uint32_t it0, n;         // first item (group-relative), items
