@@ -70,6 +70,28 @@ def test_encode_graph_replay(gpu, batch, pool):
         assert out["buf"].cpu().numpy()[:int(off[-1])].tobytes() == ref_buf.tobytes()
 
 
+@pytest.mark.parametrize("sizes", [[52] * 300, [205] * 120], ids=["4KiB-asked", "16KiB-auto"])
+def test_encode_graph_replay_run_plan(gpu, sizes):
+    """The run-level plan in the group kernel (LSM_ENCODE_RUN_PLAN, or by itself at >= 128
+    items per block): its look-back words are cleared by a kernel node on every replay."""
+    import torch
+    items, starts, d_items, d_starts = _items(gpu, sizes, seed=29)
+    nb = len(sizes)
+    ref_buf, ref_off = pyoracle.encode_blocks(items, starts)
+    enc = gpu.Encoder()
+    out = enc.encode(d_items, d_starts, nb, pool=False, run_plan=True)
+    graph = _capture(lambda: enc.encode(d_items, d_starts, nb, out=out, pool=False, run_plan=True))
+    for _ in range(3):
+        out["buf"].zero_()
+        out["status"].fill_(-1)
+        out["block_off"].fill_(-1)
+        graph.replay()
+        torch.cuda.synchronize()
+        off = out["block_off"].cpu().numpy().view(np.uint64)
+        assert (out["status"].cpu().numpy()[:nb] == 0).all() and (off == ref_off).all()
+        assert out["buf"].cpu().numpy()[:int(off[-1])].tobytes() == ref_buf.tobytes()
+
+
 @pytest.mark.parametrize("pool", [True, False])
 @pytest.mark.parametrize("batch", sorted(BATCHES))
 def test_decode_graph_replay(gpu, batch, pool):

@@ -88,3 +88,22 @@ def test_encoder_passes_exact_workspace(fake):
     assert ws[1] == fake.real.lsm_encode_workspace_size(n_items, n_blocks) < ws[0]
     flags = [args[3]._obj.flags for name, args in fake.calls if name == "lsm_encode_blocks"]
     assert flags == [lsmgpu.ENCODE_HUGE_POOL, 0]
+
+
+def test_encoder_run_plan_flag(fake):
+    """run_plan=True asks for the run-level plan (LSM_ENCODE_RUN_PLAN), alone or with the pool."""
+    n_items, n_blocks = 64, 4
+    items = {"keys": torch.zeros(64 * 16 + 64, dtype=torch.uint8),
+             "key_off": torch.arange(n_items + 1, dtype=torch.int32) * 16,
+             "vals": torch.zeros(64 * 64 + 64, dtype=torch.uint8),
+             "val_off": torch.arange(n_items + 1, dtype=torch.int32) * 64,
+             "seqno": torch.zeros(n_items, dtype=torch.int64), "vtype": torch.zeros(n_items, dtype=torch.uint8)}
+    starts = torch.arange(0, n_items + 1, 16, dtype=torch.int32)
+    e = lsmgpu.Encoder("cpu")
+    e.encode(items, starts, n_blocks, pool=False, run_plan=True)
+    e.encode(items, starts, n_blocks, pool=True, run_plan=True)
+    e.encode(items, starts, n_blocks, pool=False)
+    calls = [(name, args) for name, args in fake.calls if name.startswith("lsm_encode_blocks")]
+    assert [name for name, _ in calls] == ["lsm_encode_blocks32"] * 3  # (int32 offsets: the u32 entry)
+    assert [args[3]._obj.flags for _, args in calls] == [lsmgpu.ENCODE_RUN_PLAN,
+                                                         lsmgpu.ENCODE_HUGE_POOL | lsmgpu.ENCODE_RUN_PLAN, 0]
