@@ -1426,16 +1426,15 @@ struct GBlk {
   uint32_t step, hash_w;   // binary-index step, hash-index buckets
   uint32_t hash_base, u0;  // first vote pair, first hash unit
   uint32_t nbk, spare;     // full KiB units of the payload
-  uint64_t ck_lo, ck_hi;   // payload xxh3_128
 };
-static_assert(sizeof(GBlk) == 64, "GBlk");
+static_assert(sizeof(GBlk) == 48, "GBlk");
 
 struct GroupLds {
   uint8_t keys[kGKeys + kGSlack];
   uint8_t vals[kGVals + kGSlack];
   uint8_t img[kGImg + kGSlack];
   uint32_t uni[kGUnion / 4];
-  GBlk blk[kGBlocks];
+  GBlk blk[2][kGBlocks];  // this group's block table and the next one's (built under the chain)
   LongSecret secret;
 };
 // (the fused kernel's run-level plan keeps its LDS over vals + img, and its per-block
@@ -2080,6 +2079,41 @@ __global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(4))) 
     return cook_item<kIndex>(r, bad);
   };
 
+  // group g's block table (lane j = block j; one wave, every lane active for the shuffles)
+  auto build_table = [&](const Grp& g, GBlk* tb) {
+    const uint32_t gr0 = g.b - b_begin, gk = g.k;
+    const uint32_t gi0 = rl32(r_start, gr0);
+    const uint64_t gob = rl64(r_off, gr0);
+    const uint32_t gpad = (uint32_t)(((uint64_t)(uintptr_t)P.out + gob) & 15);
+    const uint32_t rj = gr0 + lane;
+    const uint32_t st = lane_u32(r_start, rj), st1 = lane_u32(r_start, rj + 1);
+    const uint64_t of = lane_u64(r_off, rj), of1 = lane_u64(r_off, rj + 1);
+    const uint32_t recs = lane_u32(r_plan.recs, rj), bin_len = lane_u32(r_plan.bin_len, rj);
+    const uint32_t sf = lane_u32(r_plan.step_flags, rj), hw = lane_u32(r_plan.hash_w, rj);
+    const uint32_t hb = lane_u32(r_hpre, rj) - rl32(r_hpre, gr0);
+    const bool in = (uint32_t)lane < gk;
+    const uint32_t plen = in ? (uint32_t)(of1 - of) - kHdrLen : 0;
+    const uint32_t nbk = plen > 240 ? (plen - 1) / 1024 : 0;
+    const uint32_t units = plen > 240 ? nbk + 1 : 0;
+    const uint32_t u0 = wave_incl_scan_u32(units) - units;
+    if (in) {
+      GBlk B;
+      B.it0 = st - gi0;
+      B.n = st1 - st;
+      B.img = (uint32_t)(of - gob) + gpad;
+      B.plen = plen;
+      B.recs = recs;
+      B.bin_len = bin_len;
+      B.step = sf & 0xFF;
+      B.hash_w = hw;
+      B.hash_base = hb;
+      B.u0 = u0;
+      B.nbk = nbk;
+      B.spare = 0;
+      tb[lane] = B;
+    }
+  };
+
   // Software pipeline: group G's stage DMA and item fields are issued one
   // group ahead and waited for (vmcnt(0)) just before the previous group's
   // copy-out, so no group waits on HBM latency after its stores.
@@ -2093,6 +2127,7 @@ __global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(4))) 
   if (G.k) {
     issue_dma(G);
     load_items(G, raw);
+    if (wave == 0) build_table(G, L.blk[0]);  // (later tables are built under the previous chain)
   }
   __builtin_amdgcn_s_waitcnt(0x0070);
   ENC_PHASE(11);
@@ -2112,37 +2147,7 @@ __global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(4))) 
     ItemMeta m = cook(raw);
     if (Gn.k) load_items(Gn, raw);
     ENC_PHASE(9);
-    // ---- wave 0: the group's block table (lane j = group block j; shuffles with every lane active)
-    if (wave == 0) {
-      const uint32_t rj = r0 + lane;
-      const uint32_t st = lane_u32(r_start, rj), st1 = lane_u32(r_start, rj + 1);
-      const uint64_t of = lane_u64(r_off, rj), of1 = lane_u64(r_off, rj + 1);
-      const uint32_t recs = lane_u32(r_plan.recs, rj), bin_len = lane_u32(r_plan.bin_len, rj);
-      const uint32_t sf = lane_u32(r_plan.step_flags, rj), hw = lane_u32(r_plan.hash_w, rj);
-      const uint32_t hb = lane_u32(r_hpre, rj) - rl32(r_hpre, r0);
-      const bool in = (uint32_t)lane < k;
-      const uint32_t plen = in ? (uint32_t)(of1 - of) - kHdrLen : 0;
-      const uint32_t nbk = plen > 240 ? (plen - 1) / 1024 : 0;
-      const uint32_t units = plen > 240 ? nbk + 1 : 0;
-      const uint32_t u0 = wave_incl_scan_u32(units) - units;
-      if (in) {
-        GBlk B;
-        B.it0 = st - i0;
-        B.n = st1 - st;
-        B.img = (uint32_t)(of - obase) + pad;
-        B.plen = plen;
-        B.recs = recs;
-        B.bin_len = bin_len;
-        B.step = sf & 0xFF;
-        B.hash_w = hw;
-        B.hash_base = hb;
-        B.u0 = u0;
-        B.nbk = nbk;
-        B.spare = 0;
-        B.ck_lo = B.ck_hi = 0;
-        L.blk[lane] = B;
-      }
-    }
+    GBlk* const TB = L.blk[iter & 1];  // this group's block table (built one group ahead)
     // (shuffles only with every lane active: a bpermute from an inactive lane is undefined)
     const uint32_t hsum = rl32(r_hpre, r0 + k) - rl32(r_hpre, r0);
     for (uint32_t h = tid; h < hsum; h += kGThreads) {
@@ -2165,7 +2170,7 @@ __global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(4))) 
     // A fix in one must be made in both.
     if (tsh == 0) {
     if (live && !(kDiagBuild && (P.diag & 9))) {
-      const GBlk& B = L.blk[j];
+      const GBlk& B = TB[j];
       const uint32_t roff = m.e & 0x7FFFu;
       const uint32_t p0 = B.img + kHdrLen;
       uint32_t pos = p0 + roff;
@@ -2206,7 +2211,7 @@ __global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(4))) 
     }
     } else {
     if (live && !(kDiagBuild && (P.diag & 9))) {
-      const GBlk& B = L.blk[j];
+      const GBlk& B = TB[j];
       const uint32_t roff = m.e & 0x7FFFu;
       const uint32_t p0 = B.img + kHdrLen;
       uint32_t pos = p0 + roff;
@@ -2260,7 +2265,7 @@ __global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(4))) 
     // (disjoint bytes), so they go before the barrier
     auto tails = [&]() {
       for (uint32_t jb = wave; jb < (kDiagBuild && (P.diag & 8) ? 0 : k); jb += kGWaves) {
-        const GBlk& B = L.blk[jb];
+        const GBlk& B = TB[jb];
         const uint32_t p0 = B.img + kHdrLen, bin_off = B.recs + 1;
         if (lane == 0) L.img[p0 + B.recs] = kTrailerMarker;
         const uint32_t hash_off = B.hash_w ? bin_off + B.bin_len * B.step : 0;
@@ -2291,7 +2296,7 @@ __global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(4))) 
       for (uint32_t u = row; u < units; u += 4 * kGWaves) {
         uint32_t jb = 0;  // (unit starts from the run registers: no dependent LDS reads)
         for (uint32_t x = 1; x < k; ++x) jb += (rl32(r_upre, r0 + x) - ubase <= u) ? 1u : 0u;
-        const GBlk& B = L.blk[jb];
+        const GBlk& B = TB[jb];
         const uint32_t n = u - B.u0, p0 = B.img + kHdrLen;
         uint64_t c0 = 0, c1 = 0;
         if (n < B.nbk) {
@@ -2338,15 +2343,14 @@ __global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(4))) 
     const uint32_t c0 = (pad + 15) >> 4, c1 = end >> 4;  // the whole 16-B pieces [c0, c1)
     const u32x4* const csrc = reinterpret_cast<const u32x4*>(L.img);
     u32x4* const cdst = reinterpret_cast<u32x4*>(dabs & ~15ULL);
-    // the chain wave's header pieces, taken before the barrier (the next group's block
-    // table overwrites L.blk before that group's first barrier)
-    const uint32_t hpc = (wave == cw && (uint32_t)lane < 3 * k) ? (L.blk[lane / 3].img >> 4) + lane % 3 : ~0u;
+    // the chain wave's header pieces
+    const uint32_t hpc = (wave == cw && (uint32_t)lane < 3 * k) ? (TB[lane / 3].img >> 4) + lane % 3 : ~0u;
     if (wave == cw) {
       if (!(kDiagBuild && (P.diag & 10))) {
         const uint32_t jb = (uint32_t)lane >> 2;
         const int q = lane & 3;
         const bool in = jb < k;
-        const GBlk& B = L.blk[in ? jb : 0];
+        const GBlk& B = TB[in ? jb : 0];
         const uint32_t p0 = B.img + kHdrLen, plen = B.plen;
         uint64_t lo = 0, hi = 0;
         if (in && plen > 240) {
@@ -2390,13 +2394,15 @@ __global__ __launch_bounds__(kGThreads) __attribute__((amdgpu_waves_per_eu(4))) 
         }
       }
     } else {  // (no vmcnt wait here: the next group's DMA may still be landing)
+      // the next group's block table, into the other buffer, by the wave after the chain wave
+      if (Gn.k && wave == ((cw + 1) & (kGWaves - 1))) build_table(Gn, L.blk[(iter + 1) & 1]);
       const uint32_t t3 = ((wave + kGWaves - cw - 1) & (kGWaves - 1)) * kWave + (uint32_t)lane;  // 0 .. 191
       constexpr uint32_t kT3 = (kGWaves - 1) * kWave;
       // block j's header pieces are [hc_j, hc_j + 3) (33 bytes from any offset); its
       // header-free pieces run from hc_j + 3 to the next block's hc
-      uint32_t hc = __builtin_amdgcn_readfirstlane(L.blk[0].img) >> 4;
+      uint32_t hc = __builtin_amdgcn_readfirstlane(TB[0].img) >> 4;
       for (uint32_t jb = 0; jb < k; ++jb) {
-        const uint32_t hn = jb + 1 < k ? __builtin_amdgcn_readfirstlane(L.blk[jb + 1].img) >> 4 : c1;
+        const uint32_t hn = jb + 1 < k ? __builtin_amdgcn_readfirstlane(TB[jb + 1].img) >> 4 : c1;
         for (uint32_t c = max(hc + 3, c0) + t3; c < min(hn, c1); c += kT3)
           *(__attribute__((address_space(1))) u32x4*)(cdst + c) = csrc[c];  // (plain stores, r06)
         hc = hn;
