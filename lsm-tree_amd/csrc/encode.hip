@@ -847,14 +847,8 @@ constexpr uint32_t kErecHead = 0x8000u;
 // Group write kernel (E2) budget, see encode_group_kernel.
 constexpr uint32_t kGWaves = 4, kGThreads = kGWaves * kWave;
 constexpr uint32_t kGRun = 32;          // blocks per workgroup (<= 63: one lane each)
-#ifndef LSM_EXP_GRUNF
-#define LSM_EXP_GRUNF 32
-#endif
-constexpr uint32_t kGRunFused = LSM_EXP_GRUNF;  // the same with the fused run-level plan
-#ifndef LSM_EXP_FUSED_AUTO
-#define LSM_EXP_FUSED_AUTO 128
-#endif
-constexpr uint64_t kFusedAutoItems = LSM_EXP_FUSED_AUTO;  // items per block from which the fused plan is taken
+constexpr uint32_t kGRunFused = 32;  // the same with the fused run-level plan (48 / 63: r06_experiments ab6h)
+constexpr uint64_t kFusedAutoItems = 128;  // items per block from which the fused plan is taken
 static_assert(kGRunFused <= 63, "one lane per block and one for the run's end");
 constexpr uint32_t kGBlocks = 16;    // blocks per group
 constexpr uint32_t kGItems = kGThreads;        // items per group (one thread each)
