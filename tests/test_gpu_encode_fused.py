@@ -132,3 +132,37 @@ def test_fused_give_up(gpu, diag_lib):
     # the same library without the flag: as the release
     buf2, off2, st2, _ = _encode(gpu, items, starts, True, lib=diag_lib)
     assert (st2 == 0).all() and (off2 == ref_off).all() and buf2[:int(off2[-1])].tobytes() == ref_buf.tobytes()
+
+
+def test_fused_concurrent_streams(gpu):
+    """Two batches encoded with the run-level plan on two streams at once (each call its own
+    workspace and look-back words): both bit-exact."""
+    import torch
+    a_items = counter_items(205 * 300, seed=31)
+    b_items = random_sorted_items(9000, seed=32, vmax=120)
+    a_starts = np.arange(0, 205 * 300 + 1, 205, dtype=np.uint32)
+    rng = random.Random(5)
+    b_starts = [0]
+    while b_starts[-1] < b_items.n:
+        b_starts.append(min(b_items.n, b_starts[-1] + rng.randint(1, 120)))
+    b_starts = np.array(b_starts, np.uint32)
+    outs = []
+    streams = [torch.cuda.Stream(), torch.cuda.Stream()]
+    encs = [gpu.Encoder(), gpu.Encoder()]
+    jobs = [(a_items, a_starts), (b_items, b_starts)]
+    dev = []
+    for items, starts in jobs:
+        d = gpu.items_to_device(items, off32=True)
+        ds = torch.from_numpy(starts.astype(np.int32)).cuda()
+        dev.append((d, ds, len(starts) - 1))
+    torch.cuda.synchronize()
+    for (d, ds, nb), s, e in zip(dev, streams, encs):
+        with torch.cuda.stream(s):
+            outs.append(e.encode(d, ds, nb, pool=False, run_plan=True, stream=s))
+    torch.cuda.synchronize()
+    for (items, starts), out in zip(jobs, outs):
+        nb = len(starts) - 1
+        ref_buf, ref_off = pyoracle.encode_blocks(items, starts)
+        off = out["block_off"].cpu().numpy().view(np.uint64)
+        assert (out["status"].cpu().numpy()[:nb] == 0).all() and (off == ref_off).all()
+        assert out["buf"].cpu().numpy()[:int(off[-1])].tobytes() == ref_buf.tobytes()
